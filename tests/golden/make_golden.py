@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/ from the compiled reference (survey container only).
+
+Builds oracle/_ref/librs_ref.so + gen_golden from /root/reference (oracle/Makefile, sources are
+compiled where they lie), runs every case below through the reference's public API
+(rs_generate_repair_symbols / rs_restore_symbols) and stores the outputs:
+  * outputs <= 256 KiB  -> tests/golden/<name>.bin (raw bytes)
+  * larger outputs      -> sha256 only
+plus tests/golden/manifest.json describing inputs (portable generator, see tests/_util.py).
+
+Erasure patterns are written out explicitly in the manifest; "bench" = t = r erasures of
+information symbols at i * (k // r).
+"""
+import hashlib
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+ORACLE = os.path.join(REPO, "oracle")
+SEED = 0x5EED
+INLINE_LIMIT = 256 * 1024
+
+
+def bench_pattern(k, r):
+    step = k // r
+    return [i * step for i in range(r)]
+
+
+def rand_pattern(k, r, t, seed, info_only=False):
+    rng = random.Random(seed)
+    pool = list(range(k if info_only else k + r))
+    return sorted(rng.sample(pool, t))
+
+
+def cases():
+    c = []
+    add = lambda name, op, k, r, S, n, t=0, er=(): c.append(
+        dict(name=name, op=op, k=k, r=r, S=S, n=n, seed=SEED, t=t, erased=list(er)))
+    # config 1 (k=4, r=2, 256 B) -- full vectors
+    add("c1_enc", "encode", 4, 2, 256, 1)
+    add("c1_dec_info_rep", "decode", 4, 2, 256, 1, 2, [1, 4])
+    add("c1_dec_info2", "decode", 4, 2, 256, 1, 2, [0, 1])
+    add("c1_dec_t1", "decode", 4, 2, 256, 1, 1, [2])
+    add("c1_dec_toomany", "decode", 4, 2, 256, 1, 3, [0, 1, 2])
+    add("kat_iota", "encode_iota", 4, 2, 8, 1)
+    # config 2 (k=10, r=4, 4 KiB)
+    add("c2_enc", "encode", 10, 4, 4096, 2)
+    add("c2_dec_bench", "decode", 10, 4, 4096, 2, 4, bench_pattern(10, 4))
+    add("c2_dec_mixed", "decode", 10, 4, 4096, 1, 4, [3, 7, 10, 13])
+    add("c2_dec_t3", "decode", 10, 4, 4096, 1, 3, [1, 5, 11])
+    # config 3 shape (k=128, r=32) on short symbols; full 64 KiB symbols by hash
+    add("c3_enc", "encode", 128, 32, 512, 2)
+    add("c3_dec_bench", "decode", 128, 32, 512, 2, 32, bench_pattern(128, 32))
+    add("c3_dec_rand17", "decode", 128, 32, 512, 1, 17, rand_pattern(128, 32, 17, 1))
+    add("c3_dec_t0", "decode", 128, 32, 512, 1, 0, [])
+    add("c3_dec_noncw_bench", "decode_noncw", 128, 32, 512, 1, 32, bench_pattern(128, 32))
+    add("c3_dec_noncw_rand", "decode_noncw", 128, 32, 512, 1, 20, rand_pattern(128, 32, 20, 2))
+    add("c3_enc_64k", "encode", 128, 32, 65536, 1)
+    add("c3_dec_bench_64k", "decode", 128, 32, 65536, 1, 32, bench_pattern(128, 32))
+    # config 5 shape (k=4096, r=1024), m = 16
+    add("c5_enc", "encode", 4096, 1024, 64, 1)
+    add("c5_dec_bench", "decode", 4096, 1024, 64, 1, 1024, bench_pattern(4096, 1024))
+    add("c5_dec_rand", "decode", 4096, 1024, 64, 1, 700, rand_pattern(4096, 1024, 700, 3))
+    # example.c shape: 10-byte symbols (5 words, not a multiple of 16 B)
+    add("ex_enc", "encode", 100, 10, 10, 1)
+    add("ex_dec", "decode", 100, 10, 10, 1, 10, rand_pattern(100, 10, 10, 4))
+    # coding matrices via unit vectors (word i of info i = 1)
+    add("gmat_4_2", "gmatrix", 4, 2, 8, 1)
+    add("gmat_10_4", "gmatrix", 10, 4, 20, 1)
+    add("gmat_128_32", "gmatrix", 128, 32, 256, 1)
+    add("gmat_4096_1024", "gmatrix", 4096, 1024, 8192, 1)
+    add("dmat_128_32_bench", "dmatrix", 128, 32, 320, 1, 32, bench_pattern(128, 32))
+    add("dmat_128_32_rand", "dmatrix", 128, 32, 320, 1, 25, rand_pattern(128, 32, 25, 5))
+    # edges
+    add("edge_r0", "encode", 5, 0, 16, 1)
+    add("edge_k0", "encode", 0, 4, 16, 1)
+    add("edge_k1r1", "encode", 1, 1, 2, 1)
+    add("edge_k1r1_dec", "decode", 1, 1, 2, 1, 1, [0])
+    add("edge_repair_only", "decode", 16, 8, 64, 1, 8, list(range(16, 24)))
+    add("large_n_enc", "encode", 60000, 16, 4, 1)
+    add("large_n_dec", "decode", 60000, 16, 4, 1, 16, rand_pattern(60000, 16, 16, 6))
+    add("max_n_enc", "encode", 65519, 16, 2, 1)
+    add("wide_r_enc", "encode", 2000, 2000, 4, 1)
+    add("wide_r_dec", "decode", 2000, 2000, 4, 1, 2000, rand_pattern(2000, 2000, 2000, 7))
+    add("m4_k7r8_enc", "encode", 7, 8, 32, 3)
+    add("m8_k200r55_dec", "decode", 200, 55, 32, 2, 40, rand_pattern(200, 55, 40, 8))
+    return c
+
+
+def main():
+    subprocess.check_call(["make", "-s", "-C", ORACLE, "ref"])
+    gen = os.path.join(ORACLE, "_ref", "gen_golden")
+    cs = cases()
+    with tempfile.TemporaryDirectory() as tmp:
+        spec = os.path.join(tmp, "spec.txt")
+        with open(spec, "w") as f:
+            for c in cs:
+                er = ",".join(map(str, c["erased"])) or "-"
+                f.write(f"{c['name']} {c['op']} {c['k']} {c['r']} {c['S']} {c['n']} {c['seed']} {c['t']} {er}\n")
+        out = subprocess.check_output([gen, spec, tmp], text=True)
+        rcs = dict(line.split() for line in out.strip().splitlines())
+        for c in cs:
+            raw = open(os.path.join(tmp, c["name"] + ".bin"), "rb").read()
+            c["rc"] = int(rcs[c["name"]])
+            c["nbytes"] = len(raw)
+            c["sha256"] = hashlib.sha256(raw).hexdigest()
+            dst = os.path.join(HERE, c["name"] + ".bin")
+            if len(raw) <= INLINE_LIMIT:
+                open(dst, "wb").write(raw)
+                c["file"] = c["name"] + ".bin"
+            elif os.path.exists(dst):
+                os.remove(dst)
+    meta = dict(generator="oracle/gen_golden.c against oracle/_ref/librs_ref.so "
+                          "(reference src/rs + src/memory, -O3 -DNDEBUG)",
+                input="tests/_util.py:gen_info (counter-based splitmix64)",
+                cases=cs)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print(f"wrote {len(cs)} cases")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
