@@ -1,0 +1,78 @@
+/*
+ * rs_amd/rsg.h -- batched, device-resident Reed-Solomon engine API (librs_amd.so).
+ *
+ * The per-call drop-in API (rs/reed_solomon.h) codes one stripe held in host memory. This API codes
+ * many stripes that already live in HBM: a stripe is k information + r repair symbols of
+ * `symbol_size` bytes, addressed as  base + stripe * stripe_stride + symbol * symbol_stride.
+ * It is what the reference's rs_generate_repair_symbols (src/rs/reed_solomon.c:338-441) and
+ * rs_restore_symbols (src/rs/reed_solomon.c:443-559) become when the buffers are device-resident;
+ * results are bit-identical, stripe by stripe.
+ *
+ * Plain C ABI: device pointers, sizes, `stream` is a hipStream_t (NULL = default stream).
+ * Calls only enqueue work; synchronise the stream before reading results.
+ * Alignment: base pointers, strides and symbol_size must be multiples of 8 bytes for the m<=8
+ * kernels and 4 bytes for m = 16 (symbol_size must be even in any case).
+ * Return codes are those of rs/reed_solomon.h (0, 1, RS_ERR_INVALID, RS_ERR_DEVICE, 100).
+ */
+#ifndef RS_AMD_RSG_H
+#define RS_AMD_RSG_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rsg_codec rsg_codec_t;
+
+/* Builds the (k, r) code on `device` (positions as reference cc_select_cosets) and uploads the
+ * encode matrix. */
+int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t** out);
+void rsg_codec_destroy(rsg_codec_t* c);
+/* Subfield degree m of the code (8 => GF(256) kernels, 16 => general kernels). */
+int rsg_codec_subfield(const rsg_codec_t* c);
+
+/* Options: "m8_mode" (0 register tables, 1 masked multiples), "jit" (1 = use matrix-specialised
+ * kernels compiled with hiprtc when available). Returns RS_ERR_INVALID for unknown names. */
+int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
+/* Name of the kernel the last encode/decode launched (diagnostics). */
+const char* rsg_last_kernel(const rsg_codec_t* c);
+
+/* Repair symbols of n_stripes stripes: info at d_info (k symbols per stripe), repair written to
+ * d_rep (r symbols per stripe). */
+int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stripe_stride, uint64_t info_symbol_stride,
+               void* d_rep, uint64_t rep_stripe_stride, uint64_t rep_symbol_stride, uint64_t n_stripes,
+               uint64_t symbol_size, void* stream);
+
+/* Restores, in place, the erased information symbols of n_stripes stripes of k + r symbols that share
+ * one erasure pattern (is_erased[k + r] in host memory, exactly t entries true). Erased slots are not
+ * read; erased repair slots are not written (reference src/rs/reed_solomon.c:299-336). */
+int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t n_stripes,
+               uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream);
+
+/* Synthetic inputs: fills the k information symbols of stripes [stripe0, stripe0 + n) with the
+ * counter-based generator of tests/_util.py:gen_info (symbol_size % 8 == 0). */
+int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size, uint16_t k,
+                  uint64_t stripe0, uint64_t n_stripes, uint64_t seed, void* stream);
+/* Per-stripe 64-bit fingerprint of symbols [sym0, sym0 + nsym) into d_out[n_stripes] (device). */
+int rsg_fingerprint(const void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size,
+                    uint32_t sym0, uint32_t nsym, uint64_t n_stripes, uint64_t* d_out, void* stream);
+
+/* ---- host-only helpers (no GPU needed; used by tests and integration code) ---- */
+/* Coding matrix in GF(2^16): encode when is_erased == NULL (rows = r repair, cols = k info), else the
+ * decode matrix (rows = erased information slots, cols = surviving slots). Any output pointer may be
+ * NULL to query sizes first. */
+int rsg_coding_matrix(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, uint16_t* matrix, uint32_t* rows,
+                      uint32_t* cols, int32_t* in_slots, int32_t* out_slots);
+/* Compiles the matrix-specialised kernel for the encode (is_erased == NULL) or decode matrix into the
+ * on-disk JIT cache without touching a GPU (0 also when the matrix is not JIT-eligible). */
+int rsg_jit_precompile(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t);
+/* GF(256)^2 coordinate tables used by the m <= 8 kernels (lbyte/ibyte: 2 x 256 entries each). */
+int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
+const char* rsg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

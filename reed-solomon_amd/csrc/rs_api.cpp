@@ -1,0 +1,738 @@
+// rs_api.cpp -- C ABI of librs_amd.so: the reference's drop-in API (rs/reed_solomon.h,
+// memory/*.h, scalar gf/cc helpers) and the batched device API (rs_amd/rsg.h).
+//
+// Every encode/decode runs on the GPU through rs_kernels.hip; there is no CPU compute path for
+// symbol data in this library.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gf16.hpp"
+#include "rs_jit.hpp"
+#include "rs_kernels.hpp"
+
+extern "C" {
+#include <memory/seq.h>
+#include <rs/cyclotomic_coset.h>
+#include <rs/gf65536.h>
+#include <rs/reed_solomon.h>
+#include <rs_amd/rsg.h>
+}
+
+using namespace rsamd;
+
+#define RSG_VERSION "rs_amd 0.1 (gfx950)"
+
+static int hip_fail(hipError_t e, const char* what) {
+    std::fprintf(stderr, "librs_amd: %s failed: %s\n", what, hipGetErrorString(e));
+    return RS_ERR_DEVICE;
+}
+
+#define HIP_TRY(expr)                                      \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);  \
+    } while (0)
+
+// ============================================================================ device plans
+namespace {
+
+struct DeviceTables {
+    uint32_t* d_ltab = nullptr;  // 2048 dwords, see ApplyArgs::ltab
+};
+
+std::mutex g_dev_mu;
+std::map<int, DeviceTables> g_dev;
+
+int device_tables(int device, const uint32_t** out) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    DeviceTables& t = g_dev[device];
+    if (!t.d_ltab) {
+        const Gamma8& g = gamma8();
+        std::vector<uint32_t> h(2048);
+        for (int b = 0; b < 256; ++b) {
+            h[b] = g.lbyte[0][b];
+            h[256 + b] = g.lbyte[1][b];
+            h[512 + b] = uint32_t(g.lbyte[0][b]) << 16;
+            h[768 + b] = uint32_t(g.lbyte[1][b]) << 16;
+            h[1024 + b] = g.ibyte[0][b];
+            h[1280 + b] = g.ibyte[1][b];
+            h[1536 + b] = uint32_t(g.ibyte[0][b]) << 16;
+            h[1792 + b] = uint32_t(g.ibyte[1][b]) << 16;
+        }
+        void* p = nullptr;
+        HIP_TRY(hipMalloc(&p, h.size() * 4));
+        HIP_TRY(hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        t.d_ltab = static_cast<uint32_t*>(p);
+    }
+    *out = t.d_ltab;
+    return 0;
+}
+
+// A coding matrix resident on one device, packed for the kernels.
+struct DevPlan {
+    int device = 0;
+    int m = 16, rt = 0, K = 0, R = 0, ntiles = 0;
+    int32_t* d_in = nullptr;
+    int32_t* d_out = nullptr;
+    uint32_t* d_coef = nullptr;
+    std::vector<uint16_t> matrix;  // R x K, GF(2^16)
+    std::vector<int32_t> in_slots, out_slots;
+    std::unique_ptr<JitKernel> jit;  // matrix-specialised kernel, if built
+    ~DevPlan() {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        (void)hipFree(d_in);
+        (void)hipFree(d_out);
+        (void)hipFree(d_coef);
+        (void)hipSetDevice(cur);
+    }
+};
+
+int upload(void** dst, const void* src, size_t bytes) {
+    HIP_TRY(hipMalloc(dst, std::max<size_t>(bytes, 16)));
+    if (bytes) HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::vector<int32_t> in_slots,
+               std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out) {
+    auto p = std::make_unique<DevPlan>();
+    p->device = device;
+    p->m = m <= 8 ? 8 : 16;
+    p->K = K;
+    p->R = R;
+    p->rt = apply_tile_rows(p->m, std::max(R, 1));
+    p->ntiles = (R + p->rt - 1) / p->rt;
+    const int rt = p->rt;
+    std::vector<uint32_t> coef;
+    if (p->m == 8) {
+        const Gamma8& g = gamma8();
+        coef.assign(size_t(p->ntiles) * K * (rt / 4), 0);
+        for (int t = 0; t < p->ntiles; ++t)
+            for (int i = 0; i < K; ++i)
+                for (int j = 0; j < rt; ++j) {
+                    const int row = t * rt + j;
+                    if (row >= R) continue;
+                    const uint32_t c = g.coord(M[size_t(row) * K + i]);
+                    coef[(size_t(t) * K + i) * (rt / 4) + j / 4] |= c << (8 * (j % 4));
+                }
+    } else {
+        coef.assign(size_t(p->ntiles) * K * (rt / 2), 0);
+        for (int t = 0; t < p->ntiles; ++t)
+            for (int i = 0; i < K; ++i)
+                for (int j = 0; j < rt; ++j) {
+                    const int row = t * rt + j;
+                    if (row >= R) continue;
+                    const uint32_t c = M[size_t(row) * K + i];
+                    coef[(size_t(t) * K + i) * (rt / 2) + j / 2] |= c << (16 * (j % 2));
+                }
+    }
+    out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
+    int rc;
+    if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
+    if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
+    if ((rc = upload(reinterpret_cast<void**>(&p->d_coef), coef.data(), coef.size() * 4))) return rc;
+    p->matrix = std::move(M);
+    p->in_slots = std::move(in_slots);
+    p->out_slots = std::move(out_slots);
+    out = std::move(p);
+    return 0;
+}
+
+}  // namespace
+
+// ============================================================================ codec
+struct rsg_codec {
+    int device = 0;
+    uint16_t k = 0, r = 0;
+    int m = 16;
+    std::vector<uint16_t> positions;
+    const uint32_t* d_ltab = nullptr;
+    std::unique_ptr<DevPlan> enc;
+    std::map<std::vector<uint8_t>, std::unique_ptr<DevPlan>> dec;
+    std::vector<std::vector<uint8_t>> dec_lru;
+    int m8_mode = 1;
+    int jit = 0;
+    std::string last_kernel = "none";
+};
+
+static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r, const bool* erased,
+                        std::vector<uint16_t>& M, std::vector<int32_t>& in_slots, std::vector<int32_t>& out_slots) {
+    const size_t n = size_t(k) + r;
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    in_slots.clear();
+    out_slots.clear();
+    if (!erased) {
+        // encode: solve the r repair positions from the k information positions
+        for (size_t i = 0; i < k; ++i) sources.push_back(pos[i]), in_slots.push_back(int32_t(i));
+        for (size_t p = 0; p < r; ++p) targets.push_back(pos[k + p]), emit.push_back(int(p)), out_slots.push_back(int32_t(p));
+    } else {
+        for (size_t i = 0; i < n; ++i) {
+            if (erased[i]) {
+                if (i < k) emit.push_back(int(targets.size())), out_slots.push_back(int32_t(i));
+                targets.push_back(pos[i]);
+            } else {
+                sources.push_back(pos[i]);
+                in_slots.push_back(int32_t(i));
+            }
+        }
+    }
+    M = solve_matrix(targets, emit, sources);
+    return 0;
+}
+
+extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t** out) {
+    if (!out) return RS_ERR_INVALID;
+    *out = nullptr;
+    if (uint32_t(k) + r > kN) return RS_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+        std::fprintf(stderr, "librs_amd: no HIP device %d (found %d)\n", device, ndev);
+        return RS_ERR_DEVICE;
+    }
+    HIP_TRY(hipSetDevice(device));
+    auto c = std::make_unique<rsg_codec>();
+    c->device = device;
+    c->k = k;
+    c->r = r;
+    try {
+        c->positions = code_positions(k, r);
+    } catch (...) {
+        return RS_ERR_INVALID;
+    }
+    c->m = subfield_degree(c->positions);
+    int rc = device_tables(device, &c->d_ltab);
+    if (rc) return rc;
+    std::vector<uint16_t> M;
+    std::vector<int32_t> in, outs;
+    codec_matrix(c->positions, k, r, nullptr, M, in, outs);
+    if ((rc = build_plan(device, c->m, std::move(M), k, r, std::move(in), std::move(outs), c->enc))) return rc;
+    *out = c.release();
+    return 0;
+}
+
+extern "C" void rsg_codec_destroy(rsg_codec_t* c) { delete c; }
+
+extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 ? 8 : 16) : 0; }
+
+extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
+    if (!c || !name) return RS_ERR_INVALID;
+    if (!std::strcmp(name, "m8_mode")) {
+        if (value != 0 && value != 1) return RS_ERR_INVALID;
+        c->m8_mode = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "jit")) {
+        c->jit = value ? 1 : 0;
+        return 0;
+    }
+    return RS_ERR_INVALID;
+}
+
+extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->last_kernel.c_str() : "none"; }
+
+static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
+                    int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st) {
+    if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
+    const int64_t align = p.m == 8 ? 8 : 4;
+    if ((S & 1) || (uintptr_t(src) % align) || (uintptr_t(dst) % align) || (src_stripe % align) ||
+        (src_sym % align) || (dst_stripe % align) || (dst_sym % align))
+        return RS_ERR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->jit && p.m == 8) {
+        if (!p.jit) {
+            int rc = jit_build(p.matrix, p.K, p.R, p.in_slots, p.out_slots, p.jit);
+            if (rc) return rc;
+        }
+        if (p.jit) {
+            c->last_kernel = p.jit->name;
+            return jit_launch(*p.jit, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, int64_t(n_stripes),
+                              int64_t(S), c->d_ltab, st);
+        }
+    }
+    ApplyArgs a{};
+    a.src = src;
+    a.src_stripe = src_stripe;
+    a.src_sym = src_sym;
+    a.in_idx = p.d_in;
+    a.dst = dst;
+    a.dst_stripe = dst_stripe;
+    a.dst_sym = dst_sym;
+    a.out_idx = p.d_out;
+    a.coef = p.d_coef;
+    a.ltab = c->d_ltab;
+    a.K = p.K;
+    a.R = p.R;
+    a.nbytes = int64_t(S);
+    a.mode = c->m8_mode;
+    c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(p.rt) + "_mode" + std::to_string(a.mode))
+                              : (std::string("apply_m16_rt") + std::to_string(p.rt));
+    HIP_TRY(launch_apply(p.m, p.rt, a, int64_t(n_stripes), st));
+    return 0;
+}
+
+extern "C" int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stripe_stride, uint64_t info_symbol_stride,
+                          void* d_rep, uint64_t rep_stripe_stride, uint64_t rep_symbol_stride, uint64_t n_stripes,
+                          uint64_t symbol_size, void* stream) {
+    if (!c) return RS_ERR_INVALID;
+    return run_plan(c, *c->enc, static_cast<const uint8_t*>(d_info), int64_t(info_stripe_stride),
+                    int64_t(info_symbol_stride), static_cast<uint8_t*>(d_rep), int64_t(rep_stripe_stride),
+                    int64_t(rep_symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
+}
+
+static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out) {
+    const size_t n = size_t(c->k) + c->r;
+    if (t > c->r) return RS_ERR_CANNOT_RESTORE;
+    std::vector<uint8_t> key(n);
+    size_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) cnt += (key[i] = is_erased[i] ? 1 : 0);
+    if (cnt != t) return RS_ERR_INVALID;
+    auto it = c->dec.find(key);
+    if (it == c->dec.end()) {
+        std::vector<uint16_t> M;
+        std::vector<int32_t> in, outs;
+        codec_matrix(c->positions, c->k, c->r, is_erased, M, in, outs);
+        std::unique_ptr<DevPlan> p;
+        const int R = int(outs.size()), K = int(in.size());
+        int rc = build_plan(c->device, c->m, std::move(M), K, R, std::move(in), std::move(outs), p);
+        if (rc) return rc;
+        if (c->dec_lru.size() >= 16) {
+            c->dec.erase(c->dec_lru.front());
+            c->dec_lru.erase(c->dec_lru.begin());
+        }
+        c->dec_lru.push_back(key);
+        it = c->dec.emplace(key, std::move(p)).first;
+    }
+    *out = it->second.get();
+    return 0;
+}
+
+extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
+                          uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream) {
+    if (!c || !is_erased) return RS_ERR_INVALID;
+    if (t > c->r) return RS_ERR_CANNOT_RESTORE;
+    DevPlan* p = nullptr;
+    int rc = decode_plan(c, is_erased, t, &p);
+    if (rc) return rc;
+    uint8_t* base = static_cast<uint8_t*>(d_rcv);
+    return run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
+                    int64_t(symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size,
+                             uint16_t k, uint64_t stripe0, uint64_t n_stripes, uint64_t seed, void* stream) {
+    if (symbol_size % 8 || symbol_stride % 8 || stripe_stride % 8 || uintptr_t(d_base) % 8) return RS_ERR_INVALID;
+    if (!n_stripes || !k) return 0;
+    HIP_TRY(launch_gen_info(static_cast<uint8_t*>(d_base), int64_t(stripe_stride), int64_t(symbol_stride),
+                            int64_t(symbol_size), k, int64_t(stripe0), int64_t(n_stripes), seed,
+                            static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int rsg_fingerprint(const void* d_base, uint64_t stripe_stride, uint64_t symbol_stride,
+                               uint64_t symbol_size, uint32_t sym0, uint32_t nsym, uint64_t n_stripes, uint64_t* d_out,
+                               void* stream) {
+    if (symbol_size % 8 || symbol_stride % 8 || stripe_stride % 8 || uintptr_t(d_base) % 8) return RS_ERR_INVALID;
+    if (!n_stripes) return 0;
+    HIP_TRY(launch_fingerprint(static_cast<const uint8_t*>(d_base), int64_t(stripe_stride), int64_t(symbol_stride),
+                               int64_t(symbol_size), int(sym0), int(nsym), int64_t(n_stripes),
+                               reinterpret_cast<unsigned long long*>(d_out), static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+extern "C" int rsg_coding_matrix(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, uint16_t* matrix,
+                                 uint32_t* rows, uint32_t* cols, int32_t* in_slots, int32_t* out_slots) {
+    if (uint32_t(k) + r > kN) return RS_ERR_INVALID;
+    if (is_erased) {
+        if (t > r) return RS_ERR_CANNOT_RESTORE;
+        size_t cnt = 0;
+        for (size_t i = 0; i < size_t(k) + r; ++i) cnt += is_erased[i] ? 1 : 0;
+        if (cnt != t) return RS_ERR_INVALID;
+    }
+    std::vector<uint16_t> pos = code_positions(k, r), M;
+    std::vector<int32_t> in, outs;
+    codec_matrix(pos, k, r, is_erased, M, in, outs);
+    if (rows) *rows = uint32_t(outs.size());
+    if (cols) *cols = uint32_t(in.size());
+    if (matrix) std::memcpy(matrix, M.data(), M.size() * 2);
+    if (in_slots) std::memcpy(in_slots, in.data(), in.size() * 4);
+    if (out_slots) std::memcpy(out_slots, outs.data(), outs.size() * 4);
+    return 0;
+}
+
+extern "C" int rsg_jit_precompile(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t) {
+    if (uint32_t(k) + r > kN) return RS_ERR_INVALID;
+    std::vector<uint16_t> pos = code_positions(k, r), M;
+    if (subfield_degree(pos) > 8) return 0;
+    std::vector<int32_t> in, outs;
+    if (is_erased) {
+        size_t cnt = 0;
+        for (size_t i = 0; i < size_t(k) + r; ++i) cnt += is_erased[i] ? 1 : 0;
+        if (cnt != t || t > r) return RS_ERR_INVALID;
+    }
+    codec_matrix(pos, k, r, is_erased, M, in, outs);
+    return jit_precompile(M, int(in.size()), int(outs.size()), in, outs);
+}
+
+extern "C" int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red) {
+    const Gamma8& g = gamma8();
+    if (lbyte) std::memcpy(lbyte, g.lbyte, sizeof(g.lbyte));
+    if (ibyte) std::memcpy(ibyte, g.ibyte, sizeof(g.ibyte));
+    if (red) *red = g.red;
+    return 0;
+}
+
+extern "C" const char* rsg_version(void) { return RSG_VERSION; }
+
+// ============================================================================ drop-in rs_*
+namespace {
+
+struct Impl {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::map<std::pair<uint16_t, uint16_t>, std::unique_ptr<rsg_codec>> codecs;
+    uint8_t* h_buf = nullptr;
+    uint8_t* d_buf = nullptr;
+    size_t cap = 0;
+    ~Impl() {
+        (void)hipSetDevice(device);
+        codecs.clear();
+        if (h_buf) (void)hipHostFree(h_buf);
+        if (d_buf) (void)hipFree(d_buf);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    int reserve(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (h_buf) (void)hipHostFree(h_buf);
+        if (d_buf) (void)hipFree(d_buf);
+        h_buf = nullptr;
+        d_buf = nullptr;
+        cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&h_buf), bytes, hipHostMallocDefault) != hipSuccess) return 1;
+        if (hipMalloc(reinterpret_cast<void**>(&d_buf), bytes) != hipSuccess) return 1;
+        cap = bytes;
+        return 0;
+    }
+    int codec(uint16_t k, uint16_t r, rsg_codec** out) {
+        auto key = std::make_pair(k, r);
+        auto it = codecs.find(key);
+        if (it == codecs.end()) {
+            rsg_codec* c = nullptr;
+            int rc = rsg_codec_create(device, k, r, &c);
+            if (rc) return rc;
+            it = codecs.emplace(key, std::unique_ptr<rsg_codec>(c)).first;
+        }
+        *out = it->second.get();
+        return 0;
+    }
+};
+
+inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
+
+}  // namespace
+
+extern "C" RS_t* rs_create(void) {
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        std::fprintf(stderr, "librs_amd: rs_create: no usable HIP device (%s); there is no CPU fallback\n",
+                     hipGetErrorString(e));
+        return nullptr;
+    }
+    RS_t* rs = static_cast<RS_t*>(std::calloc(1, sizeof(RS_t)));
+    if (!rs) return nullptr;
+    rs->gf = gf_create();
+    rs->cc = cc_create();
+    auto* impl = new (std::nothrow) Impl();
+    if (!rs->gf || !rs->cc || !impl) {
+        delete impl;
+        if (rs->gf) gf_destroy(rs->gf);
+        if (rs->cc) cc_destroy(rs->cc);
+        std::free(rs);
+        return nullptr;
+    }
+    (void)hipGetDevice(&impl->device);
+    if (hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete impl;
+        gf_destroy(rs->gf);
+        cc_destroy(rs->cc);
+        std::free(rs);
+        return nullptr;
+    }
+    rs->impl = impl;
+    return rs;
+}
+
+extern "C" void rs_destroy(RS_t* rs) {
+    if (!rs) return;
+    delete static_cast<Impl*>(rs->impl);
+    gf_destroy(rs->gf);
+    cc_destroy(rs->cc);
+    std::free(rs);
+}
+
+extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, symbol_seq_t* rep) {
+    if (!rs || !rs->impl || !inf || !rep) return RS_ERR_INVALID;
+    Impl& im = *static_cast<Impl*>(rs->impl);
+    const size_t S = inf->symbol_size;
+    if (S != rep->symbol_size || (S & 1) || inf->length + rep->length > kN) return RS_ERR_INVALID;
+    const uint16_t k = uint16_t(inf->length), r = uint16_t(rep->length);
+    if (r == 0 || S == 0) return 0;
+    std::lock_guard<std::mutex> lk(im.mu);
+    HIP_TRY(hipSetDevice(im.device));
+    rsg_codec* c = nullptr;
+    int rc = im.codec(k, r, &c);
+    if (rc) return rc;
+    const size_t P = pad16(S), n = size_t(k) + r;
+    if (im.reserve(n * P)) return 1;
+    for (size_t i = 0; i < k; ++i) std::memcpy(im.h_buf + i * P, inf->symbols[i]->data, S);
+    HIP_TRY(hipMemcpyAsync(im.d_buf, im.h_buf, size_t(k) * P, hipMemcpyHostToDevice, im.stream));
+    rc = rsg_encode(c, im.d_buf, n * P, P, im.d_buf + size_t(k) * P, n * P, P, 1, S, im.stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(im.h_buf + size_t(k) * P, im.d_buf + size_t(k) * P, size_t(r) * P, hipMemcpyDeviceToHost,
+                           im.stream));
+    HIP_TRY(hipStreamSynchronize(im.stream));
+    for (size_t p = 0; p < r; ++p) std::memcpy(rep->symbols[p]->data, im.h_buf + (k + p) * P, S);
+    return 0;
+}
+
+extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool* is_erased,
+                                  uint16_t t) {
+    if (r < t) return RS_ERR_CANNOT_RESTORE;  // checked first, as reference reed_solomon.c:467-470
+    if (!rs || !rs->impl || !rcv || !is_erased) return RS_ERR_INVALID;
+    Impl& im = *static_cast<Impl*>(rs->impl);
+    const size_t S = rcv->symbol_size, n = size_t(k) + r;
+    if (rcv->length != n || (S & 1) || n > kN) return RS_ERR_INVALID;
+    size_t cnt = 0;
+    bool info_lost = false;
+    for (size_t i = 0; i < n; ++i)
+        if (is_erased[i]) ++cnt, info_lost |= i < k;
+    if (cnt != t) return RS_ERR_INVALID;
+    if (!info_lost || S == 0) return 0;
+    std::lock_guard<std::mutex> lk(im.mu);
+    HIP_TRY(hipSetDevice(im.device));
+    rsg_codec* c = nullptr;
+    int rc = im.codec(k, r, &c);
+    if (rc) return rc;
+    const size_t P = pad16(S);
+    if (im.reserve(n * P)) return 1;
+    for (size_t i = 0; i < n; ++i)
+        if (!is_erased[i]) std::memcpy(im.h_buf + i * P, rcv->symbols[i]->data, S);
+    HIP_TRY(hipMemcpyAsync(im.d_buf, im.h_buf, n * P, hipMemcpyHostToDevice, im.stream));
+    rc = rsg_decode(c, im.d_buf, n * P, P, 1, S, is_erased, t, im.stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(im.h_buf, im.d_buf, size_t(k) * P, hipMemcpyDeviceToHost, im.stream));
+    HIP_TRY(hipStreamSynchronize(im.stream));
+    for (size_t i = 0; i < k; ++i)
+        if (is_erased[i]) std::memcpy(rcv->symbols[i]->data, im.h_buf + i * P, S);
+    return 0;
+}
+
+// ============================================================================ memory/*.h
+extern "C" symbol_t* symbol_create(size_t symbol_size) {
+    symbol_t* s = static_cast<symbol_t*>(std::calloc(1, sizeof(symbol_t)));
+    if (!s) return nullptr;
+    s->data = static_cast<uint8_t*>(std::calloc(symbol_size ? symbol_size : 1, 1));
+    if (!s->data) {
+        std::free(s);
+        return nullptr;
+    }
+    return s;
+}
+
+extern "C" void symbol_destroy(symbol_t* s) {
+    if (!s) return;
+    std::free(s->data);
+    std::free(s);
+}
+
+extern "C" bool symbol_eq(const symbol_t* a, const symbol_t* b, size_t symbol_size) {
+    if (!a || !b || !a->data || !b->data) return false;
+    return std::memcmp(a->data, b->data, symbol_size) == 0;
+}
+
+extern "C" void symbol_printf(const symbol_t* s, size_t symbol_size) {
+    if (!s || !s->data) {
+        std::printf("NULL");
+        return;
+    }
+    std::printf("[");
+    for (size_t i = 0; i < symbol_size; ++i) std::printf(i + 1 < symbol_size ? "%u, " : "%u", s->data[i]);
+    std::printf("]");
+}
+
+extern "C" symbol_seq_t* seq_create(size_t length, size_t symbol_size) {
+    symbol_seq_t* q = static_cast<symbol_seq_t*>(std::calloc(1, sizeof(symbol_seq_t)));
+    if (!q) return nullptr;
+    q->length = length;
+    q->symbol_size = symbol_size;
+    q->symbols = static_cast<symbol_t**>(std::calloc(length ? length : 1, sizeof(symbol_t*)));
+    if (!q->symbols) {
+        std::free(q);
+        return nullptr;
+    }
+    for (size_t i = 0; i < length; ++i) {
+        if (!(q->symbols[i] = symbol_create(symbol_size))) {
+            for (size_t j = 0; j < i; ++j) symbol_destroy(q->symbols[j]);
+            std::free(q->symbols);
+            std::free(q);
+            return nullptr;
+        }
+    }
+    return q;
+}
+
+extern "C" void seq_destroy(symbol_seq_t* q) {
+    if (!q) return;
+    for (size_t i = 0; i < q->length; ++i) symbol_destroy(q->symbols[i]);
+    std::free(q->symbols);
+    std::free(q);
+}
+
+extern "C" bool seq_eq(const symbol_seq_t* a, const symbol_seq_t* b) {
+    if (!a || !b || !a->symbols || !b->symbols) return false;
+    if (a->length != b->length || a->symbol_size != b->symbol_size) return false;
+    for (size_t i = 0; i < a->length; ++i)
+        if (!symbol_eq(a->symbols[i], b->symbols[i], a->symbol_size)) return false;
+    return true;
+}
+
+extern "C" void seq_printf(const symbol_seq_t* q) {
+    if (!q || !q->symbols) {
+        std::printf("NULL");
+        return;
+    }
+    if (!q->length) {
+        std::printf("[]");
+        return;
+    }
+    std::printf("[");
+    for (size_t i = 0; i < q->length; ++i) {
+        symbol_printf(q->symbols[i], q->symbol_size);
+        if (i + 1 < q->length) std::printf(", ");
+    }
+    std::printf("]");
+}
+
+// ============================================================================ rs/gf65536.h, rs/cyclotomic_coset.h
+static const uint16_t kNormalBases[GF_NORMAL_BASES_ELEMENTS] = {
+    1,                                                           // GF(2)
+    44234, 44235,                                                // GF(4)
+    10800, 47860, 34555, 5694,                                   // GF(16)
+    16402, 53598, 44348, 63986, 22060, 64366, 6088, 32521,       // GF(256)
+    2048, 2880, 7129, 30616, 2643, 6897, 29685, 7378, 30100, 2743, 20193, 36223, 24055, 41458, 41014, 61451};
+
+extern "C" GF_t* gf_create(void) {
+    GF_t* gf = static_cast<GF_t*>(std::malloc(sizeof(GF_t)));
+    if (!gf) return nullptr;
+    const Field& F = field();
+    for (uint32_t i = 0; i < (kN << 1) - 1; ++i) gf->pow_table[i] = F.exp[i];
+    std::memcpy(gf->log_table, F.log, sizeof(gf->log_table));
+    std::memcpy(gf->normal_bases, kNormalBases, sizeof(kNormalBases));
+    return gf;
+}
+
+extern "C" void gf_destroy(GF_t* gf) { std::free(gf); }
+
+static int m_index(uint8_t m) { return m == 1 ? 0 : m == 2 ? 1 : m == 4 ? 3 : m == 8 ? 7 : 15; }
+
+extern "C" element_t gf_get_normal_basis_element(GF_t* gf, uint8_t m, uint8_t i) {
+    return gf ? gf->normal_bases[m_index(m) + i] : kNormalBases[m_index(m) + i];
+}
+
+extern "C" uint16_t gf_get_normal_repr(GF_t* gf, uint8_t m, uint16_t d) {
+    (void)gf;
+    // coordinates of alpha^d in the normal basis of GF(2^m) (0 when alpha^d is not in GF(2^m)),
+    // as reference gf65536.c:90-108 tabulates them
+    static std::once_flag once;
+    static std::vector<uint16_t> tab[5];
+    std::call_once(once, [] {
+        const Field& F = field();
+        const uint8_t ms[5] = {1, 2, 4, 8, 16};
+        for (int li = 0; li < 5; ++li) {
+            const uint8_t mm = ms[li];
+            tab[li].assign(kN, 0);
+            for (uint32_t bits = 1; bits < (1u << mm); ++bits) {
+                uint16_t e = 0;
+                for (int j = 0; j < mm; ++j)
+                    if (bits & (1u << j)) e ^= kNormalBases[m_index(mm) + j];
+                tab[li][F.log[e]] = uint16_t(bits);
+            }
+        }
+    });
+    const int li = m == 1 ? 0 : m == 2 ? 1 : m == 4 ? 2 : m == 8 ? 3 : 4;
+    return tab[li][d % kN];
+}
+
+extern "C" element_t gf_mul_ee(GF_t* gf, element_t a, element_t b) {
+    (void)gf;
+    return field().mul(a, b);
+}
+
+extern "C" element_t gf_div_ee(GF_t* gf, element_t a, element_t b) {
+    (void)gf;
+    return field().div(a, b);
+}
+
+extern "C" CC_t* cc_create(void) {
+    CC_t* cc = static_cast<CC_t*>(std::malloc(sizeof(CC_t)));
+    if (!cc) return nullptr;
+    const Cosets& cs = cosets();
+    uint16_t* w = cc->_leaders_memory;
+    for (int i = 0; i < CC_COSET_SIZES_CNT; ++i) {
+        cc->leaders[i] = w;
+        for (uint16_t l : cs.leaders[i]) *w++ = l;
+    }
+    return cc;
+}
+
+extern "C" void cc_destroy(CC_t* cc) { std::free(cc); }
+
+extern "C" uint8_t cc_get_coset_size(uint16_t leader) {
+    uint8_t m = 1;
+    while (leader != uint16_t((uint32_t(leader) << m) % kN)) m <<= 1;
+    return m;
+}
+
+extern "C" void cc_estimate_cosets_cnt(uint16_t k, uint16_t r, uint16_t* inf_max_cnt, uint16_t* rep_max_cnt) {
+    if (inf_max_cnt) *inf_max_cnt = coset_upper_bound(k);
+    if (rep_max_cnt) *rep_max_cnt = coset_upper_bound(r);
+}
+
+extern "C" void cc_select_cosets(CC_t* cc, uint16_t k, uint16_t r, coset_t* inf_cosets, uint16_t inf_max_cnt,
+                                 uint16_t* inf_cosets_cnt, coset_t* rep_cosets, uint16_t rep_max_cnt,
+                                 uint16_t* rep_cosets_cnt) {
+    (void)cc;
+    std::vector<CosetRef> inf, rep;
+    select_cosets(k, r, inf, rep);
+    // the caller's capacities bound the output exactly like the reference loop guards
+    const size_t ni = std::min<size_t>(inf.size(), inf_max_cnt), nr = std::min<size_t>(rep.size(), rep_max_cnt);
+    for (size_t i = 0; i < ni; ++i) inf_cosets[i] = coset_t{inf[i].leader, inf[i].size};
+    for (size_t i = 0; i < nr; ++i) rep_cosets[i] = coset_t{rep[i].leader, rep[i].size};
+    *inf_cosets_cnt = uint16_t(ni);
+    *rep_cosets_cnt = uint16_t(nr);
+}
+
+extern "C" void cc_cosets_to_positions(const coset_t* cs, uint16_t cosets_cnt, uint16_t* positions,
+                                       uint16_t positions_cnt) {
+    uint16_t w = 0;
+    for (uint16_t c = 0; c < cosets_cnt && w < positions_cnt; ++c) {
+        uint16_t e = cs[c].leader;
+        do {
+            positions[w++] = e;
+            e = NEXT_COSET_ELEMENT(e);
+        } while (e != cs[c].leader && w < positions_cnt);
+    }
+}

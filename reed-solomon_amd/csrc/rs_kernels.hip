@@ -1,0 +1,265 @@
+// rs_kernels.hip -- CDNA4 (gfx950) kernels of the Reed-Solomon engine.
+//
+// Every encode and decode is one GF(2^16)-linear map applied independently to each 16-bit word
+// column of a stripe:  out_p = sum_i C[p][i] * in_i.  The kernels
+// stream the K input symbols of a stripe once from HBM, keep R output accumulators per lane in
+// VGPRs and write each output once: algorithmic traffic (K + R) * S bytes per stripe.
+//
+// GF multiply-add without per-word table gathers: for each input word x a lane builds, in
+// registers, the 16-entry nibble tables T[e] = (e-th combination of x * basis^j). A coefficient c
+// then contributes T_lo[c & 15] ^ T_hi[c >> 4] (m <= 8) -- two uniform-index register reads
+// (s_set_gpr_idx) and one 3-input XOR per dword, shared by all 64 lanes because the coefficient
+// is wave-uniform. No MFMA: GF(2) arithmetic is XOR, not a dense numeric contraction.
+//
+//  * m <= 8 (all positions in GF(256), e.g. k+r <= 255): words are moved to GF(256)^2 coordinates
+//    (x = x0 + x1*alpha, x_h in the gamma = alpha^257 polynomial basis) through LDS byte tables,
+//    so multiplication by a GF(256) coefficient is byte-wise; 8 multiples by gamma^j come from
+//    xtime on 4 packed bytes; two nibble tables; coordinates are mapped back before the store.
+//  * m = 16 (general): multiples x * alpha^j (j < 16) by 16-bit xtime on packed words, four
+//    nibble tables, no coordinate change.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rs_device.h"
+#include "rs_kernels.hpp"
+
+namespace rsamd {
+
+// ------------------------------------------------------------------------------------ m <= 8
+// Block = 256 lanes x 8 bytes = 2 KiB of columns of one stripe, RT outputs of tile blockIdx.y.
+// MODE 0: nibble tables in VGPRs read with a wave-uniform index (s_set_gpr_idx), 1 xor3 / output.
+// MODE 1: the 8 gamma-multiples masked by the coefficient's bits (SGPR masks), 8 bitop3 / output.
+template <int RT, int MODE>
+__global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
+    __shared__ uint32_t lt[2048];  // [0,1024): L byte tables, [1024,2048): L^-1 byte tables
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+
+    const int64_t bid = blockIdx.x;
+    const int64_t stripe = bid / a.nchunks;
+    const int64_t col = (bid - stripe * a.nchunks) * 2048 + int64_t(threadIdx.x) * 8;
+    const int64_t avail = a.nbytes - col;
+    const int tile = blockIdx.y;
+    const uint8_t* src = a.src + stripe * a.src_stripe + col;
+    const uint32_t* cf = a.coef + size_t(tile) * a.K * (RT / 4);
+
+    uint32_t acc[RT][2];
+#pragma unroll
+    for (int p = 0; p < RT; ++p) acc[p][0] = acc[p][1] = 0;
+
+    if (avail > 0) {
+        uint32_t nxt[2];
+        if (a.K > 0) load_slice<8>(nxt, src + int64_t(a.in_idx[0]) * a.src_sym, avail);
+        for (int i = 0; i < a.K; ++i) {
+            const uint32_t x[2] = {nxt[0], nxt[1]};
+            if (i + 1 < a.K) load_slice<8>(nxt, src + int64_t(a.in_idx[i + 1]) * a.src_sym, avail);
+            uint32_t m[2][8];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                m[v][0] = lds_lookup4(lt, x[v]);
+#pragma unroll
+                for (int j = 1; j < 8; ++j) m[v][j] = xt8(m[v][j - 1]);
+            }
+            const uint32_t* c = cf + size_t(i) * (RT / 4);
+            if constexpr (MODE == 0) {
+                const u32x16 Tl0 = build16(m[0][0], m[0][1], m[0][2], m[0][3]);
+                const u32x16 Th0 = build16(m[0][4], m[0][5], m[0][6], m[0][7]);
+                const u32x16 Tl1 = build16(m[1][0], m[1][1], m[1][2], m[1][3]);
+                const u32x16 Th1 = build16(m[1][4], m[1][5], m[1][6], m[1][7]);
+#pragma unroll
+                for (int q = 0; q < RT / 4; ++q) {
+                    const uint32_t w = c[q];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t lo = (w >> (8 * b)) & 15u, hi = (w >> (8 * b + 4)) & 15u;
+                        acc[4 * q + b][0] = xor3(acc[4 * q + b][0], Tl0[lo], Th0[hi]);
+                        acc[4 * q + b][1] = xor3(acc[4 * q + b][1], Tl1[lo], Th1[hi]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < RT / 4; ++q) {
+                    const uint32_t w = c[q];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const uint32_t mask = 0u - ((w >> (8 * b + j)) & 1u);
+                            acc[4 * q + b][0] ^= m[0][j] & mask;
+                            acc[4 * q + b][1] ^= m[1][j] & mask;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (avail <= 0) return;
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+    const int rows = min(RT, a.R - tile * RT);
+#pragma unroll
+    for (int p = 0; p < RT; ++p) {
+        if (p < rows) {
+            uint32_t y[2] = {lds_lookup4(lt + 1024, acc[p][0]), lds_lookup4(lt + 1024, acc[p][1])};
+            store_slice<8>(dst + int64_t(a.out_idx[tile * RT + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ m = 16
+// Block = 256 lanes x 4 bytes = 1 KiB of columns, RT outputs of tile blockIdx.y.
+template <int RT>
+__global__ void __launch_bounds__(256) k_apply_m16(ApplyArgs a) {
+    const int64_t bid = blockIdx.x;
+    const int64_t stripe = bid / a.nchunks;
+    const int64_t col = (bid - stripe * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
+    const int64_t avail = a.nbytes - col;
+    if (avail <= 0) return;
+    const int tile = blockIdx.y;
+    const uint8_t* src = a.src + stripe * a.src_stripe + col;
+    const uint32_t* cf = a.coef + size_t(tile) * a.K * (RT / 2);
+
+    uint32_t acc[RT];
+#pragma unroll
+    for (int p = 0; p < RT; ++p) acc[p] = 0;
+
+    uint32_t nxt[1];
+    if (a.K > 0) load_slice<4>(nxt, src + int64_t(a.in_idx[0]) * a.src_sym, avail);
+    for (int i = 0; i < a.K; ++i) {
+        const uint32_t x = nxt[0];
+        if (i + 1 < a.K) load_slice<4>(nxt, src + int64_t(a.in_idx[i + 1]) * a.src_sym, avail);
+        uint32_t m[16];
+        m[0] = x;
+#pragma unroll
+        for (int j = 1; j < 16; ++j) m[j] = xt16(m[j - 1]);
+        const u32x16 T0 = build16(m[0], m[1], m[2], m[3]);
+        const u32x16 T1 = build16(m[4], m[5], m[6], m[7]);
+        const u32x16 T2 = build16(m[8], m[9], m[10], m[11]);
+        const u32x16 T3 = build16(m[12], m[13], m[14], m[15]);
+        const uint32_t* c = cf + size_t(i) * (RT / 2);
+#pragma unroll
+        for (int q = 0; q < RT / 2; ++q) {
+            const uint32_t w = c[q];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t cc = w >> (16 * h);
+                const int p = 2 * q + h;
+                acc[p] = xor3(acc[p], T0[cc & 15u], T1[(cc >> 4) & 15u]);
+                acc[p] = xor3(acc[p], T2[(cc >> 8) & 15u], T3[(cc >> 12) & 15u]);
+            }
+        }
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+    const int rows = min(RT, a.R - tile * RT);
+#pragma unroll
+    for (int p = 0; p < RT; ++p) {
+        if (p < rows) {
+            uint32_t y[1] = {acc[p]};
+            store_slice<4>(dst + int64_t(a.out_idx[tile * RT + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ synthetic inputs
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Information region of stripe s = k symbols of S bytes; byte b = byte (b & 7) of
+// mix64(seed ^ s*G ^ (b>>3)*Q + G)  (tests/_util.py:gen_info, oracle/gen_golden.c:gen_byte).
+__global__ void k_gen_info(uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int64_t words_per_stripe,
+                           int64_t stripe0, int64_t n_stripes, uint64_t seed) {
+    const int64_t total = words_per_stripe * n_stripes;
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < total; g += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t s = g / words_per_stripe;
+        const int64_t q = g - s * words_per_stripe;
+        const uint64_t x = seed ^ (uint64_t(stripe0 + s) * 0x9E3779B97F4A7C15ull) ^ (uint64_t(q) * 0xC2B2AE3D27D4EB4Full);
+        const uint64_t v = mix64(x + 0x9E3779B97F4A7C15ull);
+        const int64_t b = q * 8, sym = b / S, off = b - sym * S;
+        *reinterpret_cast<uint64_t*>(base + s * stripe_stride + sym * sym_stride + off) = v;
+    }
+}
+
+// Order-independent, position-sensitive 64-bit fingerprint of symbols [sym0, sym0+nsym) of each
+// stripe (S % 8 == 0): out[s] ^= mix64(word ^ mix64(sym << 40 | offset)).
+__global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int sym0,
+                              int nsym, int64_t n_stripes, unsigned long long* out) {
+    const int64_t wps = (S / 8) * nsym;
+    const int64_t s = blockIdx.y;
+    if (s >= n_stripes) return;
+    uint64_t h = 0;
+    for (int64_t q = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < wps; q += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t sym = q / (S / 8), off = (q - sym * (S / 8)) * 8;
+        const uint64_t w = *reinterpret_cast<const uint64_t*>(base + s * stripe_stride + (sym0 + sym) * sym_stride + off);
+        h ^= mix64(w ^ mix64((uint64_t(sym0 + sym) << 40) | uint64_t(off)));
+    }
+    for (int o = 32; o > 0; o >>= 1) h ^= __shfl_xor(h, o);
+    if ((threadIdx.x & 63) == 0) atomicXor(out + s, (unsigned long long)h);
+}
+
+// ------------------------------------------------------------------------------ launchers
+template <int RT>
+static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
+    dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
+    if (a.mode == 1)
+        hipLaunchKernelGGL((k_apply_m8<RT, 1>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_apply_m8<RT, 0>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int RT>
+static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
+    dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
+    hipLaunchKernelGGL(k_apply_m16<RT>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+int apply_tile_rows(int m, int R) {
+    if (m <= 8) return R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
+    return R <= 16 ? 16 : R <= 32 ? 32 : 64;
+}
+
+int64_t apply_chunk_bytes(int m) { return m <= 8 ? 2048 : 1024; }
+
+hipError_t launch_apply(int m, int rt, ApplyArgs a, int64_t n_stripes, hipStream_t st) {
+    a.nchunks = (a.nbytes + apply_chunk_bytes(m) - 1) / apply_chunk_bytes(m);
+    if (n_stripes <= 0 || a.R <= 0 || a.nchunks == 0) return hipSuccess;
+    if (m <= 8) {
+        switch (rt) {
+        case 4: return launch_m8<4>(a, n_stripes, st);
+        case 8: return launch_m8<8>(a, n_stripes, st);
+        case 16: return launch_m8<16>(a, n_stripes, st);
+        case 32: return launch_m8<32>(a, n_stripes, st);
+        }
+    } else {
+        switch (rt) {
+        case 16: return launch_m16<16>(a, n_stripes, st);
+        case 32: return launch_m16<32>(a, n_stripes, st);
+        case 64: return launch_m16<64>(a, n_stripes, st);
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_gen_info(uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int k, int64_t stripe0,
+                           int64_t n_stripes, uint64_t seed, hipStream_t st) {
+    const int64_t wps = int64_t(k) * S / 8;
+    hipLaunchKernelGGL(k_gen_info, dim3(4096), dim3(256), 0, st, base, stripe_stride, sym_stride, S, wps, stripe0,
+                       n_stripes, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int sym0,
+                              int nsym, int64_t n_stripes, unsigned long long* out, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(out, 0, size_t(n_stripes) * 8, st);
+    if (e != hipSuccess) return e;
+    const int64_t wps = (S / 8) * nsym;
+    unsigned gx = unsigned(std::min<int64_t>((wps + 255) / 256, 64));
+    hipLaunchKernelGGL(k_fingerprint, dim3(gx, unsigned(n_stripes)), dim3(256), 0, st, base, stripe_stride, sym_stride,
+                       S, sym0, nsym, n_stripes, out);
+    return hipGetLastError();
+}
+
+}  // namespace rsamd

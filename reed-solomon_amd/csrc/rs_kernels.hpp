@@ -1,0 +1,35 @@
+// rs_kernels.hpp -- launch interface of the HIP kernels (rs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsamd {
+
+// out[stripe][out_idx[p]] = sum_i C[p][i] * in[stripe][in_idx[i]]   for p < R, per 16-bit word.
+struct ApplyArgs {
+    const uint8_t* src;      // stripe 0 of the input layout
+    int64_t src_stripe;      // bytes between stripes
+    int64_t src_sym;         // bytes between symbols
+    const int32_t* in_idx;   // [K] input symbol indices (device)
+    uint8_t* dst;
+    int64_t dst_stripe;
+    int64_t dst_sym;
+    const int32_t* out_idx;  // [R] output symbol indices (device)
+    const uint32_t* coef;    // [ntiles][K][RT/4] gamma-basis bytes (m<=8) | [ntiles][K][RT/2] u16 (m=16)
+    const uint32_t* ltab;    // m<=8: [2048] LDS coordinate tables (L bytes 0..3, L^-1 bytes 0..3)
+    int32_t K;
+    int32_t R;
+    int64_t nbytes;          // symbol size (even)
+    int64_t nchunks;         // filled by launch_apply
+    int32_t mode;            // m<=8 inner loop: 0 = register nibble tables, 1 = SGPR-masked multiples
+};
+
+int apply_tile_rows(int m, int R);
+int64_t apply_chunk_bytes(int m);
+hipError_t launch_apply(int m, int rt, ApplyArgs a, int64_t n_stripes, hipStream_t st);
+hipError_t launch_gen_info(uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int k, int64_t stripe0,
+                           int64_t n_stripes, uint64_t seed, hipStream_t st);
+hipError_t launch_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int sym0,
+                              int nsym, int64_t n_stripes, unsigned long long* out, hipStream_t st);
+
+}  // namespace rsamd

@@ -1,0 +1,289 @@
+"""rs_amd -- Python host side of the MI355X Reed-Solomon engine (ctypes over librs_amd.so).
+
+Two layers, both thin wrappers over the C ABI (include/rs/reed_solomon.h, include/rs_amd/rsg.h):
+
+* ``RS``     -- mirror of the reference codec API (reference include/rs/reed_solomon.h:44-74):
+               ``generate_repair_symbols(inf, rep)`` and ``restore_symbols(k, r, rcv, is_erased, t)``
+               over lists of host symbols (numpy uint8 arrays), same return codes.
+* ``Codec``  -- the batched device-resident engine over torch tensors already in HBM
+               (shape [n_stripes, k + r, symbol_size] uint8 or explicit strides).
+
+There is no CPU fallback: if librs_amd.so is missing this module raises on import, and a codec
+cannot be created without a GPU.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librs_amd.so")
+
+RS_OK = 0
+RS_ERR_ALLOC = 1
+RS_ERR_INVALID = 2
+RS_ERR_DEVICE = 3
+RS_ERR_CANNOT_RESTORE = 100
+
+
+class RSError(RuntimeError):
+    def __init__(self, rc, what):
+        super().__init__(f"{what} failed with code {rc}")
+        self.rc = rc
+
+
+def build(force=False):
+    """Compile librs_amd.so in-tree (hipcc --offload-arch=gfx950)."""
+    import subprocess
+    if force:
+        subprocess.check_call(["make", "-s", "-C", HERE, "clean"])
+    subprocess.check_call(["make", "-s", "-j8", "-C", HERE])
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {HERE}` (no CPU fallback exists)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+P = ctypes.c_void_p
+u8, u16, u32, u64, i32, i64 = (ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.c_int32, ctypes.c_int64)
+
+
+class SymbolT(ctypes.Structure):  # include/memory/symbol.h
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8))]
+
+
+class SymbolSeqT(ctypes.Structure):  # include/memory/seq.h
+    _fields_ = [("length", ctypes.c_size_t), ("symbol_size", ctypes.c_size_t),
+                ("symbols", ctypes.POINTER(ctypes.POINTER(SymbolT)))]
+
+
+def _sig(name, restype, *argtypes):
+    f = getattr(_lib, name)
+    f.restype = restype
+    f.argtypes = list(argtypes)
+    return f
+
+
+_sig("rs_create", P)
+_sig("rs_destroy", None, P)
+_sig("rs_generate_repair_symbols", ctypes.c_int, P, ctypes.POINTER(SymbolSeqT), ctypes.POINTER(SymbolSeqT))
+_sig("rs_restore_symbols", ctypes.c_int, P, u16, u16, ctypes.POINTER(SymbolSeqT), P, u16)
+_sig("rsg_codec_create", ctypes.c_int, ctypes.c_int, u16, u16, ctypes.POINTER(P))
+_sig("rsg_codec_destroy", None, P)
+_sig("rsg_codec_subfield", ctypes.c_int, P)
+_sig("rsg_set_option", ctypes.c_int, P, ctypes.c_char_p, i64)
+_sig("rsg_last_kernel", ctypes.c_char_p, P)
+_sig("rsg_encode", ctypes.c_int, P, P, u64, u64, P, u64, u64, u64, u64, P)
+_sig("rsg_decode", ctypes.c_int, P, P, u64, u64, u64, u64, P, u16, P)
+_sig("rsg_fill_info", ctypes.c_int, P, u64, u64, u64, u16, u64, u64, u64, P)
+_sig("rsg_fingerprint", ctypes.c_int, P, u64, u64, u64, u32, u32, u64, P, P)
+_sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
+_sig("rsg_jit_precompile", ctypes.c_int, u16, u16, P, u16)
+_sig("rsg_gamma_tables", ctypes.c_int, P, P, P)
+_sig("rsg_version", ctypes.c_char_p)
+_sig("gf_create", P)
+_sig("gf_destroy", None, P)
+_sig("gf_mul_ee", u16, P, u16, u16)
+_sig("gf_div_ee", u16, P, u16, u16)
+_sig("gf_get_normal_repr", u16, P, u8, u16)
+_sig("gf_get_normal_basis_element", u16, P, u8, u8)
+_sig("cc_create", P)
+_sig("cc_destroy", None, P)
+_sig("cc_get_coset_size", u8, u16)
+_sig("cc_estimate_cosets_cnt", None, u16, u16, P, P)
+_sig("cc_select_cosets", None, P, u16, u16, P, u16, P, P, u16, P)
+_sig("cc_cosets_to_positions", None, P, u16, P, u16)
+
+lib = _lib
+
+
+def _np_ptr(a):
+    return a.ctypes.data_as(P) if a is not None else None
+
+
+def version():
+    return _lib.rsg_version().decode()
+
+
+# ------------------------------------------------------------------------------ host-only helpers
+def coding_matrix(k, r, is_erased=None):
+    """(matrix[rows, cols] uint16, in_slots, out_slots) exactly as the GPU engine applies them."""
+    er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
+    t = 0 if er is None else int(er.sum())
+    rows, cols = u32(), u32()
+    rc = _lib.rsg_coding_matrix(k, r, _np_ptr(er), t, None, ctypes.byref(rows), ctypes.byref(cols), None, None)
+    if rc:
+        raise RSError(rc, "rsg_coding_matrix")
+    M = np.zeros((rows.value, cols.value), np.uint16)
+    ins = np.zeros(cols.value, np.int32)
+    outs = np.zeros(rows.value, np.int32)
+    rc = _lib.rsg_coding_matrix(k, r, _np_ptr(er), t, _np_ptr(M), None, None, _np_ptr(ins), _np_ptr(outs))
+    if rc:
+        raise RSError(rc, "rsg_coding_matrix")
+    return M, ins, outs
+
+
+def gamma_tables():
+    lbyte = np.zeros((2, 256), np.uint16)
+    ibyte = np.zeros((2, 256), np.uint16)
+    red = np.zeros(1, np.uint8)
+    _lib.rsg_gamma_tables(_np_ptr(lbyte), _np_ptr(ibyte), _np_ptr(red))
+    return lbyte, ibyte, int(red[0])
+
+
+def jit_precompile(k, r, is_erased=None):
+    er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
+    t = 0 if er is None else int(er.sum())
+    rc = _lib.rsg_jit_precompile(k, r, _np_ptr(er), t)
+    if rc:
+        raise RSError(rc, "rsg_jit_precompile")
+
+
+def bench_pattern(k, r):
+    """t = r erasures of information symbols at i * (k // r)."""
+    er = np.zeros(k + r, np.bool_)
+    step = max(k // r, 1) if r else 1
+    er[[i * step for i in range(r)]] = True
+    return er
+
+
+# ------------------------------------------------------------------------------ drop-in mirror
+class _SeqBuf:
+    """symbol_seq_t view over a list of numpy uint8 arrays (kept alive by this object)."""
+
+    def __init__(self, arrays, symbol_size):
+        self.arrays = arrays
+        self.syms = (SymbolT * max(len(arrays), 1))()
+        for i, a in enumerate(arrays):
+            assert a.dtype == np.uint8 and a.flags.c_contiguous and a.size >= symbol_size
+            self.syms[i].data = a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        self.ptrs = (ctypes.POINTER(SymbolT) * max(len(arrays), 1))()
+        for i in range(len(arrays)):
+            self.ptrs[i] = ctypes.pointer(self.syms[i])
+        self.seq = SymbolSeqT(len(arrays), symbol_size, self.ptrs)
+
+
+class RS:
+    """Mirror of the reference context API (reference include/rs/reed_solomon.h:44-74)."""
+
+    def __init__(self):
+        self._h = _lib.rs_create()
+        if not self._h:
+            raise RSError(RS_ERR_DEVICE, "rs_create (no usable GPU?)")
+
+    def close(self):
+        if self._h:
+            _lib.rs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def generate_repair_symbols(self, inf_symbols, rep_symbols):
+        """inf_symbols: k host symbols, rep_symbols: r host symbols (written). Returns the C rc."""
+        S = inf_symbols[0].size if len(inf_symbols) else rep_symbols[0].size
+        a, b = _SeqBuf(list(inf_symbols), S), _SeqBuf(list(rep_symbols), S)
+        return _lib.rs_generate_repair_symbols(self._h, ctypes.byref(a.seq), ctypes.byref(b.seq))
+
+    def restore_symbols(self, k, r, rcv_symbols, is_erased, t):
+        """rcv_symbols: k + r host symbols, erased ones zero; restored in place. Returns the C rc."""
+        S = rcv_symbols[0].size
+        a = _SeqBuf(list(rcv_symbols), S)
+        er = np.ascontiguousarray(is_erased, dtype=np.bool_)
+        return _lib.rs_restore_symbols(self._h, k, r, ctypes.byref(a.seq), _np_ptr(er), t)
+
+
+# ------------------------------------------------------------------------------ device engine
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return P(stream.cuda_stream) if hasattr(stream, "cuda_stream") else P(stream)
+
+
+class Codec:
+    """Batched (k, r) engine on one GPU. Buffers are torch uint8 CUDA tensors (or raw pointers)."""
+
+    def __init__(self, k, r, device=0, jit=False, m8_mode=None):
+        self.k, self.r, self.device = k, r, device
+        h = P()
+        rc = _lib.rsg_codec_create(device, k, r, ctypes.byref(h))
+        if rc:
+            raise RSError(rc, f"rsg_codec_create({k}, {r})")
+        self._h = h
+        if jit:
+            self.set_option("jit", 1)
+        if m8_mode is not None:
+            self.set_option("m8_mode", m8_mode)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.rsg_codec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def subfield(self):
+        return _lib.rsg_codec_subfield(self._h)
+
+    @property
+    def last_kernel(self):
+        return _lib.rsg_last_kernel(self._h).decode()
+
+    def set_option(self, name, value):
+        rc = _lib.rsg_set_option(self._h, name.encode(), int(value))
+        if rc:
+            raise RSError(rc, f"rsg_set_option({name})")
+
+    def encode(self, stripes, n_stripes=None, symbol_size=None, stream=None, check=True):
+        """Repair symbols of `stripes` ([n, k + r, S] uint8, contiguous, on this device), in place."""
+        n, nsym, S = stripes.shape
+        assert nsym == self.k + self.r and stripes.is_contiguous()
+        base = stripes.data_ptr()
+        rc = _lib.rsg_encode(self._h, P(base), nsym * S, S, P(base + self.k * S), nsym * S, S,
+                             n if n_stripes is None else n_stripes, S if symbol_size is None else symbol_size,
+                             _stream_ptr(stream))
+        if check and rc:
+            raise RSError(rc, "rsg_encode")
+        return rc
+
+    def decode(self, stripes, is_erased, stream=None, check=True):
+        """Restore erased information symbols of `stripes` ([n, k + r, S]) in place."""
+        n, nsym, S = stripes.shape
+        assert nsym == self.k + self.r and stripes.is_contiguous()
+        er = np.ascontiguousarray(is_erased, dtype=np.bool_)
+        rc = _lib.rsg_decode(self._h, P(stripes.data_ptr()), nsym * S, S, n, S, _np_ptr(er), int(er.sum()),
+                             _stream_ptr(stream))
+        if check and rc not in (0,):
+            raise RSError(rc, "rsg_decode")
+        return rc
+
+    def encode_raw(self, d_info, info_stripe, info_sym, d_rep, rep_stripe, rep_sym, n, S, stream):
+        return _lib.rsg_encode(self._h, P(d_info), info_stripe, info_sym, P(d_rep), rep_stripe, rep_sym, n, S,
+                               _stream_ptr(stream))
+
+    def decode_raw(self, d_rcv, stripe_stride, sym_stride, n, S, is_erased, stream):
+        er = np.ascontiguousarray(is_erased, dtype=np.bool_)
+        return _lib.rsg_decode(self._h, P(d_rcv), stripe_stride, sym_stride, n, S, _np_ptr(er), int(er.sum()),
+                               _stream_ptr(stream))
+
+
+def fill_info(stripes, k, seed, stripe0=0, stream=None):
+    """Counter-based synthetic information symbols (same bytes as tests/_util.py:gen_info)."""
+    n, nsym, S = stripes.shape
+    rc = _lib.rsg_fill_info(P(stripes.data_ptr()), nsym * S, S, S, k, stripe0, n, seed, _stream_ptr(stream))
+    if rc:
+        raise RSError(rc, "rsg_fill_info")
+
+
+def fingerprint(stripes, sym0, nsym, out, stream=None):
+    """Per-stripe 64-bit fingerprint of symbols [sym0, sym0 + nsym) into `out` (int64 CUDA tensor [n])."""
+    n, total, S = stripes.shape
+    rc = _lib.rsg_fingerprint(P(stripes.data_ptr()), total * S, S, S, sym0, nsym, n, P(out.data_ptr()),
+                              _stream_ptr(stream))
+    if rc:
+        raise RSError(rc, "rsg_fingerprint")

@@ -175,3 +175,45 @@ def run_case_oracle(c):
             rc = oracle_decode(k, r, buf, er, c["t"])
             outs.append(buf.tobytes())
     return rc, b"".join(outs)
+
+
+# ---------------------------------------------------------------- numpy GF(2^16) (test-side)
+_GF = None
+
+
+def gf_tables():
+    """exp[2N], log[65536] for x^16 + x^5 + x^3 + x^2 + 1 (reference gf65536.c:59-88)."""
+    global _GF
+    if _GF is None:
+        N = 65535
+        exp = np.zeros(2 * N, np.int64)
+        v = 1
+        for i in range(N):
+            exp[i] = v
+            v <<= 1
+            if v & 0x10000:
+                v ^= 0x1002D
+        exp[N:] = exp[:N]
+        log = np.zeros(65536, np.int64)
+        log[exp[:N]] = np.arange(N)
+        _GF = (exp, log)
+    return _GF
+
+
+def gf_apply(M, X):
+    """out[p] = sum_i M[p, i] * X[i] over GF(2^16); M [R, K] uint16, X [K, W] uint16 -> [R, W]."""
+    exp, log = gf_tables()
+    R, K = M.shape
+    out = np.zeros((R, X.shape[1]), np.uint16)
+    lm = log[M.astype(np.int64)]
+    for i in range(K):
+        x = X[i].astype(np.int64)
+        nz = x != 0
+        if not nz.any():
+            continue
+        lx = log[x]
+        prod = exp[(lm[:, i:i + 1] + lx[None, :]) % 65535].astype(np.uint16)
+        prod[:, ~nz] = 0
+        prod[M[:, i] == 0] = 0
+        out ^= prod
+    return out

@@ -1,0 +1,185 @@
+"""CPU tests of the product library's host side: the C ABI loads and exports every declared entry
+point, the coding matrices equal the reference's linear maps (golden fixtures), the GF(256)^2
+coordinate arithmetic of the m <= 8 kernels is exact, and the hiprtc specialiser compiles.
+No GPU compute is called here."""
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import rs_amd
+from _util import REPO, case, case_inputs, check_golden, gf_apply, gf_tables, manifest, run_case_oracle
+
+HEADERS = ["include/rs/reed_solomon.h", "include/rs/gf65536.h", "include/rs/cyclotomic_coset.h",
+           "include/memory/seq.h", "include/memory/symbol.h", "include/rs_amd/rsg.h"]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(os.path.join(REPO, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 30, names
+    missing = [n for n in names if not hasattr(rs_amd.lib, n)]
+    assert not missing, missing
+
+
+def test_scalar_kats_through_library():
+    L = rs_amd.lib
+    gf = L.gf_create()
+    try:
+        assert L.gf_mul_ee(gf, 31981, 38739) == 42167
+        assert L.gf_mul_ee(gf, 58263, 29917) == 33120
+        assert L.gf_div_ee(gf, 12320, 29623) == 11439
+        assert L.gf_div_ee(gf, 5768, 15888) == 24163
+        assert L.gf_get_normal_basis_element(gf, 8, 0) == 16402
+    finally:
+        L.gf_destroy(gf)
+    assert L.cc_get_coset_size(21845) == 2 and L.cc_get_coset_size(257) == 8 and L.cc_get_coset_size(1) == 16
+
+
+def _select(k, r):
+    L = rs_amd.lib
+    ci, cr = np.zeros(1, np.uint16), np.zeros(1, np.uint16)
+    L.cc_estimate_cosets_cnt(k, r, ci.ctypes.data, cr.ctypes.data)
+    inf = np.zeros(int(ci[0]) * 2, np.uint16)  # coset_t = {u16 leader, u8 size} padded to 4 bytes
+    rep = np.zeros(int(cr[0]) * 2, np.uint16)
+    ni, nr = np.zeros(1, np.uint16), np.zeros(1, np.uint16)
+    cc = L.cc_create()
+    L.cc_select_cosets(cc, k, r, inf.ctypes.data, int(ci[0]), ni.ctypes.data, rep.ctypes.data, int(cr[0]),
+                       nr.ctypes.data)
+    L.cc_destroy(cc)
+    f = lambda a, n: [(int(a[2 * i]), int(a[2 * i + 1] & 0xFF)) for i in range(int(n[0]))]
+    return f(inf, ni), f(rep, nr)
+
+
+def test_cc_select_cosets_kat_through_library():
+    # test/src/rs/cyclotomic_coset/test_cc_select_cosets.c:107-187
+    assert _select(16, 3) == ([(257, 8), (4369, 4), (13107, 4)], [(21845, 2), (0, 1)])
+    assert _select(22, 17) == ([(771, 8), (1285, 8), (30583, 4), (21845, 2)],
+                               [(257, 8), (4369, 4), (13107, 4), (0, 1)])
+
+
+@pytest.mark.parametrize("name,k,r", [("gmat_4_2", 4, 2), ("gmat_10_4", 10, 4), ("gmat_128_32", 128, 32),
+                                      ("gmat_4096_1024", 4096, 1024)])
+def test_encode_matrix_matches_reference(name, k, r):
+    # golden = reference encode of unit vectors: repair word i of row p is G[p][i]
+    M, ins, outs = rs_amd.coding_matrix(k, r)
+    assert M.shape == (r, k) and (ins == np.arange(k)).all() and (outs == np.arange(r)).all()
+    check_golden(case(name), M.astype("<u2").tobytes())
+
+
+@pytest.mark.parametrize("name", ["dmat_128_32_bench", "dmat_128_32_rand"])
+def test_decode_matrix_matches_reference(name):
+    c = case(name)
+    k, r = c["k"], c["r"]
+    buf, er = case_inputs(c, 0)
+    M, ins, outs = rs_amd.coding_matrix(k, r, er)
+    words = buf.view("<u2").copy()  # [k+r][k+r]: unit words at the survivors
+    for row, slot in enumerate(outs):
+        words[slot] = 0
+        words[slot, ins] = M[row]
+    check_golden(c, words.astype("<u2").tobytes())
+
+
+def _apply_case(c):
+    """Apply the engine's matrices with numpy GF arithmetic to a golden case's inputs."""
+    k, r, S = c["k"], c["r"], c["S"]
+    outs_all = []
+    rc = 0
+    for s in range(c["n"]):
+        buf, er = case_inputs(c, s)
+        W = buf.view("<u2")
+        if c["op"] in ("encode", "encode_iota", "gmatrix"):
+            if r:
+                M, ins, outs = rs_amd.coding_matrix(k, r)
+                W[k:] = gf_apply(M, W[:k])
+            outs_all.append(buf[k:].tobytes())
+            continue
+        if c["op"] == "decode":
+            M, ins, outs = rs_amd.coding_matrix(k, r)
+            W[k:] = gf_apply(M, W[:k])
+            buf[er] = 0
+        if c["t"] > r:
+            rc = 100
+        elif er[:k].any():
+            M, ins, outs = rs_amd.coding_matrix(k, r, er)
+            W[outs] = gf_apply(M, W[ins])
+        outs_all.append(buf.tobytes())
+    return rc, b"".join(outs_all)
+
+
+NP_CASES = [c["name"] for c in manifest()["cases"]
+            if c["k"] * max(c["r"], 1) * c["S"] * c["n"] <= 40_000_000 and not c["name"].startswith("gmat")]
+
+
+@pytest.mark.parametrize("name", NP_CASES)
+def test_matrix_apply_equals_reference(name):
+    """The engine's linear maps reproduce every golden vector (CPU emulation of what the GPU applies)."""
+    c = case(name)
+    rc, out = _apply_case(c)
+    assert rc == c["rc"]
+    check_golden(c, out)
+
+
+def test_gf256_coordinate_arithmetic():
+    """The m <= 8 kernels' arithmetic: L (alpha basis -> GF(256)^2 bytes), multiplication of a byte by a
+    GF(256) coefficient through gamma-multiples and nibble tables, L^-1 -- equals field multiplication."""
+    lbyte, ibyte, red = rs_amd.gamma_tables()
+    assert red == 0x1D
+    exp, log = gf_tables()
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 65536, 4096).astype(np.int64)
+    L = lbyte[0][x & 255].astype(np.int64) ^ lbyte[1][x >> 8]
+
+    def xt(b):
+        return ((b << 1) & 0xFE) ^ np.where(b & 0x80, red, 0)
+
+    for e in rng.integers(0, 255, 64):
+        c = int(exp[257 * int(e)])  # a GF(256) element
+        cb = int(lbyte[0][c & 255] ^ lbyte[1][c >> 8])
+        assert cb < 256
+        m = [L & 0xFF, L >> 8]
+        mult = [[mm] for mm in m]
+        for j in range(1, 8):
+            for h in range(2):
+                mult[h].append(xt(mult[h][-1]))
+        prod = [np.zeros_like(x), np.zeros_like(x)]
+        for h in range(2):
+            for j in range(8):
+                if cb >> j & 1:
+                    prod[h] ^= mult[h][j]
+        u = prod[0] | (prod[1] << 8)
+        y = ibyte[0][u & 255].astype(np.int64) ^ ibyte[1][u >> 8]
+        want = np.where(x == 0, 0, exp[(log[c] + log[x]) % 65535])
+        assert (y == want).all()
+
+
+def test_jit_precompile_offline(tmp_path, monkeypatch):
+    """The hiprtc specialiser generates and compiles a gfx950 code object without a GPU."""
+    monkeypatch.setenv("RS_AMD_JIT_CACHE", str(tmp_path))
+    rs_amd.jit_precompile(10, 4)
+    er = rs_amd.bench_pattern(10, 4)
+    rs_amd.jit_precompile(10, 4, er)
+    files = list(tmp_path.glob("*.co"))
+    assert len(files) == 2 and all(f.stat().st_size > 1000 for f in files)
+
+
+def test_invalid_arguments():
+    with pytest.raises(rs_amd.RSError) as e:
+        rs_amd.coding_matrix(65000, 1000)
+    assert e.value.rc == rs_amd.RS_ERR_INVALID
+    er = np.zeros(6, bool)
+    er[:3] = True
+    with pytest.raises(rs_amd.RSError) as e:
+        rs_amd.coding_matrix(4, 2, er)
+    assert e.value.rc == rs_amd.RS_ERR_CANNOT_RESTORE
