@@ -43,8 +43,8 @@ def parse():
     ap.add_argument("--r", type=int, default=32)
     ap.add_argument("--symbol", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
-    ap.add_argument("--kernel", default="jit", choices=["jit", "table", "mask"])
-    ap.add_argument("--cpu-stripes", type=int, default=64, help="CPU-baseline sample (stripes)")
+    ap.add_argument("--kernel", default="idx", choices=["idx", "table", "mask", "jit"])
+    ap.add_argument("--cpu-stripes", type=int, default=192, help="CPU-baseline sample (stripes)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="skip verification/CPU legs (profilers)")
@@ -163,7 +163,7 @@ def main():
     erased = rs_amd.bench_pattern(k, r)
     t = int(erased.sum())
     codec = rs_amd.Codec(k, r, device=local, jit=args.kernel == "jit",
-                         m8_mode={"table": 0, "mask": 1}.get(args.kernel))
+                         m8_mode={"table": 0, "mask": 1, "idx": 2}.get(args.kernel))
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     rs_amd.fill_info(stripes, k, SEED, stripe0=rank * n, stream=stream)

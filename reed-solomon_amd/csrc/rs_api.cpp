@@ -84,6 +84,7 @@ struct DevPlan {
     int32_t* d_in = nullptr;
     int32_t* d_out = nullptr;
     uint32_t* d_coef = nullptr;
+    uint32_t* d_idx = nullptr;  // m8, rt 32: pre-split nibble indices for the asm kernel
     std::vector<uint16_t> matrix;  // R x K, GF(2^16)
     std::vector<int32_t> in_slots, out_slots;
     std::unique_ptr<JitKernel> jit;  // matrix-specialised kernel, if built
@@ -94,6 +95,7 @@ struct DevPlan {
         (void)hipFree(d_in);
         (void)hipFree(d_out);
         (void)hipFree(d_coef);
+        (void)hipFree(d_idx);
         (void)hipSetDevice(cur);
     }
 };
@@ -139,6 +141,17 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     }
     out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
     int rc;
+    if (p->m == 8 && rt == 32) {
+        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 64, 0);
+        for (int t = 0; t < p->ntiles; ++t)
+            for (int i = 0; i < K; ++i)
+                for (int j = 0; j < 32; ++j) {
+                    const uint32_t c = (coef[(size_t(t) * K + i) * 8 + j / 4] >> (8 * (j % 4))) & 0xFF;
+                    idx[(size_t(t) * K + i) * 64 + 2 * j] = c & 15;
+                    idx[(size_t(t) * K + i) * 64 + 2 * j + 1] = c >> 4;
+                }
+        if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
+    }
     if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_coef), coef.data(), coef.size() * 4))) return rc;
@@ -161,7 +174,7 @@ struct rsg_codec {
     std::unique_ptr<DevPlan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<DevPlan>> dec;
     std::vector<std::vector<uint8_t>> dec_lru;
-    int m8_mode = 1;
+    int m8_mode = 2;
     int jit = 0;
     std::string last_kernel = "none";
 };
@@ -229,7 +242,7 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value != 0 && value != 1) return RS_ERR_INVALID;
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->m8_mode = int(value);
         return 0;
     }
@@ -271,11 +284,13 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.dst_sym = dst_sym;
     a.out_idx = p.d_out;
     a.coef = p.d_coef;
+    a.idx = p.d_idx;
     a.ltab = c->d_ltab;
     a.K = p.K;
     a.R = p.R;
     a.nbytes = int64_t(S);
     a.mode = c->m8_mode;
+    if (a.mode == 2 && !(p.m == 8 && p.rt == 32)) a.mode = 0;
     c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(p.rt) + "_mode" + std::to_string(a.mode))
                               : (std::string("apply_m16_rt") + std::to_string(p.rt));
     HIP_TRY(launch_apply(p.m, p.rt, a, int64_t(n_stripes), st));

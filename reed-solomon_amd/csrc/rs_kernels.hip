@@ -105,6 +105,101 @@ __global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------ m <= 8, asm
+// Same math as k_apply_m8<32, 0>, but the (output x nibble) lookups are one hand-scheduled block
+// (csrc/gen_asm.py): the wave enters gpr-index mode once per half, reads pre-split table indices
+// from SGPRs filled by SMEM loads, and retargets the index with one s_set_gpr_idx_idx per lookup
+// pair, so each output costs 2 SALU + 4 VALU instead of ~12 SALU with compiler lowering (the
+// scalar unit, shared by the CU's four SIMDs, was the bottleneck). Tables and accumulators are
+// pinned to fixed VGPRs by the constraints below.
+// One input step of k_apply_m8_idx: coordinates, gamma-multiples, nibble tables, then the asm block.
+__device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (&x)[2], const uint32_t* cp,
+                                            u32x16& a0l, u32x16& a0h, u32x16& a1l, u32x16& a1h) {
+    uint32_t m[2][8];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        m[v][0] = lds_lookup4(lt, x[v]);
+#pragma unroll
+        for (int j = 1; j < 8; ++j) m[v][j] = xt8(m[v][j - 1]);
+    }
+    const u32x16 Tl0 = build16(m[0][0], m[0][1], m[0][2], m[0][3]);
+    const u32x16 Th0 = build16(m[0][4], m[0][5], m[0][6], m[0][7]);
+    const u32x16 Tl1 = build16(m[1][0], m[1][1], m[1][2], m[1][3]);
+    const u32x16 Th1 = build16(m[1][4], m[1][5], m[1][6], m[1][7]);
+    asm volatile(
+#include "gen/m8_idx_asm.inc"
+        : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h)
+        : "{v[8:23]}"(Tl0), "{v[24:39]}"(Th0), "{v[40:55]}"(Tl1), "{v[56:71]}"(Th1), [cp] "s"(cp)
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "memory");
+}
+
+// Input loop with a two-deep load ring. FULL: the whole 2 KiB chunk lies inside the symbol (the
+// common case, decided per block), so loads are plain 8-byte loads without bounds checks.
+template <bool FULL>
+__device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* __restrict__ in_idx, const uint32_t* lt,
+                                            const uint8_t* src, int64_t avail, const uint32_t* cbase, u32x16& a0l,
+                                            u32x16& a0h, u32x16& a1l, u32x16& a1h) {
+    auto load = [&](uint32_t (&dst)[2], int i) {
+        const uint8_t* p = src + int64_t(in_idx[i]) * a.src_sym;
+        if constexpr (FULL) {
+            const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+            dst[0] = v.x;
+            dst[1] = v.y;
+        } else {
+            load_slice<8>(dst, p, avail);
+        }
+    };
+    const int K = a.K;
+    uint32_t b0[2] = {0, 0}, b1[2] = {0, 0};
+    if (K > 0) load(b0, 0);
+    if (K > 1) load(b1, 1);
+    for (int i = 0; i < K; i += 2) {
+        {
+            const uint32_t x[2] = {b0[0], b0[1]};
+            if (i + 2 < K) load(b0, i + 2);
+            m8_idx_step(lt, x, cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
+        }
+        if (i + 1 < K) {
+            const uint32_t x[2] = {b1[0], b1[1]};
+            if (i + 3 < K) load(b1, i + 3);
+            m8_idx_step(lt, x, cbase + size_t(i + 1) * 64, a0l, a0h, a1l, a1h);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t* __restrict__ in_idx) {
+    __shared__ uint32_t lt[2048];
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+
+    const int64_t bid = blockIdx.x;
+    const int64_t stripe = bid / a.nchunks;
+    const int64_t chunk0 = (bid - stripe * a.nchunks) * 2048;
+    const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
+    const int64_t avail = a.nbytes - col;
+    const int tile = blockIdx.y;
+    const uint8_t* src = a.src + stripe * a.src_stripe + col;
+    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 64;
+
+    u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
+    if (chunk0 + 2048 <= a.nbytes)
+        m8_idx_body<true>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
+    else if (avail > 0)
+        m8_idx_body<false>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
+    if (avail <= 0) return;
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+    const int rows = min(32, a.R - tile * 32);
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            const uint32_t v0 = p < 16 ? a0l[p & 15] : a0h[p & 15];
+            const uint32_t v1 = p < 16 ? a1l[p & 15] : a1h[p & 15];
+            uint32_t y[2] = {lds_lookup4(lt + 1024, v0), lds_lookup4(lt + 1024, v1)};
+            store_slice<8>(dst + int64_t(a.out_idx[tile * 32 + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------ m = 16
 // Block = 256 lanes x 4 bytes = 1 KiB of columns, RT outputs of tile blockIdx.y.
 template <int RT>
@@ -202,7 +297,9 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
 template <int RT>
 static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
-    if (a.mode == 1)
+    if (RT == 32 && a.mode == 2 && a.idx)
+        hipLaunchKernelGGL(k_apply_m8_idx, grid, dim3(256), 0, st, a, a.in_idx);
+    else if (a.mode == 1)
         hipLaunchKernelGGL((k_apply_m8<RT, 1>), grid, dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL((k_apply_m8<RT, 0>), grid, dim3(256), 0, st, a);

@@ -16,12 +16,14 @@ struct ApplyArgs {
     int64_t dst_sym;
     const int32_t* out_idx;  // [R] output symbol indices (device)
     const uint32_t* coef;    // [ntiles][K][RT/4] gamma-basis bytes (m<=8) | [ntiles][K][RT/2] u16 (m=16)
+    const uint32_t* idx;     // m<=8, RT=32, mode 2: [ntiles][K][64] pre-split nibble indices (lo, hi per output)
     const uint32_t* ltab;    // m<=8: [2048] LDS coordinate tables (L bytes 0..3, L^-1 bytes 0..3)
     int32_t K;
     int32_t R;
     int64_t nbytes;          // symbol size (even)
     int64_t nchunks;         // filled by launch_apply
-    int32_t mode;            // m<=8 inner loop: 0 = register nibble tables, 1 = SGPR-masked multiples
+    int32_t mode;            // m<=8 inner loop: 0 = register nibble tables (compiler indexing),
+                             //   1 = SGPR-masked multiples, 2 = hand-scheduled gpr-index block (RT=32)
 };
 
 int apply_tile_rows(int m, int R);

@@ -12,7 +12,7 @@ from _util import case, case_inputs, check_golden, gen_info, manifest, oracle_de
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = {"table": dict(m8_mode=0), "mask": dict(m8_mode=1), "jit": dict(jit=True)}
+VARIANTS = {"idx": dict(m8_mode=2), "table": dict(m8_mode=0), "mask": dict(m8_mode=1), "jit": dict(jit=True)}
 
 
 def _pad(S):
