@@ -142,20 +142,22 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
     int rc;
     if (p->m == 8 && rt == 32) {
-        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 64, 0);
+        // k_apply_m8_idx record per (tile, input): 32 dwords, output j -> lo nibble | hi nibble << 16
+        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 32, 0);
         for (int t = 0; t < p->ntiles; ++t)
             for (int i = 0; i < K; ++i)
                 for (int j = 0; j < 32; ++j) {
                     const uint32_t c = (coef[(size_t(t) * K + i) * 8 + j / 4] >> (8 * (j % 4))) & 0xFF;
-                    idx[(size_t(t) * K + i) * 64 + 2 * j] = c & 15;
-                    idx[(size_t(t) * K + i) * 64 + 2 * j + 1] = c >> 4;
+                    idx[(size_t(t) * K + i) * 32 + j] = (c & 15) | ((c >> 4) << 16);
                 }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
     }
+    in_slots.resize(in_slots.size() + 8, 0);  // kernels read slot indices in vectors past the end
     if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_coef), coef.data(), coef.size() * 4))) return rc;
     p->matrix = std::move(M);
+    in_slots.resize(size_t(K));
     p->in_slots = std::move(in_slots);
     p->out_slots = std::move(out_slots);
     out = std::move(p);

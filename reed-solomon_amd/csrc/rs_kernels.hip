@@ -112,35 +112,33 @@ __global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
 // pair, so each output costs 2 SALU + 4 VALU instead of ~12 SALU with compiler lowering (the
 // scalar unit, shared by the CU's four SIMDs, was the bottleneck). Tables and accumulators are
 // pinned to fixed VGPRs by the constraints below.
-// One input step of k_apply_m8_idx: coordinates, gamma-multiples, nibble tables, then the asm block.
+// One input step of k_apply_m8_idx: LDS coordinate lookup, then the asm block (multiples, tables,
+// 32 outputs x 2 dwords of indexed XORs).
 __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (&x)[2], const uint32_t* cp,
                                             u32x16& a0l, u32x16& a0h, u32x16& a1l, u32x16& a1h) {
-    uint32_t m[2][8];
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-        m[v][0] = lds_lookup4(lt, x[v]);
-#pragma unroll
-        for (int j = 1; j < 8; ++j) m[v][j] = xt8(m[v][j - 1]);
-    }
-    const u32x16 Tl0 = build16(m[0][0], m[0][1], m[0][2], m[0][3]);
-    const u32x16 Th0 = build16(m[0][4], m[0][5], m[0][6], m[0][7]);
-    const u32x16 Tl1 = build16(m[1][0], m[1][1], m[1][2], m[1][3]);
-    const u32x16 Th1 = build16(m[1][4], m[1][5], m[1][6], m[1][7]);
+    const uint32_t y0 = lds_lookup4(lt, x[0]), y1 = lds_lookup4(lt, x[1]);
+    uint32_t t0, t1, t2, t3;
+    u32x16 Tl0, Th0, Tl1, Th1;
     asm volatile(
 #include "gen/m8_idx_asm.inc"
-        : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h)
-        : "{v[8:23]}"(Tl0), "{v[24:39]}"(Th0), "{v[40:55]}"(Tl1), "{v[56:71]}"(Th1), [cp] "s"(cp)
-        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "memory");
+        : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h),
+          "=&{v[8:23]}"(Tl0), "=&{v[24:39]}"(Th0), "=&{v[40:55]}"(Tl1), "=&{v[56:71]}"(Th1),
+          [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
+        : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu)
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "memory");
 }
 
-// Input loop with a two-deep load ring. FULL: the whole 2 KiB chunk lies inside the symbol (the
-// common case, decided per block), so loads are plain 8-byte loads without bounds checks.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+// Input loop with a four-deep load ring (2 KiB in flight per wave: HBM latency under full load is
+// microseconds). Slot indices are fetched four at a time through SMEM. FULL: the whole 2 KiB chunk
+// lies inside the symbol (decided per block), so loads carry no bounds checks.
 template <bool FULL>
 __device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* __restrict__ in_idx, const uint32_t* lt,
                                             const uint8_t* src, int64_t avail, const uint32_t* cbase, u32x16& a0l,
                                             u32x16& a0h, u32x16& a1l, u32x16& a1h) {
-    auto load = [&](uint32_t (&dst)[2], int i) {
-        const uint8_t* p = src + int64_t(in_idx[i]) * a.src_sym;
+    auto load = [&](uint32_t (&dst)[2], int32_t slot) {
+        const uint8_t* p = src + int64_t(slot) * a.src_sym;
         if constexpr (FULL) {
             const u32x2 v = *reinterpret_cast<const u32x2*>(p);
             dst[0] = v.x;
@@ -150,19 +148,34 @@ __device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* _
         }
     };
     const int K = a.K;
-    uint32_t b0[2] = {0, 0}, b1[2] = {0, 0};
-    if (K > 0) load(b0, 0);
-    if (K > 1) load(b1, 1);
-    for (int i = 0; i < K; i += 2) {
+    uint32_t b0[2] = {0, 0}, b1[2] = {0, 0}, b2[2] = {0, 0}, b3[2] = {0, 0};
+    i32x4 sl = *reinterpret_cast<const i32x4*>(in_idx);  // in_idx is padded by >= 8 entries
+    if (K > 0) load(b0, sl.x);
+    if (K > 1) load(b1, sl.y);
+    if (K > 2) load(b2, sl.z);
+    if (K > 3) load(b3, sl.w);
+    for (int i = 0; i < K; i += 4) {
+        sl = *reinterpret_cast<const i32x4*>(in_idx + i + 4);
+        const uint32_t* cp = cbase + size_t(i) * 32;
         {
             const uint32_t x[2] = {b0[0], b0[1]};
-            if (i + 2 < K) load(b0, i + 2);
-            m8_idx_step(lt, x, cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
+            if (i + 4 < K) load(b0, sl.x);
+            m8_idx_step(lt, x, cp, a0l, a0h, a1l, a1h);
         }
         if (i + 1 < K) {
             const uint32_t x[2] = {b1[0], b1[1]};
-            if (i + 3 < K) load(b1, i + 3);
-            m8_idx_step(lt, x, cbase + size_t(i + 1) * 64, a0l, a0h, a1l, a1h);
+            if (i + 5 < K) load(b1, sl.y);
+            m8_idx_step(lt, x, cp + 32, a0l, a0h, a1l, a1h);
+        }
+        if (i + 2 < K) {
+            const uint32_t x[2] = {b2[0], b2[1]};
+            if (i + 6 < K) load(b2, sl.z);
+            m8_idx_step(lt, x, cp + 64, a0l, a0h, a1l, a1h);
+        }
+        if (i + 3 < K) {
+            const uint32_t x[2] = {b3[0], b3[1]};
+            if (i + 7 < K) load(b3, sl.w);
+            m8_idx_step(lt, x, cp + 96, a0l, a0h, a1l, a1h);
         }
     }
 }
@@ -179,7 +192,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t
     const int64_t avail = a.nbytes - col;
     const int tile = blockIdx.y;
     const uint8_t* src = a.src + stripe * a.src_stripe + col;
-    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 64;
+    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 32;
 
     u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
     if (chunk0 + 2048 <= a.nbytes)
