@@ -142,17 +142,18 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
     int rc;
     if (p->m == 8 && rt == 32) {
-        // k_apply_m8_idx record per (tile, input): 32 dwords, output j -> lo nibble | hi nibble << 16
-        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 32, 0);
+        // k_apply_m8_idx record per (tile, input): 64 dwords, [2j] = lo, [2j + 1] = hi nibble of output j
+        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 64, 0);
         for (int t = 0; t < p->ntiles; ++t)
             for (int i = 0; i < K; ++i)
                 for (int j = 0; j < 32; ++j) {
                     const uint32_t c = (coef[(size_t(t) * K + i) * 8 + j / 4] >> (8 * (j % 4))) & 0xFF;
-                    idx[(size_t(t) * K + i) * 32 + j] = (c & 15) | ((c >> 4) << 16);
+                    idx[(size_t(t) * K + i) * 64 + 2 * j] = c & 15;
+                    idx[(size_t(t) * K + i) * 64 + 2 * j + 1] = c >> 4;
                 }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
     }
-    in_slots.resize(in_slots.size() + 8, 0);  // kernels read slot indices in vectors past the end
+    in_slots.resize(in_slots.size() + 16, 0);  // kernels read slot indices in vectors past the end
     if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
     if ((rc = upload(reinterpret_cast<void**>(&p->d_coef), coef.data(), coef.size() * 4))) return rc;
@@ -244,7 +245,7 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        if (value < 0 || (value > 4 && value < 10) || value > 14) return RS_ERR_INVALID;
         c->m8_mode = int(value);
         return 0;
     }
@@ -292,7 +293,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.R = p.R;
     a.nbytes = int64_t(S);
     a.mode = c->m8_mode;
-    if (a.mode == 2 && !(p.m == 8 && p.rt == 32)) a.mode = 0;
+    if (a.mode >= 2 && !(p.m == 8 && p.rt == 32)) a.mode = 0;
     c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(p.rt) + "_mode" + std::to_string(a.mode))
                               : (std::string("apply_m16_rt") + std::to_string(p.rt));
     HIP_TRY(launch_apply(p.m, p.rt, a, int64_t(n_stripes), st));

@@ -114,26 +114,48 @@ __global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
 // pinned to fixed VGPRs by the constraints below.
 // One input step of k_apply_m8_idx: LDS coordinate lookup, then the asm block (multiples, tables,
 // 32 outputs x 2 dwords of indexed XORs).
+template <int ABL>
 __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (&x)[2], const uint32_t* cp,
                                             u32x16& a0l, u32x16& a0h, u32x16& a1l, u32x16& a1h) {
     const uint32_t y0 = lds_lookup4(lt, x[0]), y1 = lds_lookup4(lt, x[1]);
     uint32_t t0, t1, t2, t3;
     u32x16 Tl0, Th0, Tl1, Th1;
-    asm volatile(
+#define RS_M8_IDX_OPERANDS                                                                                     \
+    : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h), "=&{v[8:23]}"(Tl0),        \
+      "=&{v[24:39]}"(Th0), "=&{v[40:55]}"(Tl1), "=&{v[56:71]}"(Th1), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),  \
+      [t3] "=&v"(t3)                                                                                                  \
+    : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu)                                               \
+    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "memory"
+    if constexpr (ABL == 0) {
+        asm volatile(
 #include "gen/m8_idx_asm.inc"
-        : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h),
-          "=&{v[8:23]}"(Tl0), "=&{v[24:39]}"(Th0), "=&{v[40:55]}"(Tl1), "=&{v[56:71]}"(Th1),
-          [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
-        : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu)
-        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "memory");
+            RS_M8_IDX_OPERANDS);
+    } else if constexpr (ABL == 1) {
+        asm volatile(
+#include "gen/m8_idx_asm_noidx.inc"
+            RS_M8_IDX_OPERANDS);
+    } else if constexpr (ABL == 2) {
+        asm volatile(
+#include "gen/m8_idx_asm_build.inc"
+            RS_M8_IDX_OPERANDS);
+    } else if constexpr (ABL == 3) {
+        asm volatile(
+#include "gen/m8_idx_asm_look.inc"
+            RS_M8_IDX_OPERANDS);
+    } else {
+        asm volatile(
+#include "gen/m8_idx_asm_nop.inc"
+            RS_M8_IDX_OPERANDS);
+    }
+#undef RS_M8_IDX_OPERANDS
 }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
-// Input loop with a four-deep load ring (2 KiB in flight per wave: HBM latency under full load is
-// microseconds). Slot indices are fetched four at a time through SMEM. FULL: the whole 2 KiB chunk
-// lies inside the symbol (decided per block), so loads carry no bounds checks.
-template <bool FULL>
+// Input loop with a PD-deep load ring (PD x 512 B in flight per wave: HBM latency under full load
+// is microseconds). Slot indices are fetched four at a time through SMEM (in_idx is padded). FULL: the
+// whole 2 KiB chunk lies inside the symbol (decided per block), so loads carry no bounds checks.
+template <bool FULL, int ABL, int PD>
 __device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* __restrict__ in_idx, const uint32_t* lt,
                                             const uint8_t* src, int64_t avail, const uint32_t* cbase, u32x16& a0l,
                                             u32x16& a0h, u32x16& a1l, u32x16& a1h) {
@@ -148,41 +170,128 @@ __device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* _
         }
     };
     const int K = a.K;
-    uint32_t b0[2] = {0, 0}, b1[2] = {0, 0}, b2[2] = {0, 0}, b3[2] = {0, 0};
-    i32x4 sl = *reinterpret_cast<const i32x4*>(in_idx);  // in_idx is padded by >= 8 entries
-    if (K > 0) load(b0, sl.x);
-    if (K > 1) load(b1, sl.y);
-    if (K > 2) load(b2, sl.z);
-    if (K > 3) load(b3, sl.w);
-    for (int i = 0; i < K; i += 4) {
-        sl = *reinterpret_cast<const i32x4*>(in_idx + i + 4);
-        const uint32_t* cp = cbase + size_t(i) * 32;
-        {
-            const uint32_t x[2] = {b0[0], b0[1]};
-            if (i + 4 < K) load(b0, sl.x);
-            m8_idx_step(lt, x, cp, a0l, a0h, a1l, a1h);
+    uint32_t ring[PD][2];
+    int32_t sl[PD];
+#pragma unroll
+    for (int q = 0; q < PD / 4; ++q) {
+        const i32x4 v = *reinterpret_cast<const i32x4*>(in_idx + 4 * q);
+        sl[4 * q] = v.x, sl[4 * q + 1] = v.y, sl[4 * q + 2] = v.z, sl[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+        ring[j][0] = ring[j][1] = 0;
+        if (j < K) load(ring[j], sl[j]);
+    }
+    for (int i = 0; i < K; i += PD) {
+#pragma unroll
+        for (int q = 0; q < PD / 4; ++q) {
+            const i32x4 v = *reinterpret_cast<const i32x4*>(in_idx + i + PD + 4 * q);
+            sl[4 * q] = v.x, sl[4 * q + 1] = v.y, sl[4 * q + 2] = v.z, sl[4 * q + 3] = v.w;
         }
-        if (i + 1 < K) {
-            const uint32_t x[2] = {b1[0], b1[1]};
-            if (i + 5 < K) load(b1, sl.y);
-            m8_idx_step(lt, x, cp + 32, a0l, a0h, a1l, a1h);
-        }
-        if (i + 2 < K) {
-            const uint32_t x[2] = {b2[0], b2[1]};
-            if (i + 6 < K) load(b2, sl.z);
-            m8_idx_step(lt, x, cp + 64, a0l, a0h, a1l, a1h);
-        }
-        if (i + 3 < K) {
-            const uint32_t x[2] = {b3[0], b3[1]};
-            if (i + 7 < K) load(b3, sl.w);
-            m8_idx_step(lt, x, cp + 96, a0l, a0h, a1l, a1h);
+        const uint32_t* cp = cbase + size_t(i) * 64;
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+            if (i + j < K) {
+                const uint32_t x[2] = {ring[j][0], ring[j][1]};
+                if (i + j + PD < K) load(ring[j], sl[j]);
+                m8_idx_step<ABL>(lt, x, cp + 64 * j, a0l, a0h, a1l, a1h);
+            }
         }
     }
 }
 
-__global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t* __restrict__ in_idx) {
-    __shared__ uint32_t lt[2048];
-    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+// ------------------------------------------------------------------ m <= 8, asm + LDS-DMA ring
+// Input staging for full 2 KiB chunks: each input's chunk is copied HBM -> LDS by two
+// global_load_lds_dwordx4 (1 KiB, 16 B per lane) issued by one wave of the block (wave i % 4 owns
+// input i), RING_B batches of 4 inputs ahead. Completion: the issuing wave's counted
+// s_waitcnt vmcnt, then a raw s_barrier (one per batch); readers ds_read_b64 their 8 bytes.
+// Ring slot of input i = i % (4 * (RING_B + 1)): batch b + RING_B reuses batch b - 1's slots, which
+// every wave finished reading before the barrier that ended round b - 1.
+constexpr int RING_B = 3;
+constexpr int RING_SLOTS = 4 * (RING_B + 1);
+
+__device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds_byte)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most n of this wave's DMA instructions are outstanding (n even, 0..2*RING_B)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+    if (n <= 0)
+        wait_vm<0>();
+    else if (n <= 2)
+        wait_vm<2>();
+    else if (n <= 4)
+        wait_vm<4>();
+    else
+        wait_vm<6>();
+}
+
+template <int ABL>
+__device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* __restrict__ in_idx, uint32_t* lds,
+                                            const uint8_t* chunk_src, const uint32_t* cbase, u32x16& a0l,
+                                            u32x16& a0h, u32x16& a1l, u32x16& a1h) {
+    const uint32_t* lt = lds;
+    uint32_t* ring = lds + 2048;
+    const int K = a.K;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
+    const uint8_t* gl = chunk_src + 16 * lane;
+    auto issue = [&](int i) {  // wave-uniform: only the owning wave calls
+        const uint8_t* g = gl + int64_t(in_idx[i]) * a.src_sym;
+        const uint32_t dst = ring_lds + uint32_t(i % RING_SLOTS) * 2048u;
+        dma16(g, dst);
+        dma16(g + 1024, dst + 1024);
+    };
+    const int nb = (K + 3) / 4;
+    // outstanding DMA instructions of this wave for batches [lo, hi]
+    auto mine = [&](int lo, int hi) {
+        int c = 0;
+        for (int b = lo; b <= hi; ++b)
+            if (b < nb && 4 * b + wave < K) c += 2;
+        return c;
+    };
+    for (int b = 0; b < RING_B; ++b)
+        if (4 * b + wave < K) issue(4 * b + wave);
+    wait_vm_dyn(mine(1, RING_B - 1));
+    asm volatile("s_barrier" ::: "memory");
+    for (int b = 0; b < nb; ++b) {
+        const int ib = 4 * (b + RING_B) + wave;
+        if (ib < K) issue(ib);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * b + j;
+            if (i < K) {
+                const u32x2 v = *reinterpret_cast<const u32x2*>(
+                    reinterpret_cast<const uint8_t*>(ring) + (i % RING_SLOTS) * 2048 + 8 * threadIdx.x);
+                const uint32_t x[2] = {v.x, v.y};
+                m8_idx_step<ABL>(lt, x, cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
+            }
+        }
+        wait_vm_dyn(mine(b + 2, b + RING_B));
+        asm volatile("s_barrier" ::: "memory");
+    }
+}
+
+// Full 2 KiB chunks only (a.nchunks = full chunks per symbol); the tail chunk goes to k_apply_m8_idx.
+template <int ABL>
+__global__ void __launch_bounds__(256) k_apply_m8_lds(ApplyArgs a, const int32_t* __restrict__ in_idx) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2048 + RING_SLOTS * 512];
+    for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
     __syncthreads();
 
     const int64_t bid = blockIdx.x;
@@ -191,14 +300,43 @@ __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t
     const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
     const int64_t avail = a.nbytes - col;
     const int tile = blockIdx.y;
+    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 64;
+
+    u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
+    m8_lds_body<ABL>(a, in_idx, lds, a.src + stripe * a.src_stripe + chunk0, cbase, a0l, a0h, a1l, a1h);
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+    const int rows = min(32, a.R - tile * 32);
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            const uint32_t v0 = p < 16 ? a0l[p & 15] : a0h[p & 15];
+            const uint32_t v1 = p < 16 ? a1l[p & 15] : a1h[p & 15];
+            uint32_t y[2] = {lds_lookup4(lds + 1024, v0), lds_lookup4(lds + 1024, v1)};
+            store_slice<8>(dst + int64_t(a.out_idx[tile * 32 + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
+template <int ABL, int PD>
+__global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t* __restrict__ in_idx) {
+    __shared__ uint32_t lt[2048];
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+
+    const int64_t bid = blockIdx.x;
+    const int64_t stripe = bid / a.nchunks;
+    const int64_t chunk0 = (a.chunk_base + bid - stripe * a.nchunks) * 2048;
+    const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
+    const int64_t avail = a.nbytes - col;
+    const int tile = blockIdx.y;
     const uint8_t* src = a.src + stripe * a.src_stripe + col;
-    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 32;
+    const uint32_t* cbase = a.idx + size_t(tile) * a.K * 64;
 
     u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
     if (chunk0 + 2048 <= a.nbytes)
-        m8_idx_body<true>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
+        m8_idx_body<true, ABL, PD>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
     else if (avail > 0)
-        m8_idx_body<false>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
+        m8_idx_body<false, ABL, PD>(a, in_idx, lt, src, avail, cbase, a0l, a0h, a1l, a1h);
     if (avail <= 0) return;
     uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
     const int rows = min(32, a.R - tile * 32);
@@ -310,8 +448,39 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
 template <int RT>
 static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
-    if (RT == 32 && a.mode == 2 && a.idx)
-        hipLaunchKernelGGL(k_apply_m8_idx, grid, dim3(256), 0, st, a, a.in_idx);
+    if (RT == 32 && a.mode >= 2 && a.idx) {
+        // mode 2: production kernel (LDS-DMA ring over full chunks + register-ring tail);
+        // 3 / 4: register ring 4 / 8 only; 10..14: timing ablations (wrong results) of the
+        // LDS-DMA kernel: 10 no index switching, 11 multiples + tables only, 12 lookups only,
+        // 13 loads only; 14: loads only, register ring 4
+        if (a.mode == 2 || (a.mode >= 10 && a.mode <= 13)) {
+            ApplyArgs f = a;
+            f.nchunks = a.nbytes / 2048;
+            if (f.nchunks > 0) {
+                dim3 g(unsigned(n_stripes * f.nchunks), grid.y);
+                switch (a.mode) {
+                case 10: hipLaunchKernelGGL((k_apply_m8_lds<1>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 11: hipLaunchKernelGGL((k_apply_m8_lds<2>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 12: hipLaunchKernelGGL((k_apply_m8_lds<3>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 13: hipLaunchKernelGGL((k_apply_m8_lds<4>), g, dim3(256), 0, st, f, a.in_idx); break;
+                default: hipLaunchKernelGGL((k_apply_m8_lds<0>), g, dim3(256), 0, st, f, a.in_idx); break;
+                }
+            }
+            if (a.nbytes % 2048) {
+                ApplyArgs t = a;
+                t.chunk_base = f.nchunks;
+                t.nchunks = 1;
+                dim3 g(unsigned(n_stripes), grid.y);
+                hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), g, dim3(256), 0, st, t, a.in_idx);
+            }
+        } else if (a.mode == 4) {
+            hipLaunchKernelGGL((k_apply_m8_idx<0, 8>), grid, dim3(256), 0, st, a, a.in_idx);
+        } else if (a.mode == 14) {
+            hipLaunchKernelGGL((k_apply_m8_idx<4, 4>), grid, dim3(256), 0, st, a, a.in_idx);
+        } else {
+            hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), grid, dim3(256), 0, st, a, a.in_idx);
+        }
+    }
     else if (a.mode == 1)
         hipLaunchKernelGGL((k_apply_m8<RT, 1>), grid, dim3(256), 0, st, a);
     else

@@ -22,6 +22,7 @@ struct ApplyArgs {
     int32_t R;
     int64_t nbytes;          // symbol size (even)
     int64_t nchunks;         // filled by launch_apply
+    int64_t chunk_base;      // first column chunk (tail launches)
     int32_t mode;            // m<=8 inner loop: 0 = register nibble tables (compiler indexing),
                              //   1 = SGPR-masked multiples, 2 = hand-scheduled gpr-index block (RT=32)
 };

@@ -1,0 +1,24 @@
+"""Timing ablation of the m8 asm kernel (one process, interleaved rounds): full, no index switching,
+build only, lookups only. Results of the ablated variants are wrong by construction."""
+import os, sys, json
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd"))
+import rs_amd
+k, r, S, n = 128, 32, 65536, int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")
+rs_amd.fill_info(dev, k, 0x5EED)
+modes = {"lds": 2, "reg4": 3, "lds_noidx": 10, "lds_build": 11, "lds_look": 12, "lds_nop": 13, "reg4_nop": 14}
+codecs = {m: rs_amd.Codec(k, r, m8_mode=v) for m, v in modes.items()}
+res = {m: [] for m in modes}
+for rnd in range(4):
+    for m, c in codecs.items():
+        c.encode(dev); torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(); c.encode(dev); b.record(); torch.cuda.synchronize()
+        if rnd: res[m].append(a.elapsed_time(b))
+for c in codecs.values():
+    c.close()
+for m, v in res.items():
+    ms = float(np.median(v))
+    print(json.dumps({"variant": m, "ms": round(ms, 3), "GBps": round(n * (k + r) * S / ms / 1e6, 1)}))
