@@ -29,8 +29,34 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "reed-solomon_amd"))
 import rs_amd  # noqa: E402  (raises if librs_amd.so is missing: no fallback)
+import rs_dist  # noqa: E402
+
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")  # scripts/traffic.py output
+
+
+def kernel_src_hash():
+    """Identifies the kernel build a traffic measurement belongs to (hash of the kernel sources)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("csrc/rs_kernels.hip", "csrc/gen_asm.py", "csrc/rs_device.h"):
+        with open(os.path.join(REPO, "reed-solomon_amd", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(kernel, cfg):
+    """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters on this configuration
+    (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("bench_kernel") != kernel or t.get("config") != cfg or t.get("src_hash") != kernel_src_hash():
+        return None
+    return int(t["traffic_bytes"])
 SEED = 0x5EED
 
 
@@ -150,9 +176,7 @@ def cpu_baseline(args, erased, gpu_sample):
 # ------------------------------------------------------------------------------ main
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = rs_dist.env()
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -166,11 +190,8 @@ def main():
                          m8_mode={"table": 0, "mask": 1, "idx": 2}.get(args.kernel))
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
-    rs_amd.fill_info(stripes, k, SEED, stripe0=rank * n, stream=stream)
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
+    stripe0, _ = rs_dist.weak_shard(n, rank)  # this rank's global stripe ids: [stripe0, stripe0 + n)
+    rs_amd.fill_info(stripes, k, SEED, stripe0=stripe0, stream=stream)
 
     # warmup (also compiles / loads the specialised kernels)
     for _ in range(args.warmup):
@@ -181,24 +202,16 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        codec.encode(stripes, stream=stream)
-        kern_enc = codec.last_kernel
-        ev[i][1].record(stream)
-        codec.decode(stripes, erased, stream=stream)
-        kern_dec = codec.last_kernel
-        ev[i][2].record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    with rs_dist.TimedRegion(dev) as region:
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            codec.encode(stripes, stream=stream)
+            kern_enc = codec.last_kernel
+            ev[i][1].record(stream)
+            codec.decode(stripes, erased, stream=stream)
+            kern_dec = codec.last_kernel
+            ev[i][2].record(stream)
+    elapsed = region.max_elapsed
 
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
@@ -218,7 +231,7 @@ def main():
         fp1 = torch.zeros(n, dtype=torch.int64, device=dev)
         rs_amd.fingerprint(stripes, 0, k + r, fp1, stream=stream)
         torch.cuda.synchronize()
-        ok = bool(torch.equal(fp0, fp1))
+        ok = rs_dist.max_over_ranks(0.0 if torch.equal(fp0, fp1) else 1.0, dev) == 0.0  # any rank
         if rank == 0:
             gpu_sample = stripes[: args.cpu_stripes].cpu().numpy()
         parity = "roundtrip-ok" if ok else "ROUNDTRIP-MISMATCH"
@@ -231,6 +244,7 @@ def main():
     # roofline of the dominant kernel (encode and decode move the same algorithmic bytes here)
     dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, kern_enc) if enc_ms >= dec_ms else (dec_ms, dec_bytes, kern_dec)
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+    traffic = measured_traffic(dom_name, f"k{k}_r{r}_S{S}_n{n}_t{t}")
     line = {
         "metric": "encode+decode GB/s (device-resident) at k=128 r=32 64KiB symbols; % HBM roofline",
         "value": round(value, 2),
@@ -248,7 +262,7 @@ def main():
                                f"at i*{k // r})", "stripes_total": n * world, "parallelism": f"stripes x{world}",
                    "kernel": {"encode": kern_enc, "decode": kern_dec}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes},
         "encode_ms": round(enc_ms, 3),
         "decode_ms": round(dec_ms, 3),

@@ -142,14 +142,14 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
     int rc;
     if (p->m == 8 && rt == 32) {
-        // k_apply_m8_idx record per (tile, input): 64 dwords, [2j] = lo, [2j + 1] = hi nibble of output j
+        // k_apply_m8_idx record per (tile, input): 64 dwords, [j] = lo, [32 + j] = hi nibble of output j
         std::vector<uint32_t> idx(size_t(p->ntiles) * K * 64, 0);
         for (int t = 0; t < p->ntiles; ++t)
             for (int i = 0; i < K; ++i)
                 for (int j = 0; j < 32; ++j) {
                     const uint32_t c = (coef[(size_t(t) * K + i) * 8 + j / 4] >> (8 * (j % 4))) & 0xFF;
-                    idx[(size_t(t) * K + i) * 64 + 2 * j] = c & 15;
-                    idx[(size_t(t) * K + i) * 64 + 2 * j + 1] = c >> 4;
+                    idx[(size_t(t) * K + i) * 64 + j] = c & 15;
+                    idx[(size_t(t) * K + i) * 64 + 32 + j] = c >> 4;
                 }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
     }
@@ -245,7 +245,7 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value < 0 || (value > 4 && value < 10) || value > 14) return RS_ERR_INVALID;
+        if (value < 0 || (value > 4 && value < 10) || value > 16) return RS_ERR_INVALID;
         c->m8_mode = int(value);
         return 0;
     }

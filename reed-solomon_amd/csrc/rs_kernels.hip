@@ -126,6 +126,7 @@ __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (
       [t3] "=&v"(t3)                                                                                                  \
     : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu)                                               \
     : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "memory"
+    // ABL: 0 production ("split"), 1..6 timing ablations / alternative schedules (csrc/gen_asm.py)
     if constexpr (ABL == 0) {
         asm volatile(
 #include "gen/m8_idx_asm.inc"
@@ -142,9 +143,17 @@ __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (
         asm volatile(
 #include "gen/m8_idx_asm_look.inc"
             RS_M8_IDX_OPERANDS);
-    } else {
+    } else if constexpr (ABL == 4) {
         asm volatile(
 #include "gen/m8_idx_asm_nop.inc"
+            RS_M8_IDX_OPERANDS);
+    } else if constexpr (ABL == 5) {
+        asm volatile(
+#include "gen/m8_idx_asm_full.inc"
+            RS_M8_IDX_OPERANDS);
+    } else {
+        asm volatile(
+#include "gen/m8_idx_asm_plain.inc"
             RS_M8_IDX_OPERANDS);
     }
 #undef RS_M8_IDX_OPERANDS
@@ -450,10 +459,11 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
     if (RT == 32 && a.mode >= 2 && a.idx) {
         // mode 2: production kernel (LDS-DMA ring over full chunks + register-ring tail);
-        // 3 / 4: register ring 4 / 8 only; 10..14: timing ablations (wrong results) of the
-        // LDS-DMA kernel: 10 no index switching, 11 multiples + tables only, 12 lookups only,
-        // 13 loads only; 14: loads only, register ring 4
-        if (a.mode == 2 || (a.mode >= 10 && a.mode <= 13)) {
+        // 3 / 4: register ring 4 / 8 only; 10..16: the LDS-DMA kernel with asm variant ABL = mode - 9
+        // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
+        // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 per-output schedule,
+        // 15 no gpr-index mode
+        if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15)) {
             ApplyArgs f = a;
             f.nchunks = a.nbytes / 2048;
             if (f.nchunks > 0) {
@@ -463,6 +473,8 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
                 case 11: hipLaunchKernelGGL((k_apply_m8_lds<2>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 12: hipLaunchKernelGGL((k_apply_m8_lds<3>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 13: hipLaunchKernelGGL((k_apply_m8_lds<4>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 14: hipLaunchKernelGGL((k_apply_m8_lds<5>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 15: hipLaunchKernelGGL((k_apply_m8_lds<6>), g, dim3(256), 0, st, f, a.in_idx); break;
                 default: hipLaunchKernelGGL((k_apply_m8_lds<0>), g, dim3(256), 0, st, f, a.in_idx); break;
                 }
             }
@@ -475,7 +487,7 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
             }
         } else if (a.mode == 4) {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 8>), grid, dim3(256), 0, st, a, a.in_idx);
-        } else if (a.mode == 14) {
+        } else if (a.mode == 16) {  // loads only, register ring 4
             hipLaunchKernelGGL((k_apply_m8_idx<4, 4>), grid, dim3(256), 0, st, a, a.in_idx);
         } else {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), grid, dim3(256), 0, st, a, a.in_idx);

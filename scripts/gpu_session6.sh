@@ -1,0 +1,12 @@
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() { local name=$1 to=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -3 "gpurun_out/$name.log"; return $rc; }
+ok() { [ "$1" -le 1 ]; }
+step pytest_gpu 900 python -m pytest tests/test_gpu.py -x -q -m gpu -k "idx or not (table or mask or jit)"; ok $? || exit 1
+step ablate 600 python scripts/gpu_ablate.py 2048; ok $? || exit 1
+grep variant gpurun_out/ablate.log
+step bench_idx 600 python bench.py --no-cpu || exit 1
+step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof7 -o run -- python3 bench.py --no-cpu --steps 3 --warmup 1
+exit $?

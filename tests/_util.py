@@ -40,6 +40,18 @@ def gen_info(seed, stripe, nbytes, offset=0):
     return b[s:s + nbytes].copy()
 
 
+def fingerprint_np(stripe_buf, sym0, nsym):
+    """CPU port of the device fingerprint (rs_kernels.hip:k_fingerprint) of one stripe
+    [k + r][S]: XOR over 8-byte words w at (sym, off) of mix64(w ^ mix64(sym << 40 | off))."""
+    S = stripe_buf.shape[1]
+    w = np.ascontiguousarray(stripe_buf[sym0:sym0 + nsym]).view("<u8").astype(np.uint64)
+    sym = np.arange(sym0, sym0 + nsym, dtype=np.uint64)[:, None]
+    off = (np.arange(S // 8, dtype=np.uint64) * np.uint64(8))[None, :]
+    with np.errstate(over="ignore"):
+        h = _mix64(w ^ _mix64((sym << np.uint64(40)) | off))
+    return int(np.bitwise_xor.reduce(h.reshape(-1)).astype(np.int64))
+
+
 def manifest():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)

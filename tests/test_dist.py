@@ -1,0 +1,94 @@
+"""Multi-process stripe sharding (the N>1 path of bench.py) on CPU with gloo, world_size 2.
+
+Each rank owns a contiguous stripe range (rs_dist.weak_shard / shard), builds its stripes from the
+global stripe ids, encodes, erases and decodes them with the CPU oracle (the GPU engine is not
+available here), and fingerprints them; the XOR of the per-rank fingerprints must equal the
+single-process fingerprint of the whole job, and TimedRegion must report the max over ranks."""
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "reed-solomon_amd"))
+import rs_dist  # noqa: E402
+from _util import bench_pattern, fingerprint_np, gen_info, oracle_decode, oracle_encode  # noqa: E402
+
+K, R, S, PER_RANK, SEED = 10, 4, 512, 3, 0x5EED
+
+
+def _job_stripes(first, count):
+    """Encoded + round-tripped stripes [first, first + count) and their fingerprints."""
+    er = np.zeros(K + R, np.bool_)
+    er[bench_pattern(K, R)] = True
+    fps = []
+    for s in range(first, first + count):
+        buf = np.zeros((K + R, S), np.uint8)
+        buf[:K] = gen_info(SEED, s, K * S).reshape(K, S)
+        assert oracle_encode(K, R, buf) == 0
+        fp = fingerprint_np(buf, 0, K + R)
+        lost = buf.copy()
+        lost[er] = 0
+        assert oracle_decode(K, R, lost, er, int(er.sum())) == 0
+        assert np.array_equal(lost[:K], buf[:K])
+        fps.append(fp)
+    return fps
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r, w, _ = rs_dist.env()
+        first, count = rs_dist.weak_shard(PER_RANK, r)
+        fps = _job_stripes(first, count)
+        mine = np.bitwise_xor.reduce(np.array(fps, np.int64))
+        job = rs_dist.xor_over_ranks(torch.tensor([int(mine)], dtype=torch.int64))
+        with rs_dist.TimedRegion() as region:
+            time.sleep(0.05 + 0.25 * r)  # rank 1 is the slow one
+        q.put((r, first, count, int(job.item()), region.elapsed, region.max_elapsed))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_partitions():
+    for n in (0, 1, 7, 8192, 65536):
+        for world in (1, 2, 3, 8):
+            ranges = [rs_dist.shard(n, world, g) for g in range(world)]
+            assert sum(c for _, c in ranges) == n
+            assert all(ranges[g][0] + ranges[g][1] == ranges[g + 1][0] for g in range(world - 1))
+            assert max(c for _, c in ranges) - min(c for _, c in ranges) <= 1
+    assert [rs_dist.weak_shard(8192, g) for g in range(3)] == [(0, 8192), (8192, 8192), (16384, 8192)]
+
+
+def test_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(g, 2, port, q)) for g in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = sorted(q.get(timeout=10) for _ in procs)
+    want = np.bitwise_xor.reduce(np.array(_job_stripes(0, 2 * PER_RANK), np.int64))
+    assert [(r[1], r[2]) for r in res] == [(0, PER_RANK), (PER_RANK, PER_RANK)]
+    assert all(r[3] == int(want) for r in res), "XOR of shard fingerprints != whole-job fingerprint"
+    assert res[0][4] < res[1][4]
+    assert all(abs(r[5] - res[1][4]) < 1e-9 for r in res), "TimedRegion must report the max over ranks"
+    assert res[0][5] >= 0.3

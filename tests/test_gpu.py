@@ -178,3 +178,19 @@ def test_errors():
     rs = rs_amd.RS()
     syms = [np.zeros(9, np.uint8) for _ in range(6)]
     assert rs.generate_repair_symbols(syms[:4], syms[4:]) == rs_amd.RS_ERR_INVALID  # odd symbol size
+
+
+def test_fingerprint_matches_cpu_port():
+    """The device fingerprint used by bench.py's verification == tests/_util.py:fingerprint_np."""
+    from _util import fingerprint_np
+    k, r, S, n = 10, 4, 4096, 5
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xF1, stripe0=7)
+    rs_amd.Codec(k, r).encode(dev)
+    fp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(dev, 0, k + r, fp)
+    torch.cuda.synchronize()
+    host = dev.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(host[s, :k].reshape(-1), gen_info(0xF1, 7 + s, k * S))
+        assert int(fp[s]) == fingerprint_np(host[s], 0, k + r)
