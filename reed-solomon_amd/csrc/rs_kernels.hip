@@ -115,17 +115,17 @@ __global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
 // One input step of k_apply_m8_idx: LDS coordinate lookup, then the asm block (multiples, tables,
 // 32 outputs x 2 dwords of indexed XORs).
 template <int ABL>
-__device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (&x)[2], const uint32_t* cp,
-                                            u32x16& a0l, u32x16& a0h, u32x16& a1l, u32x16& a1h) {
-    const uint32_t y0 = lds_lookup4(lt, x[0]), y1 = lds_lookup4(lt, x[1]);
+__device__ __forceinline__ void m8_asm_step(uint32_t y0, uint32_t y1, const uint32_t* cp, u32x16& a0l, u32x16& a0h,
+                                            u32x16& a1l, u32x16& a1h) {
+    const uint32_t k1d = 0x1D1D1D1Du;  // VGPR operand: an SGPR operand would halve the bitop3 rate
     uint32_t t0, t1, t2, t3;
     u32x16 Tl0, Th0, Tl1, Th1;
 #define RS_M8_IDX_OPERANDS                                                                                     \
     : "+{v[72:87]}"(a0l), "+{v[88:103]}"(a0h), "+{v[104:119]}"(a1l), "+{v[120:135]}"(a1h), "=&{v[8:23]}"(Tl0),        \
       "=&{v[24:39]}"(Th0), "=&{v[40:55]}"(Tl1), "=&{v[56:71]}"(Th1), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),  \
       [t3] "=&v"(t3)                                                                                                  \
-    : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu)                                               \
-    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "memory"
+    : [y0] "v"(y0), [y1] "v"(y1), [cp] "s"(cp), [kfe] "s"(0xFEFEFEFEu), [k1d] "v"(k1d)                                               \
+    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71"
     // ABL: 0 production ("split"), 1..6 timing ablations / alternative schedules (csrc/gen_asm.py)
     if constexpr (ABL == 0) {
         asm volatile(
@@ -149,7 +149,7 @@ __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (
             RS_M8_IDX_OPERANDS);
     } else if constexpr (ABL == 5) {
         asm volatile(
-#include "gen/m8_idx_asm_full.inc"
+#include "gen/m8_idx_asm_split_mul.inc"
             RS_M8_IDX_OPERANDS);
     } else {
         asm volatile(
@@ -157,6 +157,13 @@ __device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (
             RS_M8_IDX_OPERANDS);
     }
 #undef RS_M8_IDX_OPERANDS
+}
+
+
+template <int ABL>
+__device__ __forceinline__ void m8_idx_step(const uint32_t* lt, const uint32_t (&x)[2], const uint32_t* cp,
+                                            u32x16& a0l, u32x16& a0h, u32x16& a1l, u32x16& a1h) {
+    m8_asm_step<ABL>(lds_lookup4(lt, x[0]), lds_lookup4(lt, x[1]), cp, a0l, a0h, a1l, a1h);
 }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
@@ -281,15 +288,20 @@ __device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* _
     for (int b = 0; b < nb; ++b) {
         const int ib = 4 * (b + RING_B) + wave;
         if (ib < K) issue(ib);
+        // the batch's 4 inputs: ring reads and coordinate lookups first (one LDS latency for all
+        // four; slots past K hold stale bytes and are not used), then the 4 asm steps
+        uint32_t y[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32x2 v = *reinterpret_cast<const u32x2*>(
+                reinterpret_cast<const uint8_t*>(ring) + ((4 * b + j) % RING_SLOTS) * 2048 + 8 * threadIdx.x);
+            y[j][0] = lds_lookup4(lt, v.x);
+            y[j][1] = lds_lookup4(lt, v.y);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 4 * b + j;
-            if (i < K) {
-                const u32x2 v = *reinterpret_cast<const u32x2*>(
-                    reinterpret_cast<const uint8_t*>(ring) + (i % RING_SLOTS) * 2048 + 8 * threadIdx.x);
-                const uint32_t x[2] = {v.x, v.y};
-                m8_idx_step<ABL>(lt, x, cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
-            }
+            if (i < K) m8_asm_step<ABL>(y[j][0], y[j][1], cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
         }
         wait_vm_dyn(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
@@ -461,7 +473,7 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
         // mode 2: production kernel (LDS-DMA ring over full chunks + register-ring tail);
         // 3 / 4: register ring 4 / 8 only; 10..16: the LDS-DMA kernel with asm variant ABL = mode - 9
         // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
-        // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 per-output schedule,
+        // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 split schedule with the multiply-based xtime,
         // 15 no gpr-index mode
         if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15)) {
             ApplyArgs f = a;

@@ -39,6 +39,12 @@ def body(kind):
             "xor_sdwa": f"v_xor_b32_sdwa v{d}, v{a}, v{b} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD",
             "idx_noswitch": f"v_xor_b32 v{d}, v40, v{d}",
         }
+        if kind.startswith("dep"):  # d interleaved self-dependent chains
+            dd = int(kind[3:-1])
+            r_ = 8 + i % dd
+            L.append(f"v_xor_b32 v{r_}, v{40 + i % 8}, v{r_}" if kind.endswith("x") else
+                     f"v_add_u32 v{r_}, v{r_}, v{r_}")
+            continue
         if kind in simple:
             L.append(simple[kind])
         elif kind in ("idx_sw2", "nop_sw2", "sadd_2", "idx_sw4"):
@@ -46,18 +52,18 @@ def body(kind):
             if i % per == 0:
                 s = 24 + (i // per) % 8
                 L.append({"idx_sw2": f"s_set_gpr_idx_idx s{s}", "idx_sw4": f"s_set_gpr_idx_idx s{s}", "nop_sw2": "s_nop 0",
-                          "sadd_2": f"s_add_u32 s{32 + (i // 2) % 4}, s{32 + (i // 2) % 4}, 1"}[kind])
+                          "sadd_2": f"s_add_u32 s{36 + (i // 2) % 4}, s{36 + (i // 2) % 4}, 1"}[kind])
             L.append(f"v_xor_b32 v{d}, v40, v{d}")
         else:
             raise ValueError(kind)
     return L
 
-KINDS = ["xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
+KINDS = ["dep1x", "dep2x", "dep3x", "dep4x", "dep6x", "dep8x", "dep1a", "dep2a", "dep4a", "xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
          "lshl_add", "lshl_or", "and_or", "or3", "bfi", "bfe", "perm_v", "perm_s", "alignbit", "pk_mul", "pk_mul_v",
          "mul_u24", "bitop3_s", "bitop3_v", "cndmask", "mov", "xor_sdwa", "idx_noswitch", "idx_sw2",
          "idx_sw4", "nop_sw2", "sadd_2"]
 VCLOB = ", ".join(f'"v{r}"' for r in range(8, 72))
-SCLOB = ", ".join(f'"s{r}"' for r in list(range(20, 36)))
+SCLOB = ", ".join(f'"s{r}"' for r in list(range(20, 32)) + list(range(36, 40)))
 out = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdint>', '#include <vector>', '#include <algorithm>',
        'static const char* kinds[] = {' + ", ".join(f'"{k}"' for k in KINDS) + '};']
 for n, k in enumerate(KINDS):
@@ -66,7 +72,7 @@ for n, k in enumerate(KINDS):
     idx = k.startswith("idx")
     setup = ["s_mov_b32 s20, 0xfefefefe", "s_mov_b32 s21, 0x01010101", "s_mov_b32 vcc_lo, 0x55555555",
              "s_mov_b32 vcc_hi, 0x55555555"] + [f"s_mov_b32 s{24 + j}, {(j + 1) % 8}" for j in range(8)] + \
-            [f"s_mov_b32 s{32 + j}, 0" for j in range(4)]
+            [f"s_mov_b32 s{36 + j}, 0" for j in range(4)]
     pre = ["s_set_gpr_idx_on s24, gpr_idx(SRC0)"] if idx else []
     post = ["s_set_gpr_idx_off"] if idx else []
     lines = setup + ["s_memtime %[t0]", "s_mov_b32 s22, %[iters]", "s_waitcnt lgkmcnt(0)", "BB%=:"] + pre + b + post + \
