@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--r", type=int, default=32)
     ap.add_argument("--symbol", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
-    ap.add_argument("--kernel", default="idx", choices=["idx", "table", "mask", "jit"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1", "idx", "table", "mask"],
+                    help="auto = library default policy (matrix-specialised kernels, generic fallback)")
     ap.add_argument("--cpu-stripes", type=int, default=128, help="CPU-baseline sample (stripes, resident)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (passes repeat)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -194,8 +195,9 @@ def main():
     k, r, S, n = args.k, args.r, args.symbol, args.stripes
     erased = rs_amd.bench_pattern(k, r)
     t = int(erased.sum())
-    codec = rs_amd.Codec(k, r, device=local, jit=args.kernel == "jit",
-                         m8_mode={"table": 0, "mask": 1, "idx": 2}.get(args.kernel))
+    opts = {"auto": {}, "jit": dict(jit=1), "v1": dict(jit=0, m8_mode=18), "idx": dict(jit=0, m8_mode=2),
+            "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1)}[args.kernel]
+    codec = rs_amd.Codec(k, r, device=local, **opts)
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     stripe0, _ = rs_dist.weak_shard(n, rank)  # this rank's global stripe ids: [stripe0, stripe0 + n)

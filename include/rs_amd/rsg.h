@@ -33,10 +33,12 @@ void rsg_codec_destroy(rsg_codec_t* c);
 /* Subfield degree m of the code (8 => GF(256) kernels, 16 => general kernels). */
 int rsg_codec_subfield(const rsg_codec_t* c);
 
-/* Options: "m8_mode" for GF(256) codes (2 = hand-scheduled gpr-index kernel, the default; 0 = register
- * tables with compiler indexing; 1 = masked multiples), "jit" (1 = matrix-specialised kernels compiled
- * with hiprtc; fully unrolled, instruction-fetch bound at k = 128 -- diagnostic only).
- * Returns RS_ERR_INVALID for unknown names or values. */
+/* Options: "m8_mode" for GF(256) codes without a specialised kernel (18 = one dword per lane,
+ * gpr-index lookups, the default; 2 = two dwords per lane; 0 = register tables with compiler
+ * indexing; 1 = masked multiples; 10-19 timing ablations), "jit" (matrix-specialised kernels
+ * compiled with hiprtc and cached on disk: 0 = off, 1 = every eligible matrix, 2 = the encode matrix
+ * and decode matrices from their second use, the default). Returns RS_ERR_INVALID for unknown names
+ * or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);

@@ -26,6 +26,10 @@ Variants (all but "full", "split" and "split_mul" give wrong results; they are t
   build      multiples + tables only       look  lookups only (tables not rebuilt)
   nop        consume the inputs only (memory-structure timing)
   plain      split without gpr-index mode (fixed table registers)
+  v1         one dword per lane (k_apply_m8_v1): half the registers, so 5 waves per SIMD
+  v1_plain   v1 without gpr-index mode (timing ablation)
+  v1_jitcall input step of the matrix-specialised V = 1 kernel (multiples, tables, call into the
+             input's generated lookup block)
 """
 import os
 import sys
@@ -102,6 +106,71 @@ def emit(path):
         f.write("// generated by csrc/gen_asm.py -- do not edit\n")
         f.write("".join(f'"{ln}\\n\\t"\n' for ln in L))
 
+
+if variant == "v1_jitcall":
+    # one input step of the matrix-specialised V = 1 kernel (rs_jit.cpp, rs_v1jit): multiples and both
+    # nibble tables, then s_swappc_b64 into this input's lookup block (fixed-register XORs,
+    # generated per coding matrix) at L_rs_blk0 + %[off]; the block returns with s_setpc_b64 s[72:73].
+    # L_rs_blk0 precedes every call site (the blocks are placed at the kernel entry), so the
+    # 64-bit sign extension of the negative offset is -1.
+    tl, th = 8, 24
+    tv = ("%[t0]", "%[t1]")
+    mreg = lambda j: (tl if j < 4 else th) + slots[j % 4]
+    e("s_getpc_b64 s[74:75]")
+    e("s_add_u32 s74, s74, L_rs_blk0-.")  # s_getpc returned the address of this instruction
+    e("s_addc_u32 s75, s75, -1")
+    e("s_add_u32 s74, s74, %[off]")
+    e("s_addc_u32 s75, s75, 0")
+    e(f"v_mov_b32 v{mreg(0)}, %[y0]")
+    for j in range(1, 8):
+        src, dst = mreg(j - 1), mreg(j)
+        for op in ["v_and_b32 {ta}, 0x80808080, v{src}", "v_lshrrev_b32 {tb}, 7, {ta}",
+                   "v_xor_b32 v{dst}, v{src}, {ta}", "v_sub_u32 {tb}, {ta}, {tb}", "v_add_u32 v{dst}, v{dst}, v{dst}",
+                   "v_bitop3_b32 v{dst}, v{dst}, {tb}, %[k1d] bitop3:0x78"]:
+            e(op.format(ta=tv[0], tb=tv[1], src=src, dst=dst))
+        if j == 3:
+            L.extend(table_ops((tl,)))
+    L.extend(table_ops((th,)))
+    e("s_swappc_b64 s[72:73], s[74:75]")
+    emit(out)
+    sys.exit(0)
+
+if variant in ("v1", "v1_plain"):
+    # one dword per lane per step (k_apply_m8_v1): Tl v[8:23], Th v[24:39], acc v[40:71]; temps t0, t1
+    tl, th, acc = 8, 24, 40
+    tv = ("%[t0]", "%[t1]")
+    mreg = lambda j: (tl if j < 4 else th) + slots[j % 4]
+    e("s_load_dwordx16 s[40:55], %[cp], 0x0")
+    e("s_load_dwordx16 s[56:71], %[cp], 0x40")
+    e(f"v_mov_b32 v{mreg(0)}, %[y0]")
+    for j in range(1, 8):
+        src, dst = mreg(j - 1), mreg(j)
+        for op in ["v_and_b32 {ta}, 0x80808080, v{src}", "v_lshrrev_b32 {tb}, 7, {ta}",
+                   "v_xor_b32 v{dst}, v{src}, {ta}", "v_sub_u32 {tb}, {ta}, {tb}", "v_add_u32 v{dst}, v{dst}, v{dst}",
+                   "v_bitop3_b32 v{dst}, v{dst}, {tb}, %[k1d] bitop3:0x78"]:
+            e(op.format(ta=tv[0], tb=tv[1], src=src, dst=dst))
+        if j == 3:
+            L.extend(table_ops((tl,)))
+    e("s_waitcnt lgkmcnt(0)")
+    idx = variant == "v1"
+    for p in range(32):
+        if idx:
+            e("s_set_gpr_idx_on s40, gpr_idx(SRC0)" if p == 0 else f"s_set_gpr_idx_idx s{40 + p}")
+        e(f"v_xor_b32 v{acc + p}, v{tl + (0 if idx else p % 16)}, v{acc + p}")
+    if idx:
+        e("s_set_gpr_idx_off")
+    e("s_load_dwordx16 s[40:55], %[cp], 0x80")
+    e("s_load_dwordx16 s[56:71], %[cp], 0xc0")
+    L.extend(table_ops((th,)))
+    e("s_waitcnt lgkmcnt(0)")
+    for p in range(32):
+        if idx:
+            e("s_set_gpr_idx_on s40, gpr_idx(SRC0)" if p == 0 else f"s_set_gpr_idx_idx s{40 + p}")
+        e(f"v_xor_b32 v{acc + p}, v{th + (0 if idx else (p + 5) % 16)}, v{acc + p}")
+    if idx:
+        e("s_set_gpr_idx_off")
+    emit(out)
+    sys.exit(0)
 
 if variant == "nop":
     e("v_xor_b32 v72, %[y0], v72")

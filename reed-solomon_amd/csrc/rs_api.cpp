@@ -88,6 +88,8 @@ struct DevPlan {
     std::vector<uint16_t> matrix;  // R x K, GF(2^16)
     std::vector<int32_t> in_slots, out_slots;
     std::unique_ptr<JitKernel> jit;  // matrix-specialised kernel, if built
+    bool jit_failed = false;         // compile failed once: stay on the generic kernels
+    int64_t uses = 0;                // launches of this plan (JIT policy)
     ~DevPlan() {
         int cur = 0;
         (void)hipGetDevice(&cur);
@@ -139,15 +141,18 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
                     coef[(size_t(t) * K + i) * (rt / 2) + j / 2] |= c << (16 * (j % 2));
                 }
     }
-    out_slots.resize(size_t(p->ntiles) * rt, 0);  // padded rows are never stored
+    out_slots.resize(std::max(size_t(p->ntiles) * rt, size_t((R + 31) / 32) * 32), 0);  // padded rows: never stored
     int rc;
-    if (p->m == 8 && rt == 32) {
-        // k_apply_m8_idx record per (tile, input): 64 dwords, [j] = lo, [32 + j] = hi nibble of output j
-        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 64, 0);
-        for (int t = 0; t < p->ntiles; ++t)
+    if (p->m == 8) {
+        // gpr-index kernels (k_apply_m8_idx / _lds / _v1), 32-row tiles whatever p->rt is: record per
+        // (tile, input) = 64 dwords, [j] = low, [32 + j] = high nibble of output j's coefficient
+        const Gamma8& g = gamma8();
+        const int nt32 = (R + 31) / 32;
+        std::vector<uint32_t> idx(size_t(nt32) * K * 64, 0);
+        for (int t = 0; t < nt32; ++t)
             for (int i = 0; i < K; ++i)
-                for (int j = 0; j < 32; ++j) {
-                    const uint32_t c = (coef[(size_t(t) * K + i) * 8 + j / 4] >> (8 * (j % 4))) & 0xFF;
+                for (int j = 0; j < 32 && t * 32 + j < R; ++j) {
+                    const uint32_t c = g.coord(M[size_t(t * 32 + j) * K + i]);
                     idx[(size_t(t) * K + i) * 64 + j] = c & 15;
                     idx[(size_t(t) * K + i) * 64 + 32 + j] = c >> 4;
                 }
@@ -177,8 +182,9 @@ struct rsg_codec {
     std::unique_ptr<DevPlan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<DevPlan>> dec;
     std::vector<std::vector<uint8_t>> dec_lru;
-    int m8_mode = 2;
-    int jit = 0;
+    int m8_mode = 18;
+    int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
+    uint64_t* stamps = nullptr;  // device buffer for mode 17 (instrumented timing)
     std::string last_kernel = "none";
 };
 
@@ -245,12 +251,17 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value < 0 || (value > 4 && value < 10) || value > 16) return RS_ERR_INVALID;
+        if (value < 0 || (value > 4 && value < 10) || value > 20) return RS_ERR_INVALID;
         c->m8_mode = int(value);
         return 0;
     }
+    if (!std::strcmp(name, "stamp_buffer")) {  // device pointer, [blocks * 4][4] uint64 (mode 17)
+        c->stamps = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(value));
+        return 0;
+    }
     if (!std::strcmp(name, "jit")) {
-        c->jit = value ? 1 : 0;
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        c->jit = int(value);
         return 0;
     }
     return RS_ERR_INVALID;
@@ -266,15 +277,18 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         (src_sym % align) || (dst_stripe % align) || (dst_sym % align))
         return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
-    if (c->jit && p.m == 8) {
-        if (!p.jit) {
-            int rc = jit_build(p.matrix, p.K, p.R, p.in_slots, p.out_slots, p.jit);
-            if (rc) return rc;
-        }
-        if (p.jit) {
-            c->last_kernel = p.jit->name;
-            return jit_launch(*p.jit, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, int64_t(n_stripes),
-                              int64_t(S), c->d_ltab, st);
+    ++p.uses;
+    const bool jit_ok = p.m == 8 && p.d_idx && !p.jit_failed && jit_supported(8, p.K, p.R) &&
+                        (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= 2)));
+    if (jit_ok && !p.jit) {
+        const Gamma8& g = gamma8();
+        std::vector<uint8_t> cg(p.matrix.size());
+        for (size_t e = 0; e < cg.size(); ++e) cg[e] = uint8_t(g.coord(p.matrix[e]));
+        if (jit_build(cg, p.K, p.R, p.jit) || !p.jit) {
+            std::fprintf(stderr, "librs_amd: JIT kernel unavailable for a %dx%d matrix; using the generic kernel\n",
+                         p.R, p.K);
+            p.jit_failed = true;
+            p.jit.reset();
         }
     }
     ApplyArgs a{};
@@ -293,10 +307,24 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.R = p.R;
     a.nbytes = int64_t(S);
     a.mode = c->m8_mode;
-    if (a.mode >= 2 && !(p.m == 8 && p.rt == 32)) a.mode = 0;
-    c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(p.rt) + "_mode" + std::to_string(a.mode))
-                              : (std::string("apply_m16_rt") + std::to_string(p.rt));
-    HIP_TRY(launch_apply(p.m, p.rt, a, int64_t(n_stripes), st));
+    a.stamps = c->stamps;
+    const int nt32 = (p.R + 31) / 32;
+    if (jit_ok && p.jit) {
+        const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
+        c->last_kernel = p.jit->name;
+        if (full > 0) {
+            int rc = jit_launch(*p.jit, v1_args(a, full, nullptr), int64_t(n_stripes), st);
+            if (rc) return rc;
+        }
+        launch_m8_tail(a, int64_t(n_stripes), unsigned(nt32), st);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+    // gpr-index kernel families (modes >= 2) always tile 32 rows
+    const int rt = p.m == 8 && a.mode >= 2 ? 32 : p.rt;
+    c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(rt) + "_mode" + std::to_string(a.mode))
+                              : (std::string("apply_m16_rt") + std::to_string(rt));
+    HIP_TRY(launch_apply(p.m, rt, a, int64_t(n_stripes), st));
     return 0;
 }
 
@@ -400,7 +428,10 @@ extern "C" int rsg_jit_precompile(uint16_t k, uint16_t r, const bool* is_erased,
         if (cnt != t || t > r) return RS_ERR_INVALID;
     }
     codec_matrix(pos, k, r, is_erased, M, in, outs);
-    return jit_precompile(M, int(in.size()), int(outs.size()), in, outs);
+    const Gamma8& g = gamma8();
+    std::vector<uint8_t> cg(M.size());
+    for (size_t e = 0; e < cg.size(); ++e) cg[e] = uint8_t(g.coord(M[e]));
+    return jit_precompile(cg, int(in.size()), int(outs.size()));
 }
 
 extern "C" int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red) {

@@ -4,6 +4,8 @@
 #ifndef RS_JIT_SOURCE
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "rs_v1args.h"
 #endif
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -72,3 +74,110 @@ __device__ __forceinline__ void store_slice(uint8_t* p, const uint32_t (&x)[W / 
     }
 }
 
+
+// ------------------------------------------------------------- LDS-DMA input ring (m <= 8)
+// Inputs are copied HBM -> LDS by global_load_lds_dwordx4 (16 B per lane, 1 KiB per wave
+// instruction), RING_B batches of 4 inputs ahead of use; slot of input i = i % RING_SLOTS.
+constexpr int RING_B = 3;
+constexpr int RING_SLOTS = 4 * (RING_B + 1);
+
+__device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds_byte)
+        : "memory");
+}
+
+// Wave-uniform read of an index table that no kernel writes (slot and offset arrays) through the
+// scalar cache. The compiler cannot prove these arrays unaliased with the kernels' global stores,
+// so a plain read becomes a global_load + s_waitcnt vmcnt(0) -- which also drains every LDS-DMA
+// in flight.
+__device__ __forceinline__ int32_t sload(const int32_t* p) {
+    int32_t v;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ------------------------------------------ m <= 8, one dword per lane per input step (V = 1)
+constexpr int V1_LDS_WORDS = 2048 + RING_SLOTS * 256;
+
+// Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile
+// blockIdx.y. Per batch of 4 inputs: wave (i % 4) issues input i's DMA RING_B batches ahead; every
+// wave reads its 4 dwords from the ring, maps them to GF(256)^2 coordinates (LDS byte tables) and
+// runs `step(y, i, tile, acc0_15, acc16_31)` per input; one s_barrier per batch. Outputs go back
+// through L^-1 into 4-byte stores.
+template <class Step>
+__device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&& step) {
+    for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
+    __syncthreads();
+    const uint32_t* lt = lds;
+    uint32_t* ring = lds + 2048;
+    const int64_t bid = blockIdx.x;
+    const int64_t stripe = bid / a.nchunks;
+    const int64_t chunk0 = (bid - stripe * a.nchunks) * 1024;
+    const int tile = blockIdx.y;
+    const int K = a.K;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
+    const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
+    const int32_t* in_idx = a.in_idx;
+    auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
+    const int nb = (K + 3) / 4;
+    auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
+        int c = 0;
+        for (int b = lo; b <= hi; ++b)
+            if (b < nb && 4 * b + wave < K) c += 1;
+        return c;
+    };
+    auto wait_mine = [&](int n) {
+        if (n <= 0)
+            wait_vm<0>();
+        else if (n == 1)
+            wait_vm<1>();
+        else if (n == 2)
+            wait_vm<2>();
+        else
+            wait_vm<3>();
+    };
+    u32x16 a0 = 0, a1 = 0;
+    for (int b = 0; b < RING_B; ++b)
+        if (4 * b + wave < K) issue(4 * b + wave);
+    wait_mine(mine(1, RING_B - 1));
+    asm volatile("s_barrier" ::: "memory");
+    for (int b = 0; b < nb; ++b) {
+        const int ib = 4 * (b + RING_B) + wave;
+        if (ib < K) issue(ib);
+        uint32_t y[4];  // slots past K hold stale bytes and are not used
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = lds_lookup4(lt, ring[((4 * b + j) % RING_SLOTS) * 256 + threadIdx.x]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * b + j;
+            if (i < K) step(y[j], i, tile, a0, a1);
+        }
+        wait_mine(mine(b + 2, b + RING_B));
+        asm volatile("s_barrier" ::: "memory");
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
+    const int rows = min(32, a.R - tile * 32);
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(a.out_idx + tile * 32 + p)) * a.dst_sym) =
+                lds_lookup4(lt + 1024, v);
+        }
+    }
+}

@@ -13,12 +13,17 @@
 #include <mutex>
 #include <sstream>
 
-#include "gf16.hpp"
-
 namespace rsamd {
 
+static const char* kArgsHeader =
+#include "gen/rs_v1args_h.inc"
+    ;
 static const char* kDeviceHeader =
 #include "gen/rs_device_h.inc"
+    ;
+// string literals of the generated call step (csrc/gen_asm.py v1_jitcall), as source text
+static const char* kCallAsm =
+#include "gen/v1_jitcall_text.inc"
     ;
 
 struct JitModule {
@@ -29,59 +34,74 @@ struct JitModule {
     }
 };
 
-bool jit_supported(int m, int K, int R) {
-    return m <= 8 && R >= 1 && R <= kJitMaxRows && int64_t(K) * R <= kJitMaxPairs;
+JitKernel::~JitKernel() {
+    if (d_boff) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        (void)hipFree(d_boff);
+        (void)hipSetDevice(cur);
+    }
 }
 
-std::string jit_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                       const std::vector<int32_t>& out_slots) {
-    const Gamma8& g = gamma8();
+bool jit_supported(int m, int K, int R) {
+    const int ntiles = (R + 31) / 32;
+    return m <= 8 && K >= 1 && R >= 1 && int64_t(ntiles) * K <= kJitMaxBlocks;
+}
+
+std::string jit_source(const std::vector<uint8_t>& cg, int K, int R, std::vector<int32_t>* boff) {
+    const int ntiles = (R + 31) / 32;
+    std::ostringstream blk;
+    int32_t off = 0;
+    if (boff) boff->assign(size_t(ntiles) * K, 0);
+    for (int t = 0; t < ntiles; ++t) {
+        const int rows = std::min(32, R - 32 * t);
+        for (int i = 0; i < K; ++i) {
+            if (boff) (*boff)[size_t(t) * K + i] = off;
+            for (int h = 0; h < 2; ++h)  // low nibbles (table v[8:23]), then high nibbles (v[24:39])
+                for (int p = 0; p < rows; ++p) {
+                    const int c = cg[size_t(32 * t + p) * K + i];
+                    const int e = h ? c >> 4 : c & 15;
+                    if (!e) continue;  // T[0] = 0
+                    blk << "\"v_xor_b32 v" << 40 + p << ", v" << (h ? 24 : 8) + e << ", v" << 40 + p << "\\n\"\n";
+                    off += 4;
+                }
+            blk << "\"s_setpc_b64 s[72:73]\\n\"\n";
+            off += 4;
+        }
+    }
     std::ostringstream o;
     o << "#define RS_JIT_SOURCE 1\n"
-         "typedef unsigned int uint32_t; typedef unsigned short uint16_t; typedef unsigned char uint8_t;\n"
-         "typedef long long int64_t;\n"
-      << kDeviceHeader << "\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(256) rs_jit_apply(const uint8_t* __restrict__ src,"
-         " int64_t src_stripe, int64_t src_sym, uint8_t* __restrict__ dst, int64_t dst_stripe, int64_t dst_sym,"
-         " const uint32_t* __restrict__ ltab, int64_t nbytes, int64_t nchunks) {\n"
-         "  __shared__ uint32_t lt[2048];\n"
-         "  for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = ltab[i];\n"
-         "  __syncthreads();\n"
-         "  const int64_t stripe = int64_t(blockIdx.x) / nchunks;\n"
-         "  const int64_t col = (int64_t(blockIdx.x) - stripe * nchunks) * 2048 + int64_t(threadIdx.x) * 8;\n"
-         "  const int64_t avail = nbytes - col;\n"
-         "  if (avail <= 0) return;\n"
-         "  const uint8_t* s = src + stripe * src_stripe + col;\n";
-    for (int p = 0; p < R; ++p) o << "  uint32_t a" << p << "_0 = 0, a" << p << "_1 = 0;\n";
-    if (K > 0) o << "  uint32_t x[2], nx[2];\n  load_slice<8>(x, s + " << in_slots[0] << "LL * src_sym, avail);\n";
-    for (int i = 0; i < K; ++i) {
-        o << "  {\n";
-        if (i + 1 < K) o << "    load_slice<8>(nx, s + " << in_slots[i + 1] << "LL * src_sym, avail);\n";
-        for (int v = 0; v < 2; ++v) {
-            o << "    const uint32_t m" << v << "0 = lds_lookup4(lt, x[" << v << "]);\n";
-            for (int j = 1; j < 8; ++j) o << "    const uint32_t m" << v << j << " = xt8(m" << v << (j - 1) << ");\n";
-        }
-        for (int p = 0; p < R; ++p) {
-            const uint32_t c = g.coord(M[size_t(p) * K + i]);
-            int bits[8], nb = 0;
-            for (int j = 0; j < 8; ++j)
-                if (c & (1u << j)) bits[nb++] = j;
-            for (int v = 0; v < 2; ++v) {
-                int q = 0;
-                for (; q + 1 < nb; q += 2)
-                    o << "    a" << p << "_" << v << " = xor3(a" << p << "_" << v << ", m" << v << bits[q] << ", m" << v
-                      << bits[q + 1] << ");\n";
-                if (q < nb) o << "    a" << p << "_" << v << " ^= m" << v << bits[q] << ";\n";
-            }
-        }
-        if (i + 1 < K) o << "    x[0] = nx[0]; x[1] = nx[1];\n";
-        o << "  }\n";
-    }
-    o << "  uint8_t* d = dst + stripe * dst_stripe + col;\n";
-    for (int p = 0; p < R; ++p)
-        o << "  { uint32_t y[2] = {lds_lookup4(lt + 1024, a" << p << "_0), lds_lookup4(lt + 1024, a" << p
-          << "_1)}; store_slice<8>(d + " << out_slots[p] << "LL * dst_sym, y, avail); }\n";
-    o << "}\n";
+         "typedef unsigned int uint32_t; typedef int int32_t; typedef unsigned short uint16_t;\n"
+         "typedef unsigned char uint8_t; typedef long long int64_t; typedef unsigned long long uint64_t;\n"
+         "typedef unsigned long uintptr_t;\n"
+      << kArgsHeader << "\n"
+      << kDeviceHeader << "\n"
+      << "extern \"C\" __global__ void __launch_bounds__(256) rs_v1jit(V1Args a) {\n"
+         "  __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];\n"
+         "  // lookup blocks of this matrix (entered only through s_swappc_b64 from the step below)\n"
+         "  asm volatile(\"s_branch L_rs_blocks_end\\n\"\n"
+         "\"L_rs_blk0:\\n\"\n"
+      << blk.str()
+      << "\"L_rs_blocks_end:\\n\"\n"
+         "\".if (L_rs_blocks_end - L_rs_blk0) != "
+      << off
+      << "\\n\"\n"
+         "\".error \\\"rs_v1jit: lookup block size mismatch\\\"\\n\"\n"
+         "\".endif\\n\" ::: \"memory\");\n"
+         "  m8_v1_run(a, lds, [&](uint32_t y, int i, int tile, u32x16& a0, u32x16& a1) {\n"
+         "    const int off = sload(a.boff + tile * a.K + i);\n"
+         "    const uint32_t k1d = 0x1D1D1D1Du;\n"
+         "    uint32_t t0, t1;\n"
+         "    u32x16 Tl, Th;\n"
+         "    asm volatile(\n"
+      << kCallAsm
+      << "      : \"+{v[40:55]}\"(a0), \"+{v[56:71]}\"(a1), \"=&{v[8:23]}\"(Tl), \"=&{v[24:39]}\"(Th), [t0] \"=&v\"(t0),"
+         " [t1] \"=&v\"(t1)\n"
+         "      : [y0] \"v\"(y), [off] \"s\"(off), [k1d] \"v\"(k1d)\n"
+         "      : \"s72\", \"s73\", \"s74\", \"s75\", \"scc\");\n"
+         "  });\n"
+         "}\n";
     return o.str();
 }
 
@@ -104,7 +124,7 @@ static std::string cache_dir() {
 
 static int compile(const std::string& src, std::vector<char>& code) {
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "rs_jit_apply.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return 1;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "rs_v1jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return 1;
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
     hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
     if (r != HIPRTC_SUCCESS) {
@@ -126,8 +146,8 @@ static int compile(const std::string& src, std::vector<char>& code) {
 
 // Code object for `src` from the disk cache, else compiled with hiprtc and stored there.
 static int jit_code(const std::string& src, uint64_t h, std::vector<char>& code) {
-    char name[32];
-    std::snprintf(name, sizeof name, "%016llx.co", static_cast<unsigned long long>(h));
+    char name[40];
+    std::snprintf(name, sizeof name, "v1_%016llx.co", static_cast<unsigned long long>(h));
     const std::string dir = cache_dir();
     if (!dir.empty()) {
         std::ifstream f(dir + "/" + name, std::ios::binary);
@@ -147,10 +167,9 @@ static int jit_code(const std::string& src, uint64_t h, std::vector<char>& code)
     return 0;
 }
 
-int jit_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                   const std::vector<int32_t>& out_slots) {
+int jit_precompile(const std::vector<uint8_t>& cg, int K, int R) {
     if (!jit_supported(8, K, R)) return 0;
-    const std::string src = jit_source(M, K, R, in_slots, out_slots);
+    const std::string src = jit_source(cg, K, R, nullptr);
     std::vector<char> code;
     return jit_code(src, fnv1a(src), code) ? 3 : 0;
 }
@@ -158,11 +177,11 @@ int jit_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vect
 static std::mutex g_jit_mu;
 static std::map<std::pair<int, uint64_t>, std::shared_ptr<JitModule>> g_jit_mods;
 
-int jit_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-              const std::vector<int32_t>& out_slots, std::unique_ptr<JitKernel>& out) {
+int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitKernel>& out) {
     out.reset();
     if (!jit_supported(8, K, R)) return 0;
-    const std::string src = jit_source(M, K, R, in_slots, out_slots);
+    std::vector<int32_t> boff;
+    const std::string src = jit_source(cg, K, R, &boff);
     const uint64_t h = fnv1a(src);
     int device = 0;
     (void)hipGetDevice(&device);
@@ -182,21 +201,24 @@ int jit_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<in
     }
     auto k = std::make_unique<JitKernel>();
     k->mod = slot;
-    if (hipModuleGetFunction(&k->fn, slot->mod, "rs_jit_apply") != hipSuccess) return 3;
+    k->device = device;
+    k->ntiles = (R + 31) / 32;
+    if (hipModuleGetFunction(&k->fn, slot->mod, "rs_v1jit") != hipSuccess) return 3;
+    if (hipMalloc(&k->d_boff, boff.size() * 4) != hipSuccess) return 3;
+    if (hipMemcpy(k->d_boff, boff.data(), boff.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return 3;
     char nm[64];
-    std::snprintf(nm, sizeof nm, "rs_jit_apply[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));
+    std::snprintf(nm, sizeof nm, "rs_v1jit[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));
     k->name = nm;
     out = std::move(k);
     return 0;
 }
 
-int jit_launch(const JitKernel& k, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
-               int64_t dst_stripe, int64_t dst_sym, int64_t n_stripes, int64_t nbytes, const uint32_t* ltab,
-               hipStream_t st) {
-    int64_t nchunks = (nbytes + 2047) / 2048;
-    if (n_stripes <= 0 || nchunks <= 0) return 0;
-    void* args[] = {&src, &src_stripe, &src_sym, &dst, &dst_stripe, &dst_sym, &ltab, &nbytes, &nchunks};
-    hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(n_stripes * nchunks), 1, 1, 256, 1, 1, 0, st, args, nullptr);
+int jit_launch(const JitKernel& k, V1Args v, int64_t n_stripes, hipStream_t st) {
+    if (n_stripes <= 0 || v.nchunks <= 0) return 0;
+    v.boff = k.d_boff;
+    void* args[] = {&v};
+    hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(n_stripes * v.nchunks), unsigned(k.ntiles), 1, 256, 1, 1, 0,
+                                         st, args, nullptr);
     if (e != hipSuccess) {
         std::fprintf(stderr, "librs_amd: jit launch: %s\n", hipGetErrorString(e));
         return 3;

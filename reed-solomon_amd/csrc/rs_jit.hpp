@@ -1,10 +1,12 @@
-// rs_jit.hpp -- coding-matrix-specialised kernels compiled at run time with hiprtc.
+// rs_jit.hpp -- coding-matrix-specialised V = 1 kernels compiled at run time with hiprtc.
 //
-// For m <= 8 codes the generic kernels spend most of their issue slots deciding, per
-// (output, input), which precomputed multiples to XOR (wave-uniform coefficient bits -> SALU
-// work or masks). Baking the matrix into the code turns every (output, input) pair into 1-2
-// straight-line 3-input XORs with no scalar work at all. One kernel per matrix, cached in memory
-// and on disk (RS_AMD_JIT_CACHE, default <lib dir>/jit_cache).
+// The generic m <= 8 kernels pick each (output, input) nibble table entry with gpr-index mode: an
+// s_set_gpr_idx_idx plus an indexed v_xor, which issues at half rate. With the matrix known, the
+// lookups of input i become a block of fixed-register v_xor (zero nibbles dropped) followed by
+// s_setpc_b64; the kernel's generic loop (rs_device.h:m8_v1_run) builds the nibble tables and
+// s_swappc_b64's into block i. 64 lookups per input = 260 B, so a 128-input tile's blocks
+// (33 KB) stay resident in the instruction cache. One kernel per matrix, cached in memory and on
+// disk (RS_AMD_JIT_CACHE, default <lib dir>/jit_cache).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -13,6 +15,8 @@
 #include <string>
 #include <vector>
 
+#include "rs_v1args.h"
+
 namespace rsamd {
 
 struct JitModule;
@@ -20,26 +24,25 @@ struct JitModule;
 struct JitKernel {
     std::shared_ptr<JitModule> mod;
     hipFunction_t fn = nullptr;
+    int32_t* d_boff = nullptr;  // [ntiles][K] block byte offsets (device)
+    int device = 0;
+    int ntiles = 0;
     std::string name;
+    ~JitKernel();
 };
 
-// Largest matrix (K * R) the specialiser accepts; bigger ones stay on the generic kernels.
-constexpr int64_t kJitMaxPairs = 8192;
-constexpr int kJitMaxRows = 32;
+// Largest number of lookup blocks (tiles x inputs) per kernel: 256 x 260 B = 66 KB of blocks.
+constexpr int kJitMaxBlocks = 256;
 
 bool jit_supported(int m, int K, int R);
-// Builds (or fetches) the kernel for an m <= 8 matrix M[R][K] (GF(2^16) values in GF(256)).
-// Returns 0 and leaves `out` empty when the shape is not supported; RS_ERR_DEVICE on failure.
-int jit_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-              const std::vector<int32_t>& out_slots, std::unique_ptr<JitKernel>& out);
+// cg: [R][K] coefficients in GF(256) gamma-basis coordinates (Gamma8::coord of the GF(2^16) entry).
+// Builds (or fetches) the kernel; RS_ERR_DEVICE-style nonzero on failure, `out` empty if unsupported.
+int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitKernel>& out);
 // Compiles into the disk cache only (no GPU needed).
-int jit_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                   const std::vector<int32_t>& out_slots);
-int jit_launch(const JitKernel& k, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
-               int64_t dst_stripe, int64_t dst_sym, int64_t n_stripes, int64_t nbytes, const uint32_t* ltab,
-               hipStream_t st);
-// Source text of the specialised kernel (exposed for tests / offline inspection).
-std::string jit_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                       const std::vector<int32_t>& out_slots);
+int jit_precompile(const std::vector<uint8_t>& cg, int K, int R);
+// Launches over `nchunks_1k` full 1 KiB column chunks of every stripe (v.boff is filled in here).
+int jit_launch(const JitKernel& k, V1Args v, int64_t n_stripes, hipStream_t st);
+// Source text of the specialised kernel and the per-block byte offsets (tests / inspection).
+std::string jit_source(const std::vector<uint8_t>& cg, int K, int R, std::vector<int32_t>* boff);
 
 }  // namespace rsamd

@@ -223,27 +223,6 @@ __device__ __forceinline__ void m8_idx_body(const ApplyArgs& a, const int32_t* _
 // s_waitcnt vmcnt, then a raw s_barrier (one per batch); readers ds_read_b64 their 8 bytes.
 // Ring slot of input i = i % (4 * (RING_B + 1)): batch b + RING_B reuses batch b - 1's slots, which
 // every wave finished reading before the barrier that ended round b - 1.
-constexpr int RING_B = 3;
-constexpr int RING_SLOTS = 4 * (RING_B + 1);
-
-__device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g), "s"(lds_byte)
-        : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // wait until at most n of this wave's DMA instructions are outstanding (n even, 0..2*RING_B)
 __device__ __forceinline__ void wait_vm_dyn(int n) {
     if (n <= 0)
@@ -256,7 +235,13 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
         wait_vm<6>();
 }
 
-template <int ABL>
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+}
+
+template <int ABL, bool STAMP = false>
 __device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* __restrict__ in_idx, uint32_t* lds,
                                             const uint8_t* chunk_src, const uint32_t* cbase, u32x16& a0l,
                                             u32x16& a0h, u32x16& a1l, u32x16& a1h) {
@@ -268,7 +253,7 @@ __device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* _
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
     const uint8_t* gl = chunk_src + 16 * lane;
     auto issue = [&](int i) {  // wave-uniform: only the owning wave calls
-        const uint8_t* g = gl + int64_t(in_idx[i]) * a.src_sym;
+        const uint8_t* g = gl + int64_t(sload(in_idx + i)) * a.src_sym;
         const uint32_t dst = ring_lds + uint32_t(i % RING_SLOTS) * 2048u;
         dma16(g, dst);
         dma16(g + 1024, dst + 1024);
@@ -281,11 +266,15 @@ __device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* _
             if (b < nb && 4 * b + wave < K) c += 2;
         return c;
     };
+    uint64_t ph[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0;  // STAMP: prologue+coords, asm, wait+barrier, total
+    if constexpr (STAMP) t0 = stamp_now();
+    const uint64_t tstart = t0;
     for (int b = 0; b < RING_B; ++b)
         if (4 * b + wave < K) issue(4 * b + wave);
     wait_vm_dyn(mine(1, RING_B - 1));
     asm volatile("s_barrier" ::: "memory");
     for (int b = 0; b < nb; ++b) {
+        if constexpr (STAMP) t0 = stamp_now();
         const int ib = 4 * (b + RING_B) + wave;
         if (ib < K) issue(ib);
         // the batch's 4 inputs: ring reads and coordinate lookups first (one LDS latency for all
@@ -298,18 +287,40 @@ __device__ __forceinline__ void m8_lds_body(const ApplyArgs& a, const int32_t* _
             y[j][0] = lds_lookup4(lt, v.x);
             y[j][1] = lds_lookup4(lt, v.y);
         }
+        if constexpr (STAMP) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            t1 = stamp_now();
+            ph[0] += t1 - t0;
+            t0 = t1;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 4 * b + j;
             if (i < K) m8_asm_step<ABL>(y[j][0], y[j][1], cbase + size_t(i) * 64, a0l, a0h, a1l, a1h);
         }
+        if constexpr (STAMP) {
+            t1 = stamp_now();
+            ph[1] += t1 - t0;
+            t0 = t1;
+        }
         wait_vm_dyn(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
+        if constexpr (STAMP) {
+            t1 = stamp_now();
+            ph[2] += t1 - t0;
+        }
+    }
+    if constexpr (STAMP) {
+        ph[3] = stamp_now() - tstart;
+        if (lane == 0) {
+            uint64_t* o = a.stamps + (int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 16 + wave * 4;
+            o[0] = ph[0], o[1] = ph[1], o[2] = ph[2], o[3] = ph[3];
+        }
     }
 }
 
 // Full 2 KiB chunks only (a.nchunks = full chunks per symbol); the tail chunk goes to k_apply_m8_idx.
-template <int ABL>
+template <int ABL, bool STAMP = false>
 __global__ void __launch_bounds__(256) k_apply_m8_lds(ApplyArgs a, const int32_t* __restrict__ in_idx) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[2048 + RING_SLOTS * 512];
     for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
@@ -324,7 +335,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_lds(ApplyArgs a, const int32_t
     const uint32_t* cbase = a.idx + size_t(tile) * a.K * 64;
 
     u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
-    m8_lds_body<ABL>(a, in_idx, lds, a.src + stripe * a.src_stripe + chunk0, cbase, a0l, a0h, a1l, a1h);
+    m8_lds_body<ABL, STAMP>(a, in_idx, lds, a.src + stripe * a.src_stripe + chunk0, cbase, a0l, a0h, a1l, a1h);
     uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
     const int rows = min(32, a.R - tile * 32);
 #pragma unroll
@@ -336,6 +347,44 @@ __global__ void __launch_bounds__(256) k_apply_m8_lds(ApplyArgs a, const int32_t
             store_slice<8>(dst + int64_t(a.out_idx[tile * 32 + p]) * a.dst_sym, y, avail);
         }
     }
+}
+
+// ------------------------------------------------------- m <= 8, one dword per lane (V = 1)
+// Same algorithm as k_apply_m8_lds with 4 bytes per lane per step: tables (32 VGPRs) and 32
+// accumulators (32 VGPRs) take half the registers, so 5 waves share each SIMD instead of 3 (the
+// V = 2 kernel is bound by each wave's own issue rate, not by the VALU pipe). Block = 256 lanes x 4 B
+// = one 1 KiB column chunk; each input's chunk is one global_load_lds_dwordx4 (1 KiB) issued by
+// wave i % 4, RING_B batches ahead, one s_barrier per batch of 4 inputs.
+template <int ABL>
+__device__ __forceinline__ void m8_v1_step(uint32_t y, const uint32_t* cp, u32x16& a0, u32x16& a1) {
+    const uint32_t k1d = 0x1D1D1D1Du;
+    uint32_t t0, t1;
+    u32x16 Tl, Th;
+#define RS_M8_V1_OPERANDS                                                                                  \
+    : "+{v[40:55]}"(a0), "+{v[56:71]}"(a1), "=&{v[8:23]}"(Tl), "=&{v[24:39]}"(Th), [t0] "=&v"(t0), [t1] "=&v"(t1) \
+    : [y0] "v"(y), [cp] "s"(cp), [k1d] "v"(k1d)                                                                 \
+    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", \
+      "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71"
+    if constexpr (ABL == 0) {
+        asm volatile(
+#include "gen/m8_idx_asm_v1.inc"
+            RS_M8_V1_OPERANDS);
+    } else {
+        asm volatile(
+#include "gen/m8_idx_asm_v1_plain.inc"
+            RS_M8_V1_OPERANDS);
+    }
+#undef RS_M8_V1_OPERANDS
+}
+
+// V = 1 generic kernel (rs_device.h:m8_v1_run): per input, multiples + tables + 64 gpr-indexed
+// lookups with SMEM-fed indices. The matrix-specialised variant is rs_jit.cpp's rs_v1jit.
+template <int ABL>
+__global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
+    m8_v1_run(a, lds, [&](uint32_t y, int i, int tile, u32x16& a0, u32x16& a1) {
+        m8_v1_step<ABL>(y, a.idx + (size_t(tile) * a.K + i) * 64, a0, a1);
+    });
 }
 
 template <int ABL, int PD>
@@ -466,6 +515,34 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
 }
 
 // ------------------------------------------------------------------------------ launchers
+V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
+    V1Args v{};
+    v.src = a.src;
+    v.src_stripe = a.src_stripe;
+    v.src_sym = a.src_sym;
+    v.in_idx = a.in_idx;
+    v.dst = a.dst;
+    v.dst_stripe = a.dst_stripe;
+    v.dst_sym = a.dst_sym;
+    v.out_idx = a.out_idx;
+    v.ltab = a.ltab;
+    v.idx = a.idx;
+    v.boff = boff;
+    v.K = a.K;
+    v.R = a.R;
+    v.nchunks = nchunks_1k;
+    return v;
+}
+
+// Columns past the last full 2 KiB chunk of every symbol (rows of all tiles), register-ring kernel.
+void launch_m8_tail(const ApplyArgs& a, int64_t n_stripes, unsigned tiles, hipStream_t st) {
+    if (a.nbytes % 2048 == 0) return;
+    ApplyArgs t = a;
+    t.chunk_base = a.nbytes / 2048;
+    t.nchunks = 1;
+    hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), dim3(unsigned(n_stripes), tiles), dim3(256), 0, st, t, a.in_idx);
+}
+
 template <int RT>
 static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
@@ -475,7 +552,18 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
         // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
         // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 split schedule with the multiply-based xtime,
         // 15 no gpr-index mode
-        if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15)) {
+        if (a.mode == 18 || a.mode == 19) {  // V = 1 kernel (19: without gpr-index mode, timing only)
+            const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
+            if (full > 0) {
+                const V1Args v = v1_args(a, full, nullptr);
+                dim3 g(unsigned(n_stripes * full), grid.y);
+                if (a.mode == 18)
+                    hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
+                else
+                    hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
+            }
+            launch_m8_tail(a, n_stripes, grid.y, st);
+        } else if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15) || a.mode == 17) {
             ApplyArgs f = a;
             f.nchunks = a.nbytes / 2048;
             if (f.nchunks > 0) {
@@ -487,6 +575,10 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
                 case 13: hipLaunchKernelGGL((k_apply_m8_lds<4>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 14: hipLaunchKernelGGL((k_apply_m8_lds<5>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 15: hipLaunchKernelGGL((k_apply_m8_lds<6>), g, dim3(256), 0, st, f, a.in_idx); break;
+                case 17:  // production kernel with s_memtime phase counters (needs a.stamps)
+                    if (!a.stamps) return hipErrorInvalidValue;
+                    hipLaunchKernelGGL((k_apply_m8_lds<0, true>), g, dim3(256), 0, st, f, a.in_idx);
+                    break;
                 default: hipLaunchKernelGGL((k_apply_m8_lds<0>), g, dim3(256), 0, st, f, a.in_idx); break;
                 }
             }

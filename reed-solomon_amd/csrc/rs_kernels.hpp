@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rs_v1args.h"
+
 namespace rsamd {
 
 // out[stripe][out_idx[p]] = sum_i C[p][i] * in[stripe][in_idx[i]]   for p < R, per 16-bit word.
@@ -25,9 +27,14 @@ struct ApplyArgs {
     int64_t chunk_base;      // first column chunk (tail launches)
     int32_t mode;            // m<=8 inner loop: 0 = register nibble tables (compiler indexing),
                              //   1 = SGPR-masked multiples, 2 = hand-scheduled gpr-index block (RT=32)
+    uint64_t* stamps;        // mode 17 (instrumented): [blocks * 4 waves][4] phase cycle counters
 };
 
 int apply_tile_rows(int m, int R);
+// V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)
+V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff);
+// the register-ring kernel over the columns past the last full 2 KiB chunk (no-op if none)
+void launch_m8_tail(const ApplyArgs& a, int64_t n_stripes, unsigned tiles, hipStream_t st);
 int64_t apply_chunk_bytes(int m);
 hipError_t launch_apply(int m, int rt, ApplyArgs a, int64_t n_stripes, hipStream_t st);
 hipError_t launch_gen_info(uint8_t* base, int64_t stripe_stride, int64_t sym_stride, int64_t S, int k, int64_t stripe0,

@@ -1,0 +1,22 @@
+// rs_v1args.h -- kernel-argument block of the V = 1 m <= 8 kernels, shared by host code, the AOT
+// kernels and the hiprtc sources (rs_jit.cpp embeds this text ahead of rs_device.h). Plain data only.
+#pragma once
+#ifndef RS_JIT_SOURCE
+#include <stdint.h>
+#endif
+
+// Kernel arguments of the V = 1 kernels (AOT k_apply_m8_v1 and the hiprtc-specialised rs_v1jit).
+struct V1Args {
+    const uint8_t* src;      // stripe 0 of the input layout
+    int64_t src_stripe, src_sym;
+    const int32_t* in_idx;   // [K (+16 pad)] input symbol slots
+    uint8_t* dst;
+    int64_t dst_stripe, dst_sym;
+    const int32_t* out_idx;  // [ntiles * 32] output symbol slots
+    const uint32_t* ltab;    // [2048] GF(256)^2 coordinate byte tables (L, L^-1)
+    const uint32_t* idx;     // AOT: [ntiles][K][64] nibble indices (lo p, hi 32 + p)
+    const int32_t* boff;     // JIT: [ntiles][K] byte offset of each input's lookup block
+    int32_t K, R;
+    int64_t nchunks;         // 1 KiB column chunks per symbol processed by this launch
+};
+

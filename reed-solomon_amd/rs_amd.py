@@ -206,22 +206,24 @@ def _stream_ptr(stream):
 class Codec:
     """Batched (k, r) engine on one GPU. Buffers are torch uint8 CUDA tensors (or raw pointers)."""
 
-    def __init__(self, k, r, device=0, jit=False, m8_mode=None):
+    def __init__(self, k, r, device=0, jit=None, m8_mode=None):
+        """jit: None = library default (2), 0/False = generic kernels only, 1/True = specialise every
+        eligible matrix, 2 = encode matrix + decode matrices from their second use."""
         self.k, self.r, self.device = k, r, device
         h = P()
         rc = _lib.rsg_codec_create(device, k, r, ctypes.byref(h))
         if rc:
             raise RSError(rc, f"rsg_codec_create({k}, {r})")
         self._h = h
-        if jit:
-            self.set_option("jit", 1)
+        if jit is not None:
+            self.set_option("jit", int(jit))
         if m8_mode is not None:
             self.set_option("m8_mode", m8_mode)
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and _lib is not None:  # _lib is None during interpreter shutdown
             _lib.rsg_codec_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         self.close()

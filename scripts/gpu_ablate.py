@@ -9,13 +9,14 @@ k, r, S, n = 128, 32, 65536, int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")
 rs_amd.fill_info(dev, k, 0x5EED)
 modes = {"lds": 2, "reg4": 3, "lds_noidx": 10, "lds_build": 11, "lds_look": 12, "lds_nop": 13, "lds_split_mul": 14,
-         "lds_plain": 15, "reg4_nop": 16}
-codecs = {m: rs_amd.Codec(k, r, m8_mode=v) for m, v in modes.items()}
-res = {m: [] for m in modes}
+         "lds_plain": 15, "reg4_nop": 16, "v1": 18, "v1_plain": 19}
+codecs = {m: rs_amd.Codec(k, r, m8_mode=v, jit=0) for m, v in modes.items()}
+codecs["jit"] = rs_amd.Codec(k, r, jit=1)
+res = {m: [] for m in codecs}
 # bit-exactness of the schedules that must be correct, against the table kernel (mode 0)
 ref = dev[:8].clone()
-rs_amd.Codec(k, r, m8_mode=0).encode(ref)
-for m in ("lds", "reg4", "lds_split_mul"):
+rs_amd.Codec(k, r, m8_mode=0, jit=0).encode(ref)
+for m in ("lds", "reg4", "lds_split_mul", "v1", "jit"):
     d = dev[:8].clone()
     codecs[m].encode(d)
     torch.cuda.synchronize()
