@@ -18,6 +18,7 @@
 #define RS_AMD_RSG_H
 
 #include <stdbool.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -72,6 +73,12 @@ int rsg_coding_matrix(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t,
 /* Compiles the matrix-specialised kernel for the encode (is_erased == NULL) or decode matrix into the
  * on-disk JIT cache without touching a GPU (0 also when the matrix is not JIT-eligible). */
 int rsg_jit_precompile(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t);
+/* Generated source of the bit-plane XOR kernel (rs_xj) for the encode (is_erased == NULL) or decode
+ * matrix; *len = full length, buf gets at most cap - 1 bytes + NUL. RS_ERR_INVALID when not eligible. */
+int rsg_xj_source(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, char* buf, size_t cap, size_t* len);
+/* Bit-plane basis of the XOR kernels: pivots[8], beta_y[8] (alpha^-j coordinates of beta_t) and the
+ * 8 bit-plane bits of each GF(256) element indexed by its gamma-basis byte (bits256[256]). */
+int rsg_xj_basis(int32_t* pivots, uint16_t* beta_y, uint8_t* bits256);
 /* GF(256)^2 coordinate tables used by the m <= 8 kernels (lbyte/ibyte: 2 x 256 entries each). */
 int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
 const char* rsg_version(void);

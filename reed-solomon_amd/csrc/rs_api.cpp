@@ -18,6 +18,7 @@
 #include "gf16.hpp"
 #include "rs_jit.hpp"
 #include "rs_kernels.hpp"
+#include "rs_xj.hpp"
 
 extern "C" {
 #include <memory/seq.h>
@@ -89,6 +90,8 @@ struct DevPlan {
     std::vector<int32_t> in_slots, out_slots;
     std::unique_ptr<JitKernel> jit;  // matrix-specialised kernel, if built
     bool jit_failed = false;         // compile failed once: stay on the generic kernels
+    std::unique_ptr<XjKernel> xj;    // bit-plane XOR kernel (rs_xj.hpp), if built
+    bool xj_failed = false;
     int64_t uses = 0;                // launches of this plan (JIT policy)
     ~DevPlan() {
         int cur = 0;
@@ -184,6 +187,7 @@ struct rsg_codec {
     std::vector<std::vector<uint8_t>> dec_lru;
     int m8_mode = 18;
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
+    int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
     uint64_t* stamps = nullptr;  // device buffer for mode 17 (instrumented timing)
     std::string last_kernel = "none";
 };
@@ -259,6 +263,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->stamps = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(value));
         return 0;
     }
+    if (!std::strcmp(name, "xj")) {
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->xj = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "jit")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->jit = int(value);
@@ -278,8 +287,22 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
     ++p.uses;
-    const bool jit_ok = p.m == 8 && p.d_idx && !p.jit_failed && jit_supported(8, p.K, p.R) &&
-                        (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= 2)));
+    const bool policy = p.m == 8 && p.d_idx && (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= 2)));
+    // bit-plane XOR kernel: slot * stride must fit the kernel's 32-bit scalar offsets
+    int64_t max_in = 0, max_out = 0;
+    for (int32_t v : p.in_slots) max_in = std::max<int64_t>(max_in, v);
+    for (int j = 0; j < p.R; ++j) max_out = std::max<int64_t>(max_out, p.out_slots[size_t(j)]);
+    const bool xj_ok = policy && c->xj && !p.xj_failed && xj_supported(p.m, p.K, p.R) && S >= 2048 &&
+                       (max_in + 1) * src_sym < (int64_t(1) << 31) && (max_out + 1) * dst_sym < (int64_t(1) << 31);
+    if (xj_ok && !p.xj) {
+        if (xj_build(p.matrix, p.K, p.R, p.in_slots, p.out_slots, p.xj) || !p.xj) {
+            std::fprintf(stderr, "librs_amd: XOR kernel unavailable for a %dx%d matrix; using the next kernel\n", p.R,
+                         p.K);
+            p.xj_failed = true;
+            p.xj.reset();
+        }
+    }
+    const bool jit_ok = policy && !(xj_ok && p.xj) && !p.jit_failed && jit_supported(8, p.K, p.R);
     if (jit_ok && !p.jit) {
         const Gamma8& g = gamma8();
         std::vector<uint8_t> cg(p.matrix.size());
@@ -309,6 +332,22 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.mode = c->m8_mode;
     a.stamps = c->stamps;
     const int nt32 = (p.R + 31) / 32;
+    if (xj_ok && p.xj) {
+        XJArgs x{};
+        x.src = src;
+        x.src_stripe = src_stripe;
+        x.dst = dst;
+        x.dst_stripe = dst_stripe;
+        x.src_sym = int32_t(src_sym);
+        x.dst_sym = int32_t(dst_sym);
+        c->last_kernel = p.xj->name;
+        // 256-byte column chunks up to the last full 2 KiB boundary; the rest by the generic tail kernel
+        int rc = xj_launch(*p.xj, x, int64_t(n_stripes), (a.nbytes / 2048) * (2048 / kXjChunk), st);
+        if (rc) return rc;
+        launch_m8_tail(a, int64_t(n_stripes), unsigned(nt32), st);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (jit_ok && p.jit) {
         const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
         c->last_kernel = p.jit->name;
@@ -428,10 +467,48 @@ extern "C" int rsg_jit_precompile(uint16_t k, uint16_t r, const bool* is_erased,
         if (cnt != t || t > r) return RS_ERR_INVALID;
     }
     codec_matrix(pos, k, r, is_erased, M, in, outs);
+    if (xj_supported(8, int(in.size()), int(outs.size())))
+        return xj_precompile(M, int(in.size()), int(outs.size()), in, outs);
     const Gamma8& g = gamma8();
     std::vector<uint8_t> cg(M.size());
     for (size_t e = 0; e < cg.size(); ++e) cg[e] = uint8_t(g.coord(M[e]));
     return jit_precompile(cg, int(in.size()), int(outs.size()));
+}
+
+extern "C" int rsg_xj_source(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, char* buf, size_t cap,
+                             size_t* len) {
+    if (uint32_t(k) + r > kN) return RS_ERR_INVALID;
+    std::vector<uint16_t> pos = code_positions(k, r), M;
+    if (subfield_degree(pos) > 8) return RS_ERR_INVALID;
+    if (is_erased) {
+        size_t cnt = 0;
+        for (size_t i = 0; i < size_t(k) + r; ++i) cnt += is_erased[i] ? 1 : 0;
+        if (cnt != t || t > r) return RS_ERR_INVALID;
+    }
+    std::vector<int32_t> in, outs;
+    codec_matrix(pos, k, r, is_erased, M, in, outs);
+    if (!xj_supported(8, int(in.size()), int(outs.size()))) return RS_ERR_INVALID;
+    const std::string src = xj_source(M, int(in.size()), int(outs.size()), in, outs);
+    if (len) *len = src.size();
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, src.size());
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return 0;
+}
+
+extern "C" int rsg_xj_basis(int32_t* pivots, uint16_t* beta_y, uint8_t* bits256) {
+    const XjBasis& B = xj_basis();
+    if (pivots)
+        for (int t = 0; t < 8; ++t) pivots[t] = B.pivots[t];
+    if (beta_y)
+        for (int t = 0; t < 8; ++t) beta_y[t] = B.beta_y[t];
+    if (bits256) {
+        const Gamma8& g = gamma8();
+        for (int b = 0; b < 256; ++b) bits256[b] = B.bits(g.to_elem[b]);
+    }
+    return 0;
 }
 
 extern "C" int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red) {

@@ -145,9 +145,9 @@ static int compile(const std::string& src, std::vector<char>& code) {
 }
 
 // Code object for `src` from the disk cache, else compiled with hiprtc and stored there.
-static int jit_code(const std::string& src, uint64_t h, std::vector<char>& code) {
-    char name[40];
-    std::snprintf(name, sizeof name, "v1_%016llx.co", static_cast<unsigned long long>(h));
+int jit_code(const std::string& src, const char* prefix, uint64_t h, std::vector<char>& code) {
+    char name[48];
+    std::snprintf(name, sizeof name, "%s_%016llx.co", prefix, static_cast<unsigned long long>(h));
     const std::string dir = cache_dir();
     if (!dir.empty()) {
         std::ifstream f(dir + "/" + name, std::ios::binary);
@@ -167,29 +167,21 @@ static int jit_code(const std::string& src, uint64_t h, std::vector<char>& code)
     return 0;
 }
 
-int jit_precompile(const std::vector<uint8_t>& cg, int K, int R) {
-    if (!jit_supported(8, K, R)) return 0;
-    const std::string src = jit_source(cg, K, R, nullptr);
-    std::vector<char> code;
-    return jit_code(src, fnv1a(src), code) ? 3 : 0;
-}
+uint64_t jit_hash(const std::string& s) { return fnv1a(s); }
 
 static std::mutex g_jit_mu;
 static std::map<std::pair<int, uint64_t>, std::shared_ptr<JitModule>> g_jit_mods;
 
-int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitKernel>& out) {
-    out.reset();
-    if (!jit_supported(8, K, R)) return 0;
-    std::vector<int32_t> boff;
-    const std::string src = jit_source(cg, K, R, &boff);
+int jit_module(const std::string& src, const char* prefix, std::shared_ptr<JitModule>& out, uint64_t* hash) {
     const uint64_t h = fnv1a(src);
+    if (hash) *hash = h;
     int device = 0;
     (void)hipGetDevice(&device);
     std::lock_guard<std::mutex> lk(g_jit_mu);
     std::shared_ptr<JitModule>& slot = g_jit_mods[{device, h}];
     if (!slot) {
         std::vector<char> code;
-        if (jit_code(src, h, code)) return 3;
+        if (jit_code(src, prefix, h, code)) return 3;
         auto mod = std::make_shared<JitModule>();
         mod->device = device;
         hipError_t e = hipModuleLoadData(&mod->mod, code.data());
@@ -199,6 +191,29 @@ int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitK
         }
         slot = mod;
     }
+    out = slot;
+    return 0;
+}
+
+hipModule_t jit_module_handle(const JitModule& m) { return m.mod; }
+
+int jit_precompile(const std::vector<uint8_t>& cg, int K, int R) {
+    if (!jit_supported(8, K, R)) return 0;
+    const std::string src = jit_source(cg, K, R, nullptr);
+    std::vector<char> code;
+    return jit_code(src, "v1", fnv1a(src), code) ? 3 : 0;
+}
+
+int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitKernel>& out) {
+    out.reset();
+    if (!jit_supported(8, K, R)) return 0;
+    std::vector<int32_t> boff;
+    const std::string src = jit_source(cg, K, R, &boff);
+    uint64_t h = 0;
+    std::shared_ptr<JitModule> slot;
+    if (jit_module(src, "v1", slot, &h)) return 3;
+    int device = 0;
+    (void)hipGetDevice(&device);
     auto k = std::make_unique<JitKernel>();
     k->mod = slot;
     k->device = device;

@@ -42,6 +42,12 @@ int jit_build(const std::vector<uint8_t>& cg, int K, int R, std::unique_ptr<JitK
 int jit_precompile(const std::vector<uint8_t>& cg, int K, int R);
 // Launches over `nchunks_1k` full 1 KiB column chunks of every stripe (v.boff is filled in here).
 int jit_launch(const JitKernel& k, V1Args v, int64_t n_stripes, hipStream_t st);
+// Shared hiprtc machinery (also used by rs_xj.cpp): code object from the disk cache (file
+// <prefix>_<hash>.co) or compiled; module per (device, source hash), loaded once.
+int jit_code(const std::string& src, const char* prefix, uint64_t h, std::vector<char>& code);
+uint64_t jit_hash(const std::string& s);
+int jit_module(const std::string& src, const char* prefix, std::shared_ptr<JitModule>& out, uint64_t* hash);
+hipModule_t jit_module_handle(const JitModule& m);
 // Source text of the specialised kernel and the per-block byte offsets (tests / inspection).
 std::string jit_source(const std::vector<uint8_t>& cg, int K, int R, std::vector<int32_t>* boff);
 

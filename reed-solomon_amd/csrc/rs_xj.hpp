@@ -1,0 +1,73 @@
+// rs_xj.hpp -- bit-plane XOR kernels: matrix-specialised m <= 8 encode/decode compiled at run time.
+//
+// Every coefficient c of a GF(256)-valued coding matrix is split into 8 bit-planes over a fixed basis
+// {beta_t} of GF(256):  c = sum_t b_t(c) beta_t.  Then
+//     out_p = sum_i c_{p,i} x_i = sum_t beta_t * u_{p,t},   u_{p,t} = XOR of x_i over {i : b_t(c_{p,i}) = 1},
+// so the K x R matrix apply becomes a pure XOR network on raw GF(2^16) words (8R accumulators), and
+// field multiplication happens once per OUTPUT (8 constant multiplies, Horner in alpha^-1) instead of
+// once per input. The XOR network uses four-Russians tables: per group of 4 inputs the 11 non-trivial
+// subset XORs are built once, so one v_bitop3 (3-input XOR) adds two groups (8 inputs) to an
+// accumulator. All register indices are fixed by the matrix, so the kernel is generated per coding
+// matrix (hiprtc) and cached in memory and on disk, like rs_jit.hpp.
+//
+// Work per 256-byte column of a stripe at k=128, r=32: 4096 XOR3 (rows) + 4 x 352 table XORs +
+// 32 x ~88 finish ops, against ~18000 for the per-input multiple/nibble-table kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace rsamd {
+
+struct JitModule;
+
+// Kernel arguments of rs_xj (plain data; mirrored in the generated source).
+struct XJArgs {
+    const uint8_t* src;  // stripe 0 of the input layout
+    int64_t src_stripe;
+    uint8_t* dst;
+    int64_t dst_stripe;
+    int32_t src_sym, dst_sym;  // symbol strides (slot * stride < 2^31)
+};
+
+struct XjKernel {
+    std::shared_ptr<JitModule> mod;
+    hipFunction_t fn = nullptr;
+    int device = 0;
+    int roles = 0;  // waves per block (8 outputs each)
+    std::string name;
+};
+
+constexpr int kXjOutputsPerRole = 8;
+constexpr int kXjMaxRoles = 16;     // 1024-thread blocks
+constexpr int kXjMaxWork = 6144;    // K * R bound (instruction-cache footprint of the XOR network)
+constexpr int kXjChunk = 256;       // column bytes per block (64 lanes x 4 B)
+
+// Host-side decomposition (no GPU): basis bits of a GF(256) element and the finish map.
+struct XjBasis {
+    int pivots[8];         // coordinate j (alpha^-j basis) carrying bit t
+    uint16_t beta_y[8];    // beta_t in alpha^-j coordinates
+    uint16_t ycoord(uint16_t x) const;  // x = sum_j y_j alpha^-j
+    uint8_t bits(uint16_t c) const;     // b_t(c), c in GF(256)
+    XjBasis();
+
+   private:
+    uint16_t inv_row_[16];  // row j of the inverse of [alpha^-0 .. alpha^-15] over GF(2)
+};
+const XjBasis& xj_basis();
+
+bool xj_supported(int m, int K, int R);
+// M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
+std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
+                      const std::vector<int32_t>& out_slots);
+int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
+             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out);
+int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
+                  const std::vector<int32_t>& out_slots);
+// Launches over the first `nchunks` 256-byte column chunks of every stripe.
+int xj_launch(const XjKernel& k, const XJArgs& a, int64_t n_stripes, int64_t nchunks, hipStream_t st);
+
+}  // namespace rsamd

@@ -206,9 +206,11 @@ def _stream_ptr(stream):
 class Codec:
     """Batched (k, r) engine on one GPU. Buffers are torch uint8 CUDA tensors (or raw pointers)."""
 
-    def __init__(self, k, r, device=0, jit=None, m8_mode=None):
+    def __init__(self, k, r, device=0, jit=None, m8_mode=None, xj=None):
         """jit: None = library default (2), 0/False = generic kernels only, 1/True = specialise every
-        eligible matrix, 2 = encode matrix + decode matrices from their second use."""
+        eligible matrix, 2 = encode matrix + decode matrices from their second use.
+        xj: specialised kernel family, None = library default (1 = bit-plane XOR kernels, rs_xj.hpp),
+        0 = nibble-table rs_v1jit kernels."""
         self.k, self.r, self.device = k, r, device
         h = P()
         rc = _lib.rsg_codec_create(device, k, r, ctypes.byref(h))
@@ -219,6 +221,8 @@ class Codec:
             self.set_option("jit", int(jit))
         if m8_mode is not None:
             self.set_option("m8_mode", m8_mode)
+        if xj is not None:
+            self.set_option("xj", int(xj))
 
     def close(self):
         if getattr(self, "_h", None) and _lib is not None:  # _lib is None during interpreter shutdown

@@ -12,10 +12,11 @@ from _util import case, case_inputs, check_golden, gen_info, manifest, oracle_de
 
 pytestmark = pytest.mark.gpu
 
-# every m <= 8 kernel family: jit = matrix-specialised V = 1 (hiprtc), v1 / idx = generic gpr-index
+# every m <= 8 kernel family: jit = matrix-specialised bit-plane XOR kernel (rs_xj, hiprtc), v1jit =
+# matrix-specialised nibble-table V = 1 kernel (rs_v1jit), v1 / idx = generic gpr-index
 # kernels (one / two dwords per lane), table / mask = compiler-indexed reference kernels; "auto" is
 # the library default policy (JIT for encode, generic then JIT for repeated decode patterns)
-VARIANTS = {"jit": dict(jit=1), "v1": dict(m8_mode=18, jit=0), "idx": dict(m8_mode=2, jit=0),
+VARIANTS = {"jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(m8_mode=18, jit=0), "idx": dict(m8_mode=2, jit=0),
             "table": dict(m8_mode=0, jit=0), "mask": dict(m8_mode=1, jit=0), "auto": dict()}
 
 

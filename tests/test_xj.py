@@ -1,0 +1,87 @@
+"""Bit-plane XOR kernels (reed-solomon_amd/csrc/rs_xj.cpp) on CPU: the generated program, run by the
+instruction emulator tests/xj_emu.py over one 256-byte column, must reproduce the oracle's repair
+and restored symbols bit for bit (encode and decode matrices, partial roles and input groups)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import rs_amd
+from _util import bench_pattern, oracle_decode, oracle_encode
+from xj_emu import Memory, run_block
+
+_lib = rs_amd._lib
+_lib.rsg_xj_source.argtypes = [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16, ctypes.c_char_p,
+                               ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+_lib.rsg_xj_basis.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+
+S = 256
+
+
+def xj_source(k, r, er=None):
+    n = ctypes.c_size_t()
+    t = 0 if er is None else int(er.sum())
+    p = None if er is None else er.ctypes.data
+    assert _lib.rsg_xj_source(k, r, p, t, None, 0, ctypes.byref(n)) == 0
+    buf = ctypes.create_string_buffer(n.value + 1)
+    assert _lib.rsg_xj_source(k, r, p, t, buf, n.value + 1, ctypes.byref(n)) == 0
+    return buf.value.decode()
+
+
+def test_basis_reconstructs_gf256():
+    piv = np.zeros(8, np.int32)
+    beta = np.zeros(8, np.uint16)
+    bits = np.zeros(256, np.uint8)
+    assert _lib.rsg_xj_basis(piv.ctypes.data, beta.ctypes.data, bits.ctypes.data) == 0
+    assert len(set(piv.tolist())) == 8
+    # the 256 bit patterns are a bijection onto GF(256) (linear, so distinct <=> basis)
+    assert len(set(bits.tolist())) == 256 and bits[0] == 0
+
+
+def _random_stripe(k, r, seed):
+    rng = np.random.default_rng(seed)
+    buf = np.zeros((k + r, S), np.uint8)
+    buf[:k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    return buf
+
+
+@pytest.mark.parametrize("k,r", [(4, 2), (10, 4), (13, 11), (128, 32), (30, 17), (200, 55 - 25)])
+def test_xj_encode_matches_oracle(k, r):
+    want = _random_stripe(k, r, k * 1000 + r)
+    assert oracle_encode(k, r, want) == 0
+    mem = Memory((k + r) * S)
+    mem.b[:k * S] = want[:k].reshape(-1)
+    run_block(xj_source(k, r), mem, 0, S, k * S, S)
+    got = mem.b.reshape(k + r, S)
+    assert np.array_equal(got[k:], want[k:])
+
+
+@pytest.mark.parametrize("k,r,kind", [(10, 4, "bench"), (128, 32, "bench"), (128, 32, "rand17"), (37, 12, "mixed"),
+                                      (4, 2, "info_rep")])
+def test_xj_decode_matches_oracle(k, r, kind):
+    full = _random_stripe(k, r, 7 + k + r)
+    assert oracle_encode(k, r, full) == 0
+    er = np.zeros(k + r, bool)
+    rng = np.random.default_rng(k * r)
+    if kind == "bench":
+        er[bench_pattern(k, r)] = True
+    elif kind == "rand17":
+        er[rng.choice(k + r, 17, replace=False)] = True
+    elif kind == "mixed":
+        er[rng.choice(k, 5, replace=False)] = True
+        er[k + rng.choice(r, 4, replace=False)] = True
+    else:
+        er[[1, 4]] = True
+    if not er[:k].any():
+        er[0] = True
+        er[np.nonzero(er)[0][-1]] = False if er.sum() > r else er[np.nonzero(er)[0][-1]]
+    rcv = full.copy()
+    rcv[er] = 0
+    mem = Memory((k + r) * S)
+    mem.b[:] = rcv.reshape(-1)
+    run_block(xj_source(k, r, er), mem, 0, S, 0, S)
+    got = mem.b.reshape(k + r, S)
+    assert np.array_equal(got[:k], full[:k])
+    ref = rcv.copy()
+    assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
+    assert np.array_equal(got, ref)  # erased repair slots stay zero, as in the reference

@@ -1,0 +1,137 @@
+"""CPU emulator for the generated bit-plane XOR kernel (reed-solomon_amd/csrc/rs_xj.cpp).
+
+TEST INFRASTRUCTURE: executes the instruction subset the generator emits (SALU address arithmetic,
+global_load/store_dword, v_xor/v_and/v_lshrrev/v_mul_u32_u24/v_bitop3(0x96)/v_mov, the shared finish
+block entered by s_swappc) for every role wave of one 256-byte column block, so the generator's
+XOR network and finish map can be checked bit-exactly against the oracle without a GPU.
+"""
+import re
+
+import numpy as np
+
+_STR = re.compile(r'^"(.*)\\n"$')
+
+
+def split_source(src):
+    """-> (finish_lines, [role_lines...]) from the generated hiprtc source."""
+    blocks, cur = [], None
+    for line in src.splitlines():
+        line = line.strip()
+        if line.startswith("asm volatile(") or line.endswith("asm volatile("):
+            cur = []
+            blocks.append(cur)
+            continue
+        m = _STR.match(line)
+        if m and cur is not None:
+            cur.append(m.group(1))
+    return blocks[0], blocks[1:]
+
+
+def _vreg(tok):
+    assert tok[0] == "v", tok
+    return int(tok[1:])
+
+
+class Wave:
+    def __init__(self, mem, operands):
+        self.v = np.zeros((128, 64), np.uint32)
+        self.s = np.zeros(128, np.uint64)
+        self.scc = 0
+        self.mem = mem
+        self.ops = operands  # name -> int or np.ndarray (VGPR operand)
+
+    def val(self, tok):
+        tok = tok.strip()
+        if tok.startswith("%["):
+            return self.ops[tok[2:-1]]
+        if tok[0] == "v" and tok[1:].isdigit():
+            return self.v[int(tok[1:])]
+        if tok[0] == "s" and tok[1:].isdigit():
+            return int(self.s[int(tok[1:])])
+        return int(tok, 0) & 0xFFFFFFFF
+
+    def sset(self, tok, x):
+        self.s[int(tok[1:])] = np.uint64(x & 0xFFFFFFFF)
+
+    def vset(self, tok, x):
+        self.v[_vreg(tok)] = np.asarray(x, dtype=np.uint64).astype(np.uint32) if np.ndim(x) else np.uint32(x)
+
+    def pair(self, tok):
+        m = re.match(r"s\[(\d+):(\d+)\]", tok)
+        lo, hi = int(m.group(1)), int(m.group(2))
+        return int(self.s[lo]) | (int(self.s[hi]) << 32)
+
+    def run(self, lines, finish):
+        for ln in lines:
+            if ln.endswith(":"):
+                continue
+            op, _, rest = ln.partition(" ")
+            a = [x.strip() for x in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
+            if op in ("s_nop", "s_waitcnt", "s_branch", "s_getpc_b64", "s_setpc_b64"):
+                continue
+            if op == "s_swappc_b64":
+                self.run(finish, finish)
+            elif op == "s_mov_b32":
+                self.sset(a[0], self.val(a[1]))
+            elif op == "s_mul_i32":
+                self.sset(a[0], self.val(a[1]) * self.val(a[2]))
+            elif op == "s_add_u32":
+                if "L_" in a[2]:
+                    continue  # call-target arithmetic
+                t = self.val(a[1]) + self.val(a[2])
+                self.scc = t >> 32
+                self.sset(a[0], t)
+            elif op == "s_addc_u32":
+                if a[0] == "s57":
+                    continue
+                t = self.val(a[1]) + (self.val(a[2]) & 0xFFFFFFFF) + self.scc
+                self.scc = t >> 32
+                self.sset(a[0], t)
+            elif op == "v_mov_b32":
+                self.vset(a[0], self.val(a[1]))
+            elif op == "v_xor_b32":
+                self.vset(a[0], self.val(a[1]) ^ self.val(a[2]))
+            elif op == "v_and_b32":
+                self.vset(a[0], np.uint32(self.val(a[1])) & self.val(a[2]))
+            elif op == "v_lshrrev_b32":
+                self.vset(a[0], self.val(a[2]) >> np.uint32(self.val(a[1])))
+            elif op == "v_mul_u32_u24":
+                x = self.val(a[2]).astype(np.uint64) & np.uint64(0xFFFFFF)
+                self.vset(a[0], (np.uint64(self.val(a[1]) & 0xFFFFFF) * x) & np.uint64(0xFFFFFFFF))
+            elif op == "v_bitop3_b32":
+                a3, mod = a[3].split()
+                assert mod == "bitop3:0x96", ln
+                self.vset(a[0], self.val(a[1]) ^ self.val(a[2]) ^ self.val(a3))
+            elif op == "global_load_dword":
+                addr = self.pair(a[2]) + self.val(a[1]).astype(np.uint64)
+                self.vset(a[0], self.mem.load32(addr))
+            elif op == "global_store_dword":
+                addr = self.pair(a[2]) + self.val(a[0]).astype(np.uint64)
+                self.mem.store32(addr, self.val(a[1]))
+            else:
+                raise NotImplementedError(ln)
+
+
+class Memory:
+    """Flat little-endian byte space for emulated loads/stores."""
+
+    def __init__(self, nbytes):
+        self.b = np.zeros(nbytes, np.uint8)
+
+    def load32(self, addr):
+        idx = addr.astype(np.int64)[:, None] + np.arange(4)[None, :]
+        return self.b[idx].copy().view("<u4").reshape(-1)
+
+    def store32(self, addr, val):
+        idx = addr.astype(np.int64)[:, None] + np.arange(4)[None, :]
+        self.b[idx.reshape(-1)] = np.ascontiguousarray(val, dtype="<u4").view(np.uint8)
+
+
+def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
+    """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`."""
+    finish, roles = split_source(src)
+    col = (chunk * 256 + np.arange(64) * 4).astype(np.uint32)
+    ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF, dh=dst_base >> 32,
+               ss=src_sym, ds=dst_sym)
+    for lines in roles:
+        Wave(mem, ops).run(lines, finish)
