@@ -499,7 +499,7 @@ extern "C" int rsg_xj_source(uint16_t k, uint16_t r, const bool* is_erased, uint
 }
 
 extern "C" int rsg_xj_basis(int32_t* pivots, uint16_t* beta_y, uint8_t* bits256) {
-    const XjBasis& B = xj_basis();
+    const XjBasis& B = xj_basis(xj_horner());
     if (pivots)
         for (int t = 0; t < 8; ++t) pivots[t] = B.pivots[t];
     if (beta_y)

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <sstream>
 
 #include "gf16.hpp"
@@ -27,51 +28,81 @@ namespace rsamd {
 // ------------------------------------------------------------------------------- host math
 static int parity16(uint32_t v) { return __builtin_popcount(v & 0xFFFFu) & 1; }
 
-XjBasis::XjBasis() {
+// finish instructions per output for basis coordinates `B` (see finish_block)
+static int finish_cost(const uint16_t* B, int horner) {
+    int w[16] = {0};
+    for (int j = 0; j < 16; ++j)
+        for (int t = 0; t < 8; ++t) w[j] += (B[t] >> j) & 1;
+    int jtop = 15;
+    while (jtop > 0 && !w[jtop]) --jtop;
+    int c = w[jtop] > 1 ? w[jtop] / 2 : 0;
+    for (int j = jtop - 1; j >= 0; --j) c += horner ? 3 + (w[j] + 1) / 2 : 4 + (w[j] ? 1 + w[j] / 2 : 1);
+    return c;
+}
+
+XjBasis::XjBasis(int horner_) : horner(horner_) {
     const Field& F = field();
-    // A: column j = alpha^-j (16-bit); invert over GF(2) by Gauss-Jordan on rows.
-    uint32_t row[16];  // row i: bits j = bit i of alpha^-j ; augmented identity in bits 16..31
+    // A: column j = z^j (16-bit); invert over GF(2) by Gauss-Jordan on rows.
+    uint32_t row[16];  // row i: bits j = bit i of z^j ; augmented identity in bits 16..31
     for (int i = 0; i < 16; ++i) {
         uint32_t r = 0;
-        for (int j = 0; j < 16; ++j)
-            if ((F.exp[(kN - j) % kN] >> i) & 1) r |= 1u << j;
+        for (int j = 0; j < 16; ++j) {
+            const uint16_t zj = F.exp[horner ? uint32_t(j) : (kN - uint32_t(j)) % kN];
+            if ((zj >> i) & 1) r |= 1u << j;
+        }
         row[i] = r | (1u << (16 + i));
     }
     for (int c = 0; c < 16; ++c) {
         int p = c;
-        while (!((row[p] >> c) & 1)) ++p;  // A is invertible (alpha^-j are independent)
+        while (!((row[p] >> c) & 1)) ++p;  // the z^j are independent
         std::swap(row[p], row[c]);
         for (int i = 0; i < 16; ++i)
             if (i != c && ((row[i] >> c) & 1)) row[i] ^= row[c];
     }
     for (int j = 0; j < 16; ++j) inv_row_[j] = uint16_t(row[j] >> 16);
-    // RREF basis (pivot = highest set bit) of the GF(256) subspace in alpha^-j coordinates
-    uint16_t piv[16] = {0};
-    bool has[16] = {false};
-    for (int t = 0; t < 8; ++t) {
-        uint16_t v = ycoord(F.exp[(257u * t) % kN]);
-        for (int b = 15; b >= 0; --b) {
-            if (!((v >> b) & 1)) continue;
-            if (has[b]) {
-                v ^= piv[b];
-            } else {
-                has[b] = true;
-                piv[b] = v;
+    // GF(256) = span of gamma^t (gamma = alpha^257) in z-coordinates; for every pivot set whose 8 x 8
+    // minor is invertible, the reduced basis is unique -- keep the cheapest finish
+    uint16_t G[8];
+    for (int t = 0; t < 8; ++t) G[t] = ycoord(F.exp[(257u * t) % kN]);
+    int best = 1 << 30;
+    for (uint32_t set = 0; set < (1u << 16); ++set) {
+        if (__builtin_popcount(set) != 8) continue;
+        int pv[8], n = 0;
+        for (int j = 0; j < 16; ++j)
+            if ((set >> j) & 1) pv[n++] = j;
+        // solve: rows of G restricted to pv -> invert the 8 x 8 minor
+        uint16_t aug[8];
+        for (int t = 0; t < 8; ++t) {
+            uint8_t m = 0;
+            for (int s2 = 0; s2 < 8; ++s2) m |= uint8_t(((G[t] >> pv[s2]) & 1) << s2);
+            aug[t] = uint16_t(m | (1u << (8 + t)));
+        }
+        bool ok = true;
+        for (int c = 0; c < 8 && ok; ++c) {
+            int p = c;
+            while (p < 8 && !((aug[p] >> c) & 1)) ++p;
+            if (p == 8) {
+                ok = false;
                 break;
             }
+            std::swap(aug[p], aug[c]);
+            for (int i = 0; i < 8; ++i)
+                if (i != c && ((aug[i] >> c) & 1)) aug[i] ^= aug[c];
+        }
+        if (!ok) continue;
+        uint16_t B[8];
+        for (int t = 0; t < 8; ++t) {  // basis vector with unit coordinate at pv[t]
+            uint16_t v = 0;
+            for (int i = 0; i < 8; ++i)
+                if ((aug[t] >> (8 + i)) & 1) v ^= G[i];
+            B[t] = v;
+        }
+        const int c = finish_cost(B, horner);
+        if (c < best) {
+            best = c;
+            for (int t = 0; t < 8; ++t) pivots[t] = pv[t], beta_y[t] = B[t];
         }
     }
-    for (int b = 0; b < 16; ++b)  // full reduction
-        if (has[b])
-            for (int q = 0; q < 16; ++q)
-                if (q != b && has[q] && ((piv[q] >> b) & 1)) piv[q] ^= piv[b];
-    int t = 0;
-    for (int b = 0; b < 16; ++b)
-        if (has[b]) {
-            pivots[t] = b;
-            beta_y[t] = piv[b];
-            ++t;
-        }
 }
 
 uint16_t XjBasis::ycoord(uint16_t x) const {
@@ -87,19 +118,61 @@ uint8_t XjBasis::bits(uint16_t c) const {
     return b;
 }
 
-const XjBasis& xj_basis() {
-    static const XjBasis* b = new XjBasis();
-    return *b;
+const XjBasis& xj_basis(int horner) {
+    static const XjBasis* b[2] = {new XjBasis(0), new XjBasis(1)};
+    return *b[horner ? 1 : 0];
 }
 
 bool xj_supported(int m, int K, int R) {
-    return m <= 8 && K >= 1 && R >= 1 && R <= kXjOutputsPerRole * kXjMaxRoles && K * R <= kXjMaxWork;
+    return m <= 8 && K >= 1 && R >= 1 && R <= xj_outputs_per_role() * kXjMaxRoles && K * R <= kXjMaxWork;
 }
 
 // --------------------------------------------------------------------------- code generator
 namespace {
 
-constexpr int kAcc = 8, kRing = 72, kTabA = 96, kTabB = 107, kCol = 118;
+// Generation knobs (defaults = measured best; RS_XJ_* environment variables override them for
+// experiments -- they change the source text, hence the cache key).
+struct XjConfig {
+    int opr = 16;      // outputs per role (wave): 8 -> 64 accumulators (4 waves/SIMD), 16 -> 128 (3 waves/SIMD)
+    int ring = 2;      // input ring slots (group pairs in flight = ring - 1)
+    int buffer = 0;    // 1: buffer_load/store with a V# and one SALU offset per input; 0: global + SGPR pair
+    int spread = 0;    // 1: next pairs' loads interleaved into the row stream; 0: issued as a burst
+    int horner = 0;    // finish: 1 = Horner in alpha (packed-16 ops), 0 = in alpha^-1
+    int ablate = 0;    // timing ablations (wrong results): 1 no finish, 2 no rows, 4 no tables
+    int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
+    XjConfig() {
+        auto env = [](const char* n, int& v) {
+            if (const char* e = std::getenv(n)) v = std::atoi(e);
+        };
+        env("RS_XJ_OPR", opr);
+        env("RS_XJ_RING", ring);
+        env("RS_XJ_BUFFER", buffer);
+        env("RS_XJ_SPREAD", spread);
+        env("RS_XJ_HORNER", horner);
+        env("RS_XJ_ABLATE", ablate);
+        env("RS_XJ_LDS", lds);
+        lds = lds ? std::max(2, std::min(8, lds)) : 0;
+        if (lds) ring = 2;  // VGPR double buffer behind the LDS ring
+        opr = std::max(1, std::min(16, opr));
+        ring = std::max(2, std::min(6, ring));
+        horner = horner ? 1 : 0;
+    }
+    // register map (the column offset is the compiler's %[col] operand register, outside this range)
+    int acc(int q, int t) const { return 1 + 8 * q + t; }
+    int ring_base() const { return 1 + 8 * opr; }
+    int tab(int h) const { return ring_base() + 8 * ring + 11 * h; }
+    int max_vgpr() const { return tab(2) - 1; }
+    // after the XOR network: result of output q, and per-chain temporaries (chains run in batches of 8)
+    int fin(int q) const { return ring_base() + q; }
+    int tmp(int q, int k) const { return ring_base() + opr + 2 * (q % 8) + k; }
+    int cst() const { return ring_base() + opr + 16; }
+    std::string tag() const {
+        char b[80];
+        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d", opr, ring, buffer, spread,
+                      horner, ablate, lds);
+        return b;
+    }
+};
 
 // built-entry register index of subset pattern e (popcount >= 2) within a group's 11 registers
 int built_index(int e) {
@@ -111,10 +184,14 @@ struct Emitter {
     std::vector<std::string> L;
     void e(const std::string& s) { L.push_back(s); }
     template <class... A>
-    void f(const char* fmt, A... a) {
+    std::string fmt(const char* f, A... a) {
         char buf[160];
-        std::snprintf(buf, sizeof buf, fmt, a...);
-        L.emplace_back(buf);
+        std::snprintf(buf, sizeof buf, f, a...);
+        return buf;
+    }
+    template <class... A>
+    void f(const char* f, A... a) {
+        L.push_back(fmt(f, a...));
     }
 };
 
@@ -124,78 +201,95 @@ std::string as_string_literals(const std::vector<std::string>& L) {
     return o;
 }
 
-// The finish block: for every output q, H_q = sum_j alpha^-j v_j with v_j = XOR of u_{q,t} over the t
-// whose beta_t has coordinate j; Horner from the top coordinate down, the 8 chains interleaved.
-std::vector<std::string> finish_block() {
-    const XjBasis& B = xj_basis();
-    std::vector<std::vector<std::string>> chains(8);
-    for (int q = 0; q < 8; ++q) {
-        std::vector<std::string>& c = chains[q];
-        char buf[160];
-        auto add = [&](const char* fmt, auto... a) {
-            std::snprintf(buf, sizeof buf, fmt, a...);
-            c.emplace_back(buf);
-        };
-        const int H = 72 + 4 * q, T1 = H + 1, T2 = H + 2;
-        auto terms = [&](int j) {
-            std::vector<int> r;
-            for (int t = 0; t < 8; ++t)
-                if ((B.beta_y[t] >> j) & 1) r.push_back(kAcc + 8 * q + t);
-            return r;
-        };
-        // fold `rest` (after `first` went into dst) pairwise into dst
-        auto fold = [&](int dst, const std::vector<int>& v, size_t from) {
-            size_t i = from;
-            for (; i + 1 < v.size(); i += 2) add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", dst, dst, v[i], v[i + 1]);
-            if (i < v.size()) add("v_xor_b32 v%d, v%d, v%d", dst, v[i], dst);
-        };
-        int jtop = 15;
-        while (jtop > 0 && terms(jtop).empty()) --jtop;
-        std::vector<int> top = terms(jtop);
-        int cur;
-        if (top.size() == 1) {
-            cur = top[0];
-        } else if (top.empty()) {
-            add("v_mov_b32 v%d, 0", H);
-            cur = H;
-        } else {
-            add("v_xor_b32 v%d, v%d, v%d", H, top[0], top[1]);
-            fold(H, top, 2);
-            cur = H;
-        }
-        for (int j = jtop - 1; j >= 0; --j) {
-            // cur * alpha^-1 per 16-bit lane: (w >> 1) ^ (w & 1 ? 0x8016 : 0)
-            add("v_and_b32 v%d, 0xfffeffff, v%d", T1, cur);
-            add("v_lshrrev_b32 v%d, 1, v%d", T1, T1);
-            add("v_and_b32 v%d, 0x10001, v%d", T2, cur);
-            add("v_mul_u32_u24 v%d, 0x8016, v%d", T2, T2);
-            std::vector<int> v = terms(j);
-            if (v.empty()) {
-                add("v_xor_b32 v%d, v%d, v%d", H, T1, T2);
-            } else {
-                add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", H, T1, T2, v[0]);
-                fold(H, v, 1);
-            }
-            cur = H;
-        }
-        if (cur != H) add("v_mov_b32 v%d, v%d", H, cur);
-    }
+// The finish block: for every output q, H_q = sum_j z^j v_j with v_j = XOR of u_{q,t} over the t whose
+// beta_t has z-coordinate j; Horner from the top coordinate down, up to 8 chains interleaved.
+//   z = alpha:    H <- (H + H per 16-bit lane) ^ (sign mask per lane & 0x2D), then ^ v_j
+//   z = alpha^-1: H <- ((H & 0xfffeffff) >> 1) ^ ((H & 0x10001) * 0x8016) ^ v_j
+std::vector<std::string> finish_block(const XjConfig& C) {
+    const XjBasis& B = xj_basis(C.horner);
     std::vector<std::string> L;
     L.push_back("s_branch L_xj_fin_end");
     L.push_back("L_xj_fin:");
-    const size_t n = chains[0].size();
-    for (size_t i = 0; i < n; ++i)
-        for (int q = 0; q < 8; ++q) L.push_back(chains[q][i]);
+    if (C.horner) L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0x2d002d");
+    for (int q0 = 0; q0 < C.opr; q0 += 8) {
+        const int nc = std::min(8, C.opr - q0);
+        std::vector<std::vector<std::string>> chains(static_cast<size_t>(nc));
+        for (int c = 0; c < nc; ++c) {
+            const int q = q0 + c;
+            std::vector<std::string>& out = chains[size_t(c)];
+            char buf[160];
+            auto add = [&](const char* fmt, auto... a) {
+                std::snprintf(buf, sizeof buf, fmt, a...);
+                out.emplace_back(buf);
+            };
+            const int H = C.fin(q), T1 = C.tmp(q, 0), T2 = C.tmp(q, 1);
+            auto terms = [&](int j) {
+                std::vector<int> r;
+                for (int t = 0; t < 8; ++t)
+                    if ((B.beta_y[t] >> j) & 1) r.push_back(C.acc(q, t));
+                return r;
+            };
+            auto fold = [&](int dst, const std::vector<int>& v, size_t from) {  // v[from..] into dst
+                size_t i = from;
+                for (; i + 1 < v.size(); i += 2)
+                    add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", dst, dst, v[i], v[i + 1]);
+                if (i < v.size()) add("v_xor_b32 v%d, v%d, v%d", dst, v[i], dst);
+            };
+            int jtop = 15;
+            while (jtop > 0 && terms(jtop).empty()) --jtop;
+            std::vector<int> top = terms(jtop);
+            int cur;
+            if (top.size() == 1) {
+                cur = top[0];
+            } else if (top.empty()) {
+                add("v_mov_b32 v%d, 0", H);
+                cur = H;
+            } else {
+                add("v_xor_b32 v%d, v%d, v%d", H, top[0], top[1]);
+                fold(H, top, 2);
+                cur = H;
+            }
+            for (int j = jtop - 1; j >= 0; --j) {
+                std::vector<int> v = terms(j);
+                if (C.horner) {
+                    add("v_pk_add_u16 v%d, v%d, v%d", T1, cur, cur);
+                    add("v_pk_ashrrev_i16 v%d, 15, v%d op_sel_hi:[0,1]", T2, cur);
+                    add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x78", H, T1, T2, C.cst());  // T1 ^ (T2 & C)
+                    fold(H, v, 0);
+                } else {
+                    add("v_and_b32 v%d, 0xfffeffff, v%d", T1, cur);
+                    add("v_lshrrev_b32 v%d, 1, v%d", T1, T1);
+                    add("v_and_b32 v%d, 0x10001, v%d", T2, cur);
+                    add("v_mul_u32_u24 v%d, 0x8016, v%d", T2, T2);
+                    if (v.empty()) {
+                        add("v_xor_b32 v%d, v%d, v%d", H, T1, T2);
+                    } else {
+                        add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", H, T1, T2, v[0]);
+                        fold(H, v, 1);
+                    }
+                }
+                cur = H;
+            }
+            if (cur != H) add("v_mov_b32 v%d, v%d", H, cur);
+        }
+        const size_t n = chains[0].size();
+        for (size_t i = 0; i < n; ++i)
+            for (int c = 0; c < nc; ++c) L.push_back(chains[size_t(c)][i]);
+    }
     L.push_back("s_setpc_b64 s[58:59]");
     L.push_back("L_xj_fin_end:");
     return L;
 }
 
-// One role: outputs p = 8w + q (q < nq) of the R x K bit-plane matrix `cb` (cb[p*K + i] = b(c_{p,i})).
-std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K, int R,
+// One role: outputs p = opr*w + q (q < nq) of the R x K bit-plane matrix `cb` (cb[p*K + i] = b(c_{p,i})).
+// SGPRs: s[32:33] src base, s34 src stride, s[36:37] dst base, s38 dst stride, s[40:55] address pairs
+// (global form) / s[40:47] offsets + s[48:51] src V# + s[52:55] dst V# (buffer form), s[56:59] call,
+// s62 scratch.
+std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<uint8_t>& cb, int K, int R,
                                     const std::vector<int32_t>& in_slots, const std::vector<int32_t>& out_slots) {
     Emitter E;
-    const int p0 = 8 * w, nq = std::min(8, R - p0);
+    const int p0 = C.opr * w, nq = std::min(C.opr, R - p0);
+    const char* COL = "%[col]";
     E.e("s_nop 4");  // "s" operands may come from v_readfirstlane (VALU SGPR write -> VMEM read)
     E.e("s_mov_b32 s32, %[sl]");
     E.e("s_mov_b32 s33, %[sh]");
@@ -203,28 +297,97 @@ std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K
     E.e("s_mov_b32 s36, %[dl]");
     E.e("s_mov_b32 s37, %[dh]");
     E.e("s_mov_b32 s38, %[ds]");
-    E.f("v_mov_b32 v%d, %%[col]", kCol);
-    for (int q = 0; q < nq; ++q) E.f("s_mul_i32 s%d, s38, %d", 64 + q, out_slots[size_t(p0 + q)]);
+    if (C.buffer || C.lds) {  // raw buffer descriptors: base, stride 0, num_records 2^32 - 1, 32-bit data format
+        E.e("s_mov_b32 s48, s32");
+        E.e("s_and_b32 s49, s33, 0xffff");
+        E.e("s_mov_b32 s50, -1");
+        E.e("s_mov_b32 s51, 0x20000");
+        E.e("s_mov_b32 s52, s36");
+        E.e("s_and_b32 s53, s37, 0xffff");
+        E.e("s_mov_b32 s54, -1");
+        E.e("s_mov_b32 s55, 0x20000");
+    }
     const int ngp = (K + 7) / 8;
     auto nload = [&](int g) { return g < ngp ? std::min(8, K - 8 * g) : 0; };
-    auto loads = [&](int g) {
+    // instruction lists of the loads of pair g (address arithmetic first, then the loads)
+    auto load_ops = [&](int g) {
+        std::vector<std::string> ops;
         const int n = nload(g);
         for (int j = 0; j < n; ++j) {
-            E.f("s_mul_i32 s62, s34, %d", in_slots[size_t(8 * g + j)]);
-            E.f("s_add_u32 s%d, s32, s62", 40 + 2 * j);
-            E.f("s_addc_u32 s%d, s33, 0", 41 + 2 * j);
+            const int dst = C.ring_base() + 8 * (g % C.ring) + j;
+            const int slot = in_slots[size_t(8 * g + j)];
+            if (C.buffer) {
+                ops.push_back(E.fmt("s_mul_i32 s%d, s34, %d", 40 + j, slot));
+                ops.push_back(E.fmt("buffer_load_dword v%d, %s, s[48:51], s%d offen", dst, COL, 40 + j));
+            } else {
+                ops.push_back(E.fmt("s_mul_i32 s62, s34, %d", slot));
+                ops.push_back(E.fmt("s_add_u32 s%d, s32, s62", 40 + 2 * j));
+                ops.push_back(E.fmt("s_addc_u32 s%d, s33, 0", 41 + 2 * j));
+                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]", dst, COL, 40 + 2 * j, 41 + 2 * j));
+            }
         }
-        for (int j = 0; j < n; ++j)
-            E.f("global_load_dword v%d, v%d, s[%d:%d]", kRing + 8 * (g % 3) + j, kCol, 40 + 2 * j, 41 + 2 * j);
+        return ops;
     };
-    bool init[8][8] = {};
-    loads(0);
-    loads(1);
+    bool init[16][8] = {};
+    const int ahead = C.ring - 1;  // pairs in flight beyond the current one
+    const int D = C.lds;
+    // LDS-DMA ring: pair g lives in LDS slot g % D of this wave's region (s39 = region base); each lane's
+    // dword of input j at slot * 2048 + j * 256 + 4 * lane (%[la] = region base + 4 * lane)
+    auto dma_ops = [&](int g) {
+        std::vector<std::string> ops;
+        for (int j = 0; j < nload(g); ++j) {
+            ops.push_back(E.fmt("s_mul_i32 s%d, s34, %d", 40 + j, in_slots[size_t(8 * g + j)]));
+            ops.push_back(E.fmt("s_add_u32 m0, s39, %d", (g % D) * 2048 + j * 256));
+            ops.push_back("s_nop 0");
+            ops.push_back(E.fmt("buffer_load_dword %s, s[48:51], s%d offen lds", COL, 40 + j));
+        }
+        return ops;
+    };
+    auto ds_ops = [&](int g) {
+        std::vector<std::string> ops;
+        for (int j = 0; j < nload(g); ++j)
+            ops.push_back(E.fmt("ds_read_b32 v%d, %%[la] offset:%d", C.ring_base() + 8 * (g % C.ring) + j,
+                                (g % D) * 2048 + j * 256));
+        return ops;
+    };
+    if (D) {
+        E.e("s_mov_b32 s63, m0");
+        E.e("s_mov_b32 s39, %[lb]");
+        for (int g = 0; g < std::min(D, ngp); ++g)
+            for (auto& op : dma_ops(g)) E.e(op);
+        int pend = 0;
+        for (int x = 1; x < std::min(D, ngp); ++x) pend += nload(x);
+        E.f("s_waitcnt vmcnt(%d)", pend);
+        for (auto& op : ds_ops(0)) E.e(op);
+    } else {
+        for (int g = 0; g < ahead; ++g)
+            for (auto& op : load_ops(g)) E.e(op);
+    }
     for (int g = 0; g < ngp; ++g) {
-        loads(g + 2);
-        E.f("s_waitcnt vmcnt(%d)", nload(g + 1) + nload(g + 2));
+        std::vector<std::string> next, mid;
+        if (D) {
+            E.e("s_waitcnt lgkmcnt(0)");
+            if (g + 1 < ngp) {  // pair g+1 has landed in LDS once only pairs g+2 .. g+D-1 are pending
+                int pend = 0;
+                for (int x = g + 2; x <= std::min(g + D - 1, ngp - 1); ++x) pend += nload(x);
+                mid.push_back(E.fmt("s_waitcnt vmcnt(%d)", pend));
+                for (auto& op : ds_ops(g + 1)) mid.push_back(op);
+            }
+            if (g + D < ngp)  // into the slot pair g has left (its ds_reads completed above)
+                for (auto& op : dma_ops(g + D)) mid.push_back(op);
+        } else {
+            // loads issued so far beyond pair g: pairs g+1 .. g+ahead-1 (g+ahead is issued below)
+            int pending = 0;
+            for (int x = g + 1; x < g + ahead; ++x) pending += nload(x);
+            next = load_ops(g + ahead);
+            if (!C.spread) {
+                for (auto& op : next) E.e(op);
+                pending += nload(g + ahead);
+            }
+            E.f("s_waitcnt vmcnt(%d)", pending);
+        }
         // patterns of this role's rows over the pair's two groups
-        int pat[8][8][2];
+        int pat[16][8][2];
         bool need[2][16] = {};
         for (int q = 0; q < nq; ++q)
             for (int t = 0; t < 8; ++t)
@@ -237,11 +400,12 @@ std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K
                     pat[q][t][h] = e;
                     need[h][e] = true;
                 }
-        auto single = [&](int h, int jj) { return kRing + 8 * (g % 3) + 4 * h + jj; };
+        auto single = [&](int h, int jj) { return C.ring_base() + 8 * (g % C.ring) + 4 * h + jj; };
         auto reg = [&](int h, int e) {
             if (__builtin_popcount(e) == 1) return single(h, __builtin_ctz(e));
-            return (h ? kTabB : kTabA) + built_index(e);
+            return C.tab(h) + built_index(e);
         };
+        std::vector<std::string> body;
         for (int h = 0; h < 2; ++h) {
             // popcount 2 and 3 straight from the inputs; 15 from a built triple or pair
             bool built[16] = {};
@@ -251,9 +415,9 @@ std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K
                 for (int jj = 0; jj < 4; ++jj)
                     if ((e >> jj) & 1) b[nb++] = single(h, jj);
                 if (nb == 2)
-                    E.f("v_xor_b32 v%d, v%d, v%d", reg(h, e), b[0], b[1]);
+                    body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", reg(h, e), b[0], b[1]));
                 else
-                    E.f("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", reg(h, e), b[0], b[1], b[2]);
+                    body.push_back(E.fmt("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", reg(h, e), b[0], b[1], b[2]));
                 built[e] = true;
             }
             if (need[h][15]) {
@@ -263,49 +427,87 @@ std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K
                 for (int e : {3, 5, 6, 9, 10, 12})
                     if (built[e]) pair = e;
                 if (tri >= 0) {
-                    E.f("v_xor_b32 v%d, v%d, v%d", reg(h, 15), reg(h, tri), single(h, __builtin_ctz(15 & ~tri)));
+                    body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", reg(h, 15), reg(h, tri),
+                                         single(h, __builtin_ctz(15 & ~tri))));
                 } else {
                     if (pair < 0) {
                         pair = 3;
-                        E.f("v_xor_b32 v%d, v%d, v%d", reg(h, 3), single(h, 0), single(h, 1));
+                        body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", reg(h, 3), single(h, 0), single(h, 1)));
                     }
                     const int rest = 15 & ~pair;
-                    E.f("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", reg(h, 15), reg(h, pair),
-                        single(h, __builtin_ctz(rest)), single(h, 31 - __builtin_clz(rest)));
+                    body.push_back(E.fmt("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", reg(h, 15), reg(h, pair),
+                                         single(h, __builtin_ctz(rest)), single(h, 31 - __builtin_clz(rest))));
                 }
             }
         }
+        if (C.ablate & 4) body.clear();
+        for (auto& op : mid) body.push_back(op);  // LDS ring: next pair's reads + refills after the tables
+        const size_t nbuild = body.size();
         for (int t = 0; t < 8; ++t)
             for (int q = 0; q < nq; ++q) {
-                const int a = pat[q][t][0], b = pat[q][t][1], acc = kAcc + 8 * q + t;
-                if (!a && !b) continue;
+                const int a = pat[q][t][0], b = pat[q][t][1], acc = C.acc(q, t);
+                if ((!a && !b) || (C.ablate & 2)) continue;
                 if (!init[q][t]) {
                     if (a && b)
-                        E.f("v_xor_b32 v%d, v%d, v%d", acc, reg(0, a), reg(1, b));
+                        body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, reg(0, a), reg(1, b)));
                     else
-                        E.f("v_mov_b32 v%d, v%d", acc, a ? reg(0, a) : reg(1, b));
+                        body.push_back(E.fmt("v_mov_b32 v%d, v%d", acc, a ? reg(0, a) : reg(1, b)));
                     init[q][t] = true;
                 } else if (a && b) {
-                    E.f("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", acc, acc, reg(0, a), reg(1, b));
+                    body.push_back(E.fmt("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", acc, acc, reg(0, a), reg(1, b)));
                 } else {
-                    E.f("v_xor_b32 v%d, v%d, v%d", acc, a ? reg(0, a) : reg(1, b), acc);
+                    body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, a ? reg(0, a) : reg(1, b), acc));
                 }
             }
+        if (C.spread && !next.empty()) {
+            // the next pair's loads go into this pair's row stream (after the table build: their ring
+            // slot was last read by the previous pair), one every few rows
+            std::vector<std::string> merged(body.begin(), body.begin() + long(nbuild));
+            const size_t rows = body.size() - nbuild, nn = next.size();
+            size_t k = 0;
+            for (size_t i = 0; i < rows; ++i) {
+                merged.push_back(body[nbuild + i]);
+                while (k < nn && k * rows < (i + 1) * nn) merged.push_back(next[k++]);
+            }
+            while (k < nn) merged.push_back(next[k++]);
+            body.swap(merged);
+        }
+        for (auto& op : body) E.e(op);
     }
     for (int q = 0; q < nq; ++q)
         for (int t = 0; t < 8; ++t)
-            if (!init[q][t]) E.f("v_mov_b32 v%d, 0", kAcc + 8 * q + t);
+            if (!init[q][t]) E.f("v_mov_b32 v%d, 0", C.acc(q, t));
     // finish (shared block; returns through s[58:59]); L_xj_fin precedes every role block
-    E.e("s_getpc_b64 s[56:57]");
-    E.e("s_add_u32 s56, s56, L_xj_fin-.");
-    E.e("s_addc_u32 s57, s57, -1");
-    E.e("s_swappc_b64 s[58:59], s[56:57]");
-    for (int q = 0; q < nq; ++q) {
-        E.f("s_add_u32 s%d, s36, s%d", 40 + 2 * q, 64 + q);
-        E.f("s_addc_u32 s%d, s37, 0", 41 + 2 * q);
+    if (!(C.ablate & 1)) {
+        E.e("s_getpc_b64 s[56:57]");
+        E.e("s_add_u32 s56, s56, L_xj_fin-.");
+        E.e("s_addc_u32 s57, s57, -1");
+        E.e("s_swappc_b64 s[58:59], s[56:57]");
+    } else {  // keep the network live: store accumulator 0 of each output
+        for (int q = 0; q < nq; ++q) E.f("v_mov_b32 v%d, v%d", C.fin(q), C.acc(q, 0));
     }
-    for (int q = 0; q < nq; ++q) E.f("global_store_dword v%d, v%d, s[%d:%d]", kCol, 72 + 4 * q, 40 + 2 * q, 41 + 2 * q);
+    for (int q0 = 0; q0 < nq; q0 += 8) {  // stores in batches of 8 address registers
+        const int nb = std::min(8, nq - q0);
+        for (int j = 0; j < nb; ++j) {
+            const int slot = out_slots[size_t(p0 + q0 + j)];
+            if (C.buffer) {
+                E.f("s_mul_i32 s%d, s38, %d", 40 + j, slot);
+            } else {
+                E.f("s_mul_i32 s62, s38, %d", slot);
+                E.f("s_add_u32 s%d, s36, s62", 40 + 2 * j);
+                E.f("s_addc_u32 s%d, s37, 0", 41 + 2 * j);
+            }
+        }
+        for (int j = 0; j < nb; ++j) {
+            if (C.buffer)
+                E.f("buffer_store_dword v%d, %s, s[52:55], s%d offen", C.fin(q0 + j), COL, 40 + j);
+            else
+                E.f("global_store_dword %s, v%d, s[%d:%d]", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j);
+        }
+        if (q0 + 8 < nq) E.e("s_waitcnt vmcnt(0)");  // address registers are reused by the next batch
+    }
     E.e("s_waitcnt vmcnt(0)");
+    if (D) E.e("s_mov_b32 m0, s63");
     return E.L;
 }
 
@@ -313,39 +515,47 @@ std::vector<std::string> role_block(int w, const std::vector<uint8_t>& cb, int K
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots) {
-    const XjBasis& B = xj_basis();
+    const XjConfig C;
+    const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
     for (size_t e = 0; e < M.size(); ++e) cb[e] = B.bits(M[e]);
-    const int roles = (R + kXjOutputsPerRole - 1) / kXjOutputsPerRole;
+    const int roles = (R + C.opr - 1) / C.opr;
     std::ostringstream o;
     o << "typedef unsigned int uint32_t; typedef int int32_t; typedef unsigned char uint8_t;\n"
          "typedef long long int64_t; typedef unsigned long long uint64_t;\n"
          "struct XJArgs { const uint8_t* src; int64_t src_stripe; uint8_t* dst; int64_t dst_stripe;"
          " int32_t src_sym, dst_sym; };\n"
-      << "// K=" << K << " R=" << R << " roles=" << roles << "\n"
+      << "// K=" << K << " R=" << R << " roles=" << roles << " " << C.tag() << "\n"
       << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles << ") rs_xj(XJArgs a) {\n"
-      << "  asm volatile(\n" << as_string_literals(finish_block()) << "  ::: \"memory\");\n"
+      << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds[" << std::max(1, roles * C.lds * 512) << "];\n"
+      << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
       << "  const uint64_t stripe = blockIdx.y;\n"
          "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
          "  const uint64_t db = (uint64_t)a.dst + stripe * (uint64_t)a.dst_stripe;\n"
          "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
          "  const uint32_t sl = (uint32_t)sb, sh = (uint32_t)(sb >> 32), dl = (uint32_t)db, dh = (uint32_t)(db >> 32);\n"
          "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
+         "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
+      << C.lds * 2048 << "u;\n"
+         "  const uint32_t la = lb + (threadIdx.x & 63u) * 4u;\n"
          "  switch (role) {\n";
     std::string clob;
-    for (int v = 8; v <= 119; ++v) clob += "\"v" + std::to_string(v) + "\", ";
-    for (int s = 32; s <= 71; ++s) clob += "\"s" + std::to_string(s) + "\", ";
+    for (int v = 1; v <= C.max_vgpr(); ++v) clob += "\"v" + std::to_string(v) + "\", ";
+    for (int s = 32; s <= 63; ++s) clob += "\"s" + std::to_string(s) + "\", ";
     clob += "\"scc\", \"memory\"";
     for (int w = 0; w < roles; ++w) {
         o << "  case " << w << ": asm volatile(\n"
-          << as_string_literals(role_block(w, cb, K, R, in_slots, out_slots))
-          << "  : : [col] \"v\"(col), [sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
-             " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym)\n  : "
+          << as_string_literals(role_block(C, w, cb, K, R, in_slots, out_slots))
+          << "  : : [col] \"v\"(col), [la] \"v\"(la), [sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
+             " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)\n  : "
           << clob << ");\n    break;\n";
     }
     o << "  }\n}\n";
     return o.str();
 }
+
+int xj_outputs_per_role() { return XjConfig().opr; }
+int xj_horner() { return XjConfig().horner; }
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                   const std::vector<int32_t>& out_slots) {
@@ -366,7 +576,7 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     auto k = std::make_unique<XjKernel>();
     k->mod = mod;
     (void)hipGetDevice(&k->device);
-    k->roles = (R + kXjOutputsPerRole - 1) / kXjOutputsPerRole;
+    k->roles = (R + xj_outputs_per_role() - 1) / xj_outputs_per_role();
     if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), "rs_xj") != hipSuccess) return 3;
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));

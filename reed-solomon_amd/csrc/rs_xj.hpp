@@ -41,25 +41,32 @@ struct XjKernel {
     std::string name;
 };
 
-constexpr int kXjOutputsPerRole = 8;
 constexpr int kXjMaxRoles = 16;     // 1024-thread blocks
 constexpr int kXjMaxWork = 6144;    // K * R bound (instruction-cache footprint of the XOR network)
 constexpr int kXjChunk = 256;       // column bytes per block (64 lanes x 4 B)
 
 // Host-side decomposition (no GPU): basis bits of a GF(256) element and the finish map.
+// Finish = Horner over a power basis {z^j} of GF(2^16): out = sum_j z^j v_j, v_j = XOR of the u_t whose
+// beta_t has z-coordinate j. horner 1: z = alpha (packed-16 shift + sign-mask reduction, 3 ops per
+// step), coordinates = raw bits; horner 0: z = alpha^-1 (mask/shift/multiply, 4 ops per step).
+// beta_t is the reduced basis of GF(256) whose coordinates at pivots[t] form the identity; the pivot set
+// minimises the finish cost.
 struct XjBasis {
-    int pivots[8];         // coordinate j (alpha^-j basis) carrying bit t
-    uint16_t beta_y[8];    // beta_t in alpha^-j coordinates
-    uint16_t ycoord(uint16_t x) const;  // x = sum_j y_j alpha^-j
+    int horner;            // 1: z = alpha, 0: z = alpha^-1
+    int pivots[8];         // z-coordinate j carrying bit t
+    uint16_t beta_y[8];    // beta_t in z-coordinates
+    uint16_t ycoord(uint16_t x) const;  // x = sum_j y_j z^j
     uint8_t bits(uint16_t c) const;     // b_t(c), c in GF(256)
-    XjBasis();
+    explicit XjBasis(int horner);
 
    private:
-    uint16_t inv_row_[16];  // row j of the inverse of [alpha^-0 .. alpha^-15] over GF(2)
+    uint16_t inv_row_[16];  // row j of the inverse of [z^0 .. z^15] over GF(2)
 };
-const XjBasis& xj_basis();
+const XjBasis& xj_basis(int horner);
+int xj_horner();  // generation setting (RS_XJ_HORNER, default 1)
 
 bool xj_supported(int m, int K, int R);
+int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 8)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots);

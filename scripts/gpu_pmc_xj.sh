@@ -1,0 +1,17 @@
+# PMC passes over the k=128 r=32 encode kernel (scripts/pmc_xj.py), one counter group per run.
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+D=gpurun_out/pmcxj
+mkdir -p $D
+timeout -k 10 120 rocprofv3 -L > $D/avail.txt 2>&1; echo "list rc=$?"
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+           "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $grp -d $D/p$i -o run -- python3 scripts/pmc_xj.py ${KIND:-jit} 1024 > $D/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  case $rc in 124|134|137|139) exit $rc;; esac
+done
+exit 0

@@ -33,7 +33,7 @@ fetch_b = med(fetch) * 1024 * 2
 write_b = med(write) * 1024
 import hashlib
 h = hashlib.sha256()
-for f in ("csrc/rs_kernels.hip", "csrc/gen_asm.py", "csrc/rs_device.h"):
+for f in ("csrc/rs_kernels.hip", "csrc/gen_asm.py", "csrc/rs_device.h", "csrc/rs_xj.cpp"):
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd", f), "rb") as fh:
         h.update(fh.read())
 print(json.dumps({"src_hash": h.hexdigest()[:16], "kernel": kern, "bench_kernel": bench_kernel, "config": cfg,

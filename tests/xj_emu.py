@@ -34,9 +34,11 @@ def _vreg(tok):
 
 class Wave:
     def __init__(self, mem, operands):
-        self.v = np.zeros((128, 64), np.uint32)
+        self.v = np.zeros((256, 64), np.uint32)
         self.s = np.zeros(128, np.uint64)
         self.scc = 0
+        self.m0 = 0
+        self.lds = None  # np.uint8 array shared by the block's waves
         self.mem = mem
         self.ops = operands  # name -> int or np.ndarray (VGPR operand)
 
@@ -44,6 +46,8 @@ class Wave:
         tok = tok.strip()
         if tok.startswith("%["):
             return self.ops[tok[2:-1]]
+        if tok == "m0":
+            return self.m0
         if tok[0] == "v" and tok[1:].isdigit():
             return self.v[int(tok[1:])]
         if tok[0] == "s" and tok[1:].isdigit():
@@ -51,6 +55,9 @@ class Wave:
         return int(tok, 0) & 0xFFFFFFFF
 
     def sset(self, tok, x):
+        if tok == "m0":
+            self.m0 = x & 0xFFFFFFFF
+            return
         self.s[int(tok[1:])] = np.uint64(x & 0xFFFFFFFF)
 
     def vset(self, tok, x):
@@ -60,6 +67,11 @@ class Wave:
         m = re.match(r"s\[(\d+):(\d+)\]", tok)
         lo, hi = int(m.group(1)), int(m.group(2))
         return int(self.s[lo]) | (int(self.s[hi]) << 32)
+
+    def vsharp(self, tok):
+        m = re.match(r"s\[(\d+):(\d+)\]", tok)
+        lo = int(m.group(1))
+        return int(self.s[lo]) | ((int(self.s[lo + 1]) & 0xFFFF) << 32)
 
     def run(self, lines, finish):
         for ln in lines:
@@ -73,6 +85,8 @@ class Wave:
                 self.run(finish, finish)
             elif op == "s_mov_b32":
                 self.sset(a[0], self.val(a[1]))
+            elif op == "s_and_b32":
+                self.sset(a[0], self.val(a[1]) & self.val(a[2]))
             elif op == "s_mul_i32":
                 self.sset(a[0], self.val(a[1]) * self.val(a[2]))
             elif op == "s_add_u32":
@@ -100,14 +114,55 @@ class Wave:
                 self.vset(a[0], (np.uint64(self.val(a[1]) & 0xFFFFFF) * x) & np.uint64(0xFFFFFFFF))
             elif op == "v_bitop3_b32":
                 a3, mod = a[3].split()
-                assert mod == "bitop3:0x96", ln
-                self.vset(a[0], self.val(a[1]) ^ self.val(a[2]) ^ self.val(a3))
+                tt = int(mod.split(":")[1], 0)
+                x, y, z = (np.broadcast_to(np.uint32(self.val(t)), (64,)) for t in (a[1], a[2], a3))
+                r = np.zeros(64, np.uint32)
+                for idx in range(8):  # truth table index = src0 << 2 | src1 << 1 | src2
+                    if (tt >> idx) & 1:
+                        m0 = x if idx & 4 else ~x
+                        m1 = y if idx & 2 else ~y
+                        m2 = z if idx & 1 else ~z
+                        r |= m0 & m1 & m2
+                self.vset(a[0], r)
+            elif op == "v_pk_add_u16":
+                x, y = self.val(a[1]), self.val(a[2])
+                lo = ((x & 0xFFFF) + (y & 0xFFFF)) & 0xFFFF
+                hi = ((x >> 16) + (y >> 16)) & 0xFFFF
+                self.vset(a[0], lo | (hi << np.uint32(16)))
+            elif op == "v_pk_ashrrev_i16":
+                src, mod = a[2].split()
+                assert mod == "op_sel_hi:[0,1]", ln  # shift count from the low half for both lanes
+                sh = self.val(a[1]) & 0xF
+                x = self.val(src)
+                lo = ((x & 0xFFFF).astype(np.uint16).view(np.int16) >> sh).view(np.uint16).astype(np.uint32)
+                hi = ((x >> 16).astype(np.uint16).view(np.int16) >> sh).view(np.uint16).astype(np.uint32)
+                self.vset(a[0], lo | (hi << np.uint32(16)))
             elif op == "global_load_dword":
                 addr = self.pair(a[2]) + self.val(a[1]).astype(np.uint64)
                 self.vset(a[0], self.mem.load32(addr))
             elif op == "global_store_dword":
                 addr = self.pair(a[2]) + self.val(a[0]).astype(np.uint64)
                 self.mem.store32(addr, self.val(a[1]))
+            elif op == "buffer_load_dword" and ln.endswith(" lds"):
+                # LDS DMA: a[0] = voffset, a[1] = V#, a[2] = "soffset offen lds"
+                addr = self.vsharp(a[1]) + self.val(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
+                data = self.mem.load32(addr)
+                dst = self.m0 + 4 * np.arange(64)
+                idx = dst[:, None] + np.arange(4)[None, :]
+                self.lds[idx.reshape(-1)] = data.astype("<u4").view(np.uint8)
+            elif op == "ds_read_b32":
+                base, off = a[1].split()
+                assert off.startswith("offset:"), ln
+                addr = self.val(base).astype(np.int64) + int(off.split(":")[1])
+                idx = addr[:, None] + np.arange(4)[None, :]
+                self.vset(a[0], self.lds[idx].copy().view("<u4").reshape(-1))
+            elif op == "buffer_load_dword":
+                assert a[3].endswith("offen"), ln
+                addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
+                self.vset(a[0], self.mem.load32(addr))
+            elif op == "buffer_store_dword":
+                addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
+                self.mem.store32(addr, self.val(a[0]))
             else:
                 raise NotImplementedError(ln)
 
@@ -128,10 +183,18 @@ class Memory:
 
 
 def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
-    """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`."""
+    """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`
+    (LDS base address 0; each role's ring region at role * region bytes)."""
     finish, roles = split_source(src)
+    m = re.search(r"\(uint32_t\)role \* (\d+)u", src)
+    region = int(m.group(1)) if m else 0
+    lds = np.zeros(max(1, region * len(roles)) + 64, np.uint8)
     col = (chunk * 256 + np.arange(64) * 4).astype(np.uint32)
-    ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF, dh=dst_base >> 32,
-               ss=src_sym, ds=dst_sym)
-    for lines in roles:
-        Wave(mem, ops).run(lines, finish)
+    for w, lines in enumerate(roles):
+        lb = w * region
+        ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF,
+                   dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb,
+                   la=(lb + np.arange(64) * 4).astype(np.uint32))
+        wave = Wave(mem, ops)
+        wave.lds = lds
+        wave.run(lines, finish)
