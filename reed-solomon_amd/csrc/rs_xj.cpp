@@ -587,6 +587,17 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
 
 int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nchunks, hipStream_t st) {
     if (n_stripes <= 0 || nchunks <= 0) return 0;
+    static const bool alias = std::getenv("RS_XJ_ALIAS") && std::atoi(std::getenv("RS_XJ_ALIAS"));
+    if (alias) {  // diagnostic (wrong results): every stripe reads and writes stripe 0, inputs cache-resident
+        XJArgs a = a0;
+        a.src_stripe = 0;
+        a.dst_stripe = 0;
+        void* args[] = {&a};
+        const unsigned ny = unsigned(std::min<int64_t>(65535, n_stripes));
+        hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(nchunks), ny, 1, unsigned(64 * k.roles), 1, 1, 0, st, args,
+                                             nullptr);
+        return e == hipSuccess ? 0 : 3;
+    }
     for (int64_t s0 = 0; s0 < n_stripes; s0 += 65535) {  // grid.y limit
         XJArgs a = a0;
         a.src += s0 * a.src_stripe;
