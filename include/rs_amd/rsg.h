@@ -56,6 +56,14 @@ int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stripe_stride, 
 int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t n_stripes,
                uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream);
 
+/* Per-stripe erasure patterns: is_erased is [n_stripes][k + r] in host memory (stripe s lost the
+ * symbols flagged in row s). Stripes are grouped by pattern; each distinct pattern is decoded by one
+ * launch over its stripes (decode plans are cached, 16 most recent). Returns RS_ERR_CANNOT_RESTORE
+ * without writing anything if any stripe has more than r erasures; stripes without erased
+ * information symbols are left untouched. Synchronises `stream` once (stripe-id upload). */
+int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t n_stripes,
+                     uint64_t symbol_size, const bool* is_erased, void* stream);
+
 /* Synthetic inputs: fills the k information symbols of stripes [stripe0, stripe0 + n) with the
  * counter-based generator of tests/_util.py:gen_info (symbol_size % 8 == 0). */
 int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size, uint16_t k,

@@ -189,6 +189,14 @@ struct rsg_codec {
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
     uint64_t* stamps = nullptr;  // device buffer for mode 17 (instrumented timing)
+    int32_t* d_ids = nullptr;    // stripe-id lists of rsg_decode_batch
+    size_t ids_cap = 0;
+    ~rsg_codec() {
+        if (d_ids) {
+            (void)hipSetDevice(device);
+            (void)hipFree(d_ids);
+        }
+    }
     std::string last_kernel = "none";
 };
 
@@ -279,7 +287,8 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
 extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->last_kernel.c_str() : "none"; }
 
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
-                    int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st) {
+                    int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
+                    const int32_t* d_ids = nullptr) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
     const int64_t align = p.m == 8 ? 8 : 4;
     if ((S & 1) || (uintptr_t(src) % align) || (uintptr_t(dst) % align) || (src_stripe % align) ||
@@ -331,6 +340,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.nbytes = int64_t(S);
     a.mode = c->m8_mode;
     a.stamps = c->stamps;
+    a.ids = d_ids;
     const int nt32 = (p.R + 31) / 32;
     if (xj_ok && p.xj) {
         XJArgs x{};
@@ -340,6 +350,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         x.dst_stripe = dst_stripe;
         x.src_sym = int32_t(src_sym);
         x.dst_sym = int32_t(dst_sym);
+        x.ids = d_ids;
         c->last_kernel = p.xj->name;
         // 256-byte column chunks up to the last full 2 KiB boundary; the rest by the generic tail kernel
         int rc = xj_launch(*p.xj, x, int64_t(n_stripes), (a.nbytes / 2048) * (2048 / kXjChunk), st);
@@ -413,6 +424,61 @@ extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, u
     uint8_t* base = static_cast<uint8_t*>(d_rcv);
     return run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
                     int64_t(symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
+                                uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
+    if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
+    const size_t n = size_t(c->k) + c->r;
+    // validate every stripe first (nothing is written when one pattern cannot be restored), then group
+    // the stripes that share a pattern: one plan and one launch (over a stripe-id list) per pattern
+    std::map<std::vector<uint8_t>, std::vector<int32_t>> groups;
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const bool* e = is_erased + s * n;
+        size_t t = 0;
+        bool info = false;
+        for (size_t i = 0; i < n; ++i)
+            if (e[i]) ++t, info |= i < c->k;
+        if (t > c->r) return RS_ERR_CANNOT_RESTORE;
+        if (!info) continue;  // nothing to restore (erased repair slots are never written)
+        if (s > uint64_t(INT32_MAX)) return RS_ERR_INVALID;
+        std::vector<uint8_t> key(e, e + n);
+        groups[key].push_back(int32_t(s));
+    }
+    if (groups.empty() || !symbol_size) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    std::vector<int32_t> ids;
+    std::vector<size_t> first;
+    for (auto& g : groups) {
+        first.push_back(ids.size());
+        ids.insert(ids.end(), g.second.begin(), g.second.end());
+    }
+    if (ids.size() > c->ids_cap) {
+        if (c->d_ids) (void)hipFree(c->d_ids);
+        c->d_ids = nullptr;
+        c->ids_cap = 0;
+        HIP_TRY(hipMalloc(&c->d_ids, ids.size() * 4));
+        c->ids_cap = ids.size();
+    }
+    // the list must stay valid until the launches have read it: upload on the caller's stream
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint8_t* base = static_cast<uint8_t*>(d_rcv);
+    size_t gi = 0;
+    for (auto& g : groups) {
+        std::unique_ptr<bool[]> er(new bool[n]);
+        uint16_t t = 0;
+        for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.first[i] != 0));
+        DevPlan* p = nullptr;
+        int rc = decode_plan(c, er.get(), t, &p);
+        if (rc) return rc;
+        rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
+                      int64_t(symbol_stride), g.second.size(), symbol_size, st, c->d_ids + first[gi]);
+        if (rc) return rc;
+        ++gi;
+    }
+    return 0;
 }
 
 extern "C" int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size,

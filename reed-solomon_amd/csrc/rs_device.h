@@ -124,8 +124,9 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     const uint32_t* lt = lds;
     uint32_t* ring = lds + 2048;
     const int64_t bid = blockIdx.x;
-    const int64_t stripe = bid / a.nchunks;
-    const int64_t chunk0 = (bid - stripe * a.nchunks) * 1024;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
     const int tile = blockIdx.y;
     const int K = a.K;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);

@@ -36,8 +36,9 @@ __global__ void __launch_bounds__(256) k_apply_m8(ApplyArgs a) {
     __syncthreads();
 
     const int64_t bid = blockIdx.x;
-    const int64_t stripe = bid / a.nchunks;
-    const int64_t col = (bid - stripe * a.nchunks) * 2048 + int64_t(threadIdx.x) * 8;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t col = (bid - local * a.nchunks) * 2048 + int64_t(threadIdx.x) * 8;
     const int64_t avail = a.nbytes - col;
     const int tile = blockIdx.y;
     const uint8_t* src = a.src + stripe * a.src_stripe + col;
@@ -327,8 +328,9 @@ __global__ void __launch_bounds__(256) k_apply_m8_lds(ApplyArgs a, const int32_t
     __syncthreads();
 
     const int64_t bid = blockIdx.x;
-    const int64_t stripe = bid / a.nchunks;
-    const int64_t chunk0 = (bid - stripe * a.nchunks) * 2048;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t chunk0 = (bid - local * a.nchunks) * 2048;
     const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
     const int64_t avail = a.nbytes - col;
     const int tile = blockIdx.y;
@@ -394,7 +396,8 @@ __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t
     __syncthreads();
 
     const int64_t bid = blockIdx.x;
-    const int64_t stripe = bid / a.nchunks;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
     const int64_t chunk0 = (a.chunk_base + bid - stripe * a.nchunks) * 2048;
     const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
     const int64_t avail = a.nbytes - col;
@@ -426,8 +429,9 @@ __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t
 template <int RT>
 __global__ void __launch_bounds__(256) k_apply_m16(ApplyArgs a) {
     const int64_t bid = blockIdx.x;
-    const int64_t stripe = bid / a.nchunks;
-    const int64_t col = (bid - stripe * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t col = (bid - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
     const int64_t avail = a.nbytes - col;
     if (avail <= 0) return;
     const int tile = blockIdx.y;
@@ -531,6 +535,7 @@ V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
     v.K = a.K;
     v.R = a.R;
     v.nchunks = nchunks_1k;
+    v.ids = a.ids;
     return v;
 }
 

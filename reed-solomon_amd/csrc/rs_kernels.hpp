@@ -28,6 +28,7 @@ struct ApplyArgs {
     int32_t mode;            // m<=8 inner loop: 0 = register nibble tables (compiler indexing),
                              //   1 = SGPR-masked multiples, 2 = hand-scheduled gpr-index block (RT=32)
     uint64_t* stamps;        // mode 17 (instrumented): [blocks * 4 waves][4] phase cycle counters
+    const int32_t* ids;      // optional [n_stripes] stripe indices (per-stripe erasure patterns); null = 0..n-1
 };
 
 int apply_tile_rows(int m, int R);

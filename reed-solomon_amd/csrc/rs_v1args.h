@@ -18,5 +18,9 @@ struct V1Args {
     const int32_t* boff;     // JIT: [ntiles][K] byte offset of each input's lookup block
     int32_t K, R;
     int64_t nchunks;         // 1 KiB column chunks per symbol processed by this launch
+    const int32_t* ids;      // optional [n_stripes] stripe indices; null = 0..n-1
 };
+
+// Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.
+#define RS_STRIPE(ids, s) ((ids) ? int64_t((ids)[(s)]) : int64_t(s))
 

@@ -524,12 +524,12 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
     o << "typedef unsigned int uint32_t; typedef int int32_t; typedef unsigned char uint8_t;\n"
          "typedef long long int64_t; typedef unsigned long long uint64_t;\n"
          "struct XJArgs { const uint8_t* src; int64_t src_stripe; uint8_t* dst; int64_t dst_stripe;"
-         " int32_t src_sym, dst_sym; };\n"
+         " int32_t src_sym, dst_sym; const int32_t* ids; };\n"
       << "// K=" << K << " R=" << R << " roles=" << roles << " " << C.tag() << "\n"
       << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles << ") rs_xj(XJArgs a) {\n"
       << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds[" << std::max(1, roles * C.lds * 512) << "];\n"
       << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
-      << "  const uint64_t stripe = blockIdx.y;\n"
+      << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
          "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
          "  const uint64_t db = (uint64_t)a.dst + stripe * (uint64_t)a.dst_stripe;\n"
          "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
@@ -600,8 +600,12 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
     }
     for (int64_t s0 = 0; s0 < n_stripes; s0 += 65535) {  // grid.y limit
         XJArgs a = a0;
-        a.src += s0 * a.src_stripe;
-        a.dst += s0 * a.dst_stripe;
+        if (a.ids) {
+            a.ids += s0;
+        } else {
+            a.src += s0 * a.src_stripe;
+            a.dst += s0 * a.dst_stripe;
+        }
         const unsigned ny = unsigned(std::min<int64_t>(65535, n_stripes - s0));
         void* args[] = {&a};
         hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(nchunks), ny, 1, unsigned(64 * k.roles), 1, 1, 0, st, args,

@@ -31,6 +31,7 @@ struct XJArgs {
     uint8_t* dst;
     int64_t dst_stripe;
     int32_t src_sym, dst_sym;  // symbol strides (slot * stride < 2^31)
+    const int32_t* ids;        // optional [n_stripes] stripe indices; null = 0..n-1
 };
 
 struct XjKernel {

@@ -77,6 +77,7 @@ _sig("rsg_set_option", ctypes.c_int, P, ctypes.c_char_p, i64)
 _sig("rsg_last_kernel", ctypes.c_char_p, P)
 _sig("rsg_encode", ctypes.c_int, P, P, u64, u64, P, u64, u64, u64, u64, P)
 _sig("rsg_decode", ctypes.c_int, P, P, u64, u64, u64, u64, P, u16, P)
+_sig("rsg_decode_batch", ctypes.c_int, P, P, u64, u64, u64, u64, P, P)
 _sig("rsg_fill_info", ctypes.c_int, P, u64, u64, u64, u16, u64, u64, u64, P)
 _sig("rsg_fingerprint", ctypes.c_int, P, u64, u64, u64, u32, u32, u64, P, P)
 _sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
@@ -266,6 +267,18 @@ class Codec:
                              _stream_ptr(stream))
         if check and rc not in (0,):
             raise RSError(rc, "rsg_decode")
+        return rc
+
+    def decode_batch(self, stripes, patterns, stream=None, check=True):
+        """Per-stripe erasure patterns: patterns [n, k + r] bool (host); restores in place."""
+        n, nsym, S = stripes.shape
+        assert nsym == self.k + self.r and stripes.is_contiguous()
+        er = np.ascontiguousarray(patterns, dtype=np.bool_)
+        assert er.shape == (n, nsym)
+        rc = _lib.rsg_decode_batch(self._h, P(stripes.data_ptr()), nsym * S, S, n, S, _np_ptr(er),
+                                   _stream_ptr(stream))
+        if check and rc:
+            raise RSError(rc, "rsg_decode_batch")
         return rc
 
     def encode_raw(self, d_info, info_stripe, info_sym, d_rep, rep_stripe, rep_sym, n, S, stream):
