@@ -264,7 +264,7 @@ def main():
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
     traffic = measured_traffic(dom_name, f"k{k}_r{r}_S{S}_n{n}_t{t}")
     line = {
-        "metric": "encode+decode GB/s (device-resident) at k=128 r=32 64KiB symbols; % HBM roofline",
+        "metric": "encode+decode GB/s (device-resident) at k/r/symbol_len; % HBM roofline",  # BASELINE.json
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,

@@ -140,7 +140,7 @@ struct XjConfig {
     int horner = 0;    // finish: 1 = Horner in alpha (packed-16 ops), 0 = in alpha^-1
     int ablate = 0;    // timing ablations (wrong results): 1 no finish, 2 no rows, 4 no tables
     int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
-    XjConfig() {
+    explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
         };
@@ -154,6 +154,7 @@ struct XjConfig {
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
         if (lds) ring = 2;  // VGPR double buffer behind the LDS ring
         opr = std::max(1, std::min(16, opr));
+        if (R > 0) opr = std::min(opr, R);  // small codes: smaller register layout, more waves per SIMD
         ring = std::max(2, std::min(6, ring));
         horner = horner ? 1 : 0;
     }
@@ -515,7 +516,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots) {
-    const XjConfig C;
+    const XjConfig C(R);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
     for (size_t e = 0; e < M.size(); ++e) cb[e] = B.bits(M[e]);
@@ -555,6 +556,10 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
 }
 
 int xj_outputs_per_role() { return XjConfig().opr; }
+int xj_roles(int R) {
+    const int opr = XjConfig(R).opr;
+    return (R + opr - 1) / opr;
+}
 int xj_horner() { return XjConfig().horner; }
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
@@ -576,7 +581,7 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     auto k = std::make_unique<XjKernel>();
     k->mod = mod;
     (void)hipGetDevice(&k->device);
-    k->roles = (R + xj_outputs_per_role() - 1) / xj_outputs_per_role();
+    k->roles = xj_roles(R);
     if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), "rs_xj") != hipSuccess) return 3;
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));

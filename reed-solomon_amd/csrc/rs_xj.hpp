@@ -64,10 +64,11 @@ struct XjBasis {
     uint16_t inv_row_[16];  // row j of the inverse of [z^0 .. z^15] over GF(2)
 };
 const XjBasis& xj_basis(int horner);
-int xj_horner();  // generation setting (RS_XJ_HORNER, default 1)
+int xj_horner();  // generation setting (RS_XJ_HORNER, default 0)
 
 bool xj_supported(int m, int K, int R);
-int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 8)
+int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 16)
+int xj_roles(int R);         // waves per block for R outputs
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots);
