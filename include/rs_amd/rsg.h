@@ -38,8 +38,9 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * gpr-index lookups, the default; 2 = two dwords per lane; 0 = register tables with compiler
  * indexing; 1 = masked multiples; 10-19 timing ablations), "jit" (matrix-specialised kernels
  * compiled with hiprtc and cached on disk: 0 = off, 1 = every eligible matrix, 2 = the encode matrix
- * and decode matrices from their second use, the default). Returns RS_ERR_INVALID for unknown names
- * or values. */
+ * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
+ * before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
+ * 0 = nibble-table kernels). Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);

@@ -18,7 +18,9 @@
 #include "gf16.hpp"
 #include "rs_jit.hpp"
 #include "rs_kernels.hpp"
+#include "rs_pool.hpp"
 #include "rs_xj.hpp"
+#include <thread>
 
 extern "C" {
 #include <memory/seq.h>
@@ -187,6 +189,7 @@ struct rsg_codec {
     std::vector<std::vector<uint8_t>> dec_lru;
     int m8_mode = 18;
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
+    int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
     uint64_t* stamps = nullptr;  // device buffer for mode 17 (instrumented timing)
     int32_t* d_ids = nullptr;    // stripe-id lists of rsg_decode_batch
@@ -276,6 +279,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->xj = int(value);
         return 0;
     }
+    if (!std::strcmp(name, "dec_jit_uses")) {
+        if (value < 1 || value > (int64_t(1) << 30)) return RS_ERR_INVALID;
+        c->dec_jit_uses = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "jit")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->jit = int(value);
@@ -296,7 +304,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
     ++p.uses;
-    const bool policy = p.m == 8 && p.d_idx && (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= 2)));
+    const bool policy = p.m == 8 && p.d_idx && (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= c->dec_jit_uses)));
     // bit-plane XOR kernel: slot * stride must fit the kernel's 32-bit scalar offsets
     int64_t max_in = 0, max_out = 0;
     for (int32_t v : p.in_slots) max_in = std::max<int64_t>(max_in, v);
@@ -590,6 +598,8 @@ extern "C" const char* rsg_version(void) { return RSG_VERSION; }
 // ============================================================================ drop-in rs_*
 namespace {
 
+constexpr int kMaxChunks = 4;
+
 struct Impl {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -598,9 +608,13 @@ struct Impl {
     uint8_t* h_buf = nullptr;
     uint8_t* d_buf = nullptr;
     size_t cap = 0;
+    std::unique_ptr<HostPool> pool;  // gather / scatter workers
+    hipEvent_t ev[kMaxChunks] = {};
     ~Impl() {
         (void)hipSetDevice(device);
         codecs.clear();
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
         if (h_buf) (void)hipHostFree(h_buf);
         if (d_buf) (void)hipFree(d_buf);
         if (stream) (void)hipStreamDestroy(stream);
@@ -624,6 +638,8 @@ struct Impl {
             rsg_codec* c = nullptr;
             int rc = rsg_codec_create(device, k, r, &c);
             if (rc) return rc;
+            // one call launches up to kMaxChunks decodes: specialise a pattern from its third call on
+            c->dec_jit_uses = 2 * kMaxChunks + 1;
             it = codecs.emplace(key, std::unique_ptr<rsg_codec>(c)).first;
         }
         *out = it->second.get();
@@ -631,6 +647,14 @@ struct Impl {
     }
 };
 
+// Column chunks of one per-call stripe: large symbols are split into up to kMaxChunks column ranges
+// (multiples of the 2 KiB kernel block), so the host gather of chunk c + 1 and the scatter of chunk
+// c - 1 overlap the copies and kernel of chunk c.
+size_t chunk_width(size_t S) {
+    if (S < 4 * 8192) return S;
+    const size_t w = (S + kMaxChunks - 1) / kMaxChunks;
+    return (w + 2047) / 2048 * 2048;
+}
 inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
 
 }  // namespace
@@ -656,7 +680,12 @@ extern "C" RS_t* rs_create(void) {
         return nullptr;
     }
     (void)hipGetDevice(&impl->device);
-    if (hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking) != hipSuccess) {
+    int workers = int(std::min(8u, std::max(1u, std::thread::hardware_concurrency()))) - 1;
+    if (const char* e = std::getenv("RS_AMD_HOST_THREADS")) workers = std::max(0, std::atoi(e) - 1);
+    impl->pool = std::make_unique<HostPool>(workers);
+    bool ev_ok = true;
+    for (hipEvent_t& e : impl->ev) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok || hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking) != hipSuccess) {
         delete impl;
         gf_destroy(rs->gf);
         cc_destroy(rs->cc);
@@ -687,16 +716,30 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    const size_t P = pad16(S), n = size_t(k) + r;
+    const size_t P = pad16(S), n = size_t(k) + r, W = chunk_width(S), nch = (S + W - 1) / W;
     if (im.reserve(n * P)) return 1;
-    for (size_t i = 0; i < k; ++i) std::memcpy(im.h_buf + i * P, inf->symbols[i]->data, S);
-    HIP_TRY(hipMemcpyAsync(im.d_buf, im.h_buf, size_t(k) * P, hipMemcpyHostToDevice, im.stream));
-    rc = rsg_encode(c, im.d_buf, n * P, P, im.d_buf + size_t(k) * P, n * P, P, 1, S, im.stream);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(im.h_buf + size_t(k) * P, im.d_buf + size_t(k) * P, size_t(r) * P, hipMemcpyDeviceToHost,
-                           im.stream));
-    HIP_TRY(hipStreamSynchronize(im.stream));
-    for (size_t p = 0; p < r; ++p) std::memcpy(rep->symbols[p]->data, im.h_buf + (k + p) * P, S);
+    uint8_t *h = im.h_buf, *d = im.d_buf;
+    // chunk c: gather k columns -> H2D (2D) -> encode -> D2H (2D); scatter of c - 1 overlaps it
+    auto scatter = [&](size_t c) {
+        const size_t off = c * W, w = std::min(W, S - off);
+        im.pool->run(r, [&](int p) { std::memcpy(rep->symbols[p]->data + off, h + (k + size_t(p)) * P + off, w); });
+    };
+    for (size_t ch = 0; ch < nch; ++ch) {
+        const size_t off = ch * W, w = std::min(W, S - off);
+        im.pool->run(k, [&](int i) { std::memcpy(h + size_t(i) * P + off, inf->symbols[i]->data + off, w); });
+        HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, k, hipMemcpyHostToDevice, im.stream));
+        rc = rsg_encode(c, d + off, n * P, P, d + size_t(k) * P + off, n * P, P, 1, w, im.stream);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy2DAsync(h + size_t(k) * P + off, P, d + size_t(k) * P + off, P, w, r, hipMemcpyDeviceToHost,
+                                 im.stream));
+        HIP_TRY(hipEventRecord(im.ev[ch], im.stream));
+        if (ch) {
+            HIP_TRY(hipEventSynchronize(im.ev[ch - 1]));
+            scatter(ch - 1);
+        }
+    }
+    HIP_TRY(hipEventSynchronize(im.ev[nch - 1]));
+    scatter(nch - 1);
     return 0;
 }
 
@@ -708,27 +751,52 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     const size_t S = rcv->symbol_size, n = size_t(k) + r;
     if (rcv->length != n || (S & 1) || n > kN) return RS_ERR_INVALID;
     size_t cnt = 0;
-    bool info_lost = false;
-    for (size_t i = 0; i < n; ++i)
-        if (is_erased[i]) ++cnt, info_lost |= i < k;
+    std::vector<int> keep, lost;  // surviving slots (gathered), erased information slots (scattered)
+    for (size_t i = 0; i < n; ++i) {
+        if (is_erased[i]) {
+            ++cnt;
+            if (i < k) lost.push_back(int(i));
+        } else {
+            keep.push_back(int(i));
+        }
+    }
     if (cnt != t) return RS_ERR_INVALID;
-    if (!info_lost || S == 0) return 0;
+    if (lost.empty() || S == 0) return 0;
     std::lock_guard<std::mutex> lk(im.mu);
     HIP_TRY(hipSetDevice(im.device));
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    const size_t P = pad16(S);
+    const size_t P = pad16(S), W = chunk_width(S), nch = (S + W - 1) / W;
     if (im.reserve(n * P)) return 1;
-    for (size_t i = 0; i < n; ++i)
-        if (!is_erased[i]) std::memcpy(im.h_buf + i * P, rcv->symbols[i]->data, S);
-    HIP_TRY(hipMemcpyAsync(im.d_buf, im.h_buf, n * P, hipMemcpyHostToDevice, im.stream));
-    rc = rsg_decode(c, im.d_buf, n * P, P, 1, S, is_erased, t, im.stream);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(im.h_buf, im.d_buf, size_t(k) * P, hipMemcpyDeviceToHost, im.stream));
-    HIP_TRY(hipStreamSynchronize(im.stream));
-    for (size_t i = 0; i < k; ++i)
-        if (is_erased[i]) std::memcpy(rcv->symbols[i]->data, im.h_buf + i * P, S);
+    uint8_t *h = im.h_buf, *d = im.d_buf;
+    // erased slots are neither gathered nor read by the decoder; only rows lost[0] .. lost.back() come back
+    const size_t lo = size_t(lost.front()), rows = size_t(lost.back()) - lo + 1;
+    auto scatter = [&](size_t ch) {
+        const size_t off = ch * W, w = std::min(W, S - off);
+        im.pool->run(int(lost.size()), [&](int j) {
+            const size_t i = size_t(lost[size_t(j)]);
+            std::memcpy(rcv->symbols[i]->data + off, h + i * P + off, w);
+        });
+    };
+    for (size_t ch = 0; ch < nch; ++ch) {
+        const size_t off = ch * W, w = std::min(W, S - off);
+        im.pool->run(int(keep.size()), [&](int j) {
+            const size_t i = size_t(keep[size_t(j)]);
+            std::memcpy(h + i * P + off, rcv->symbols[i]->data + off, w);
+        });
+        HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, n, hipMemcpyHostToDevice, im.stream));
+        rc = rsg_decode(c, d + off, n * P, P, 1, w, is_erased, t, im.stream);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy2DAsync(h + lo * P + off, P, d + lo * P + off, P, w, rows, hipMemcpyDeviceToHost, im.stream));
+        HIP_TRY(hipEventRecord(im.ev[ch], im.stream));
+        if (ch) {
+            HIP_TRY(hipEventSynchronize(im.ev[ch - 1]));
+            scatter(ch - 1);
+        }
+    }
+    HIP_TRY(hipEventSynchronize(im.ev[nch - 1]));
+    scatter(nch - 1);
     return 0;
 }
 
