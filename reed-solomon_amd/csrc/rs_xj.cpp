@@ -139,6 +139,7 @@ struct XjConfig {
     int spread = 0;    // 1: next pairs' loads interleaved into the row stream; 0: issued as a burst
     int horner = 0;    // finish: 1 = Horner in alpha (packed-16 ops), 0 = in alpha^-1
     int ablate = 0;    // timing ablations (wrong results): 1 no finish, 2 no rows, 4 no tables
+    int nt = 0;        // cache policy bits on the global loads / stores: 1 = nt loads, 2 = nt stores, 3 = both
     int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
@@ -151,6 +152,7 @@ struct XjConfig {
         env("RS_XJ_HORNER", horner);
         env("RS_XJ_ABLATE", ablate);
         env("RS_XJ_LDS", lds);
+        env("RS_XJ_NT", nt);
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
         if (lds) ring = 2;  // VGPR double buffer behind the LDS ring
         opr = std::max(1, std::min(16, opr));
@@ -169,8 +171,8 @@ struct XjConfig {
     int cst() const { return ring_base() + opr + 16; }
     std::string tag() const {
         char b[80];
-        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d", opr, ring, buffer, spread,
-                      horner, ablate, lds);
+        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d", opr, ring, buffer,
+                      spread, horner, ablate, lds, nt);
         return b;
     }
 };
@@ -324,7 +326,8 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 ops.push_back(E.fmt("s_mul_i32 s62, s34, %d", slot));
                 ops.push_back(E.fmt("s_add_u32 s%d, s32, s62", 40 + 2 * j));
                 ops.push_back(E.fmt("s_addc_u32 s%d, s33, 0", 41 + 2 * j));
-                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]", dst, COL, 40 + 2 * j, 41 + 2 * j));
+                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
+                                    (C.nt & 1) ? " nt" : ""));
             }
         }
         return ops;
@@ -503,7 +506,8 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
             if (C.buffer)
                 E.f("buffer_store_dword v%d, %s, s[52:55], s%d offen", C.fin(q0 + j), COL, 40 + j);
             else
-                E.f("global_store_dword %s, v%d, s[%d:%d]", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j);
+                E.f("global_store_dword %s, v%d, s[%d:%d]%s", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j,
+                    (C.nt & 2) ? " nt" : "");
         }
         if (q0 + 8 < nq) E.e("s_waitcnt vmcnt(0)");  // address registers are reused by the next batch
     }

@@ -138,10 +138,10 @@ class Wave:
                 hi = ((x >> 16).astype(np.uint16).view(np.int16) >> sh).view(np.uint16).astype(np.uint32)
                 self.vset(a[0], lo | (hi << np.uint32(16)))
             elif op == "global_load_dword":
-                addr = self.pair(a[2]) + self.val(a[1]).astype(np.uint64)
+                addr = self.pair(a[2].split()[0]) + self.val(a[1]).astype(np.uint64)
                 self.vset(a[0], self.mem.load32(addr))
             elif op == "global_store_dword":
-                addr = self.pair(a[2]) + self.val(a[0]).astype(np.uint64)
+                addr = self.pair(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
                 self.mem.store32(addr, self.val(a[1]))
             elif op == "buffer_load_dword" and ln.endswith(" lds"):
                 # LDS DMA: a[0] = voffset, a[1] = V#, a[2] = "soffset offen lds"
