@@ -20,6 +20,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "rs_device.h"
 #include "rs_kernels.hpp"
 
@@ -618,7 +621,7 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
 
 int apply_tile_rows(int m, int R) {
     if (m <= 8) return R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
-    return R <= 16 ? 16 : R <= 32 ? 32 : 64;
+    return R <= 16 ? 16 : R <= 32 ? 32 : 64;  // 64 measured best for C5 (RT 32: -3 %, RT 16: -22 %)
 }
 
 int64_t apply_chunk_bytes(int m) { return m <= 8 ? 2048 : 1024; }
