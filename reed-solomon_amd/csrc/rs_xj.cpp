@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <sstream>
 
 #include "gf16.hpp"
@@ -141,6 +143,8 @@ struct XjConfig {
     int ablate = 0;    // timing ablations (wrong results): 1 no finish, 2 no rows, 4 no tables
     int nt = 0;        // cache policy bits on the global loads / stores: 1 = nt loads, 2 = nt stores, 3 = both
     int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
+    int lfin = 0;      // finish: 0 = VALU Horner over z (above); 1 = Horner in gamma through a 128 KiB LDS
+                       // table T[w] = gamma * w (persistent kernel, one workgroup per CU)
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
@@ -153,6 +157,9 @@ struct XjConfig {
         env("RS_XJ_ABLATE", ablate);
         env("RS_XJ_LDS", lds);
         env("RS_XJ_NT", nt);
+        env("RS_XJ_FIN", lfin);
+        lfin = lfin ? 1 : 0;
+        if (lfin) lds = 0;  // the table takes the LDS
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
         if (lds) ring = 2;  // VGPR double buffer behind the LDS ring
         opr = std::max(1, std::min(16, opr));
@@ -170,9 +177,9 @@ struct XjConfig {
     int tmp(int q, int k) const { return ring_base() + opr + 2 * (q % 8) + k; }
     int cst() const { return ring_base() + opr + 16; }
     std::string tag() const {
-        char b[80];
-        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d", opr, ring, buffer,
-                      spread, horner, ablate, lds, nt);
+        char b[96];
+        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d", opr, ring,
+                      buffer, spread, horner, ablate, lds, nt, lfin);
         return b;
     }
 };
@@ -208,7 +215,10 @@ std::string as_string_literals(const std::vector<std::string>& L) {
 // beta_t has z-coordinate j; Horner from the top coordinate down, up to 8 chains interleaved.
 //   z = alpha:    H <- (H + H per 16-bit lane) ^ (sign mask per lane & 0x2D), then ^ v_j
 //   z = alpha^-1: H <- ((H & 0xfffeffff) >> 1) ^ ((H & 0x10001) * 0x8016) ^ v_j
+std::vector<std::string> finish_block_lds(const XjConfig& C);
+
 std::vector<std::string> finish_block(const XjConfig& C) {
+    if (C.lfin) return finish_block_lds(C);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<std::string> L;
     L.push_back("s_branch L_xj_fin_end");
@@ -278,6 +288,71 @@ std::vector<std::string> finish_block(const XjConfig& C) {
         const size_t n = chains[0].size();
         for (size_t i = 0; i < n; ++i)
             for (int c = 0; c < nc; ++c) L.push_back(chains[size_t(c)][i]);
+    }
+    L.push_back("s_setpc_b64 s[58:59]");
+    L.push_back("L_xj_fin_end:");
+    return L;
+}
+
+// LDS finish (fin = 1): bit-planes over the gamma power basis (beta_t = gamma^t), so
+//   out = u_0 + gamma (u_1 + gamma (u_2 + ... + gamma u_7))
+// and gamma * H on both 16-bit lanes of H is two LDS reads from T[w] = gamma * w at LDS address 0, each
+// into its own address register: ds_read_u16 (zero-extended low lane) and ds_read_u16_d16_hi (high lane;
+// on gfx950, an SRAM-ECC target, d16 loads zero the unused half, so two d16 loads into one register
+// would clobber each other). 4 address ops + 2 LDS reads + 1 XOR3 per step, 7 steps per output. Chains run in two
+// groups of 4 so that one group's reads (8 in flight) overlap the other group's address arithmetic.
+std::vector<std::string> finish_block_lds(const XjConfig& C) {
+    std::vector<std::string> L;
+    char buf[160];
+    auto add = [&](const char* fmt, auto... a) {
+        std::snprintf(buf, sizeof buf, fmt, a...);
+        L.emplace_back(buf);
+    };
+    L.push_back("s_branch L_xj_fin_end");
+    L.push_back("L_xj_fin:");
+    for (int q0 = 0; q0 < C.opr; q0 += 8) {
+        const int nc = std::min(8, C.opr - q0);
+        std::vector<int> grp[2];
+        for (int c = 0; c < nc; ++c) grp[c < 4 ? 0 : 1].push_back(q0 + c);
+        auto addr = [&](int g, int t) {  // addresses of gamma * (current H), H = u_7 before the first step
+            for (int q : grp[g]) {
+                const int cur = t == 6 ? C.acc(q, 7) : C.fin(q);
+                add("v_add_u32 v%d, v%d, v%d", C.tmp(q, 0), cur, cur);
+                add("v_lshrrev_b32 v%d, 15, v%d", C.tmp(q, 1), cur);
+            }
+            for (int q : grp[g]) {
+                add("v_and_b32 v%d, 0x1fffe, v%d", C.tmp(q, 0), C.tmp(q, 0));
+                add("v_and_b32 v%d, 0x1fffe, v%d", C.tmp(q, 1), C.tmp(q, 1));
+            }
+        };
+        auto reads = [&](int g) {
+            for (int q : grp[g]) {
+                add("ds_read_u16 v%d, v%d", C.tmp(q, 0), C.tmp(q, 0));
+                add("ds_read_u16_d16_hi v%d, v%d", C.tmp(q, 1), C.tmp(q, 1));
+            }
+        };
+        auto xors = [&](int g, int t) {
+            for (int q : grp[g])
+                add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", C.fin(q), C.tmp(q, 0), C.tmp(q, 1), C.acc(q, t));
+        };
+        const bool two = !grp[1].empty();
+        addr(0, 6);
+        reads(0);
+        if (two) addr(1, 6);
+        for (int t = 6; t >= 0; --t) {
+            L.push_back("s_waitcnt lgkmcnt(0)");
+            xors(0, t);
+            if (two) reads(1);
+            if (t > 0) addr(0, t - 1);
+            if (two) {
+                L.push_back("s_waitcnt lgkmcnt(0)");
+                xors(1, t);
+            }
+            if (t > 0) {
+                reads(0);
+                if (two) addr(1, t - 1);
+            }
+        }
     }
     L.push_back("s_setpc_b64 s[58:59]");
     L.push_back("L_xj_fin_end:");
@@ -523,26 +598,48 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
     const XjConfig C(R);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
-    for (size_t e = 0; e < M.size(); ++e) cb[e] = B.bits(M[e]);
+    for (size_t e = 0; e < M.size(); ++e) cb[e] = C.lfin ? gamma8().coord(M[e]) : B.bits(M[e]);
     const int roles = (R + C.opr - 1) / C.opr;
+    const int pairs = C.lfin ? xj_pairs(R) : 1;
     std::ostringstream o;
     o << "typedef unsigned int uint32_t; typedef int int32_t; typedef unsigned char uint8_t;\n"
-         "typedef long long int64_t; typedef unsigned long long uint64_t;\n"
+         "typedef unsigned short uint16_t; typedef long long int64_t; typedef unsigned long long uint64_t;\n"
+         "typedef unsigned int xj_u4 __attribute__((ext_vector_type(4)));\n"
          "struct XJArgs { const uint8_t* src; int64_t src_stripe; uint8_t* dst; int64_t dst_stripe;"
-         " int32_t src_sym, dst_sym; const int32_t* ids; };\n"
-      << "// K=" << K << " R=" << R << " roles=" << roles << " " << C.tag() << "\n"
-      << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles << ") rs_xj(XJArgs a) {\n"
-      << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds[" << std::max(1, roles * C.lds * 512) << "];\n"
-      << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
-      << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
-         "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
+         " int32_t src_sym, dst_sym; const int32_t* ids; const uint16_t* tab; uint32_t nchunks, ncols; };\n"
+      << "// K=" << K << " R=" << R << " roles=" << roles << " pairs=" << pairs << " " << C.tag() << "\n"
+      << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles * pairs << ") rs_xj(XJArgs a) {\n";
+    if (C.lfin) {
+        // the gamma table is the kernel's only LDS variable, at address 0 (checked: the finish block
+        // addresses it absolutely); every workgroup copies it once, then loops over columns
+        o << "  __shared__ __attribute__((aligned(16))) uint16_t xj_tab[65536];\n"
+          << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
+          << "  if ((uint32_t)(unsigned long)xj_tab != 0u) return;\n"
+             "  for (uint32_t i = threadIdx.x; i < 8192u; i += blockDim.x)\n"
+             "    ((xj_u4*)xj_tab)[i] = ((const xj_u4*)a.tab)[i];\n"
+             "  __syncthreads();\n"
+             "  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
+          << "  const int role = wave % " << roles << ", pair = wave / " << roles << ";\n"
+          << "  const uint32_t la = 0u, lb = 0u;\n"
+             "  for (uint32_t c = blockIdx.x * " << pairs << "u + (uint32_t)pair; c < a.ncols; c += gridDim.x * "
+          << pairs << "u) {\n"
+             "  const uint32_t local = c / a.nchunks, chunk = c - local * a.nchunks;\n"
+             "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[local] : (uint64_t)local;\n"
+             "  const uint32_t col = chunk * 256u + (threadIdx.x & 63u) * 4u;\n";
+    } else {
+        o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds[" << std::max(1, roles * C.lds * 512) << "];\n"
+          << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
+          << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
+             "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
+             "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
+             "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
+          << C.lds * 2048 << "u;\n"
+             "  const uint32_t la = lb + (threadIdx.x & 63u) * 4u;\n"
+             "  {\n";
+    }
+    o << "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
          "  const uint64_t db = (uint64_t)a.dst + stripe * (uint64_t)a.dst_stripe;\n"
-         "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
          "  const uint32_t sl = (uint32_t)sb, sh = (uint32_t)(sb >> 32), dl = (uint32_t)db, dh = (uint32_t)(db >> 32);\n"
-         "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
-         "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
-      << C.lds * 2048 << "u;\n"
-         "  const uint32_t la = lb + (threadIdx.x & 63u) * 4u;\n"
          "  switch (role) {\n";
     std::string clob;
     for (int v = 1; v <= C.max_vgpr(); ++v) clob += "\"v" + std::to_string(v) + "\", ";
@@ -555,7 +652,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
              " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)\n  : "
           << clob << ");\n    break;\n";
     }
-    o << "  }\n}\n";
+    o << "  }\n  }\n}\n";
     return o.str();
 }
 
@@ -565,6 +662,17 @@ int xj_roles(int R) {
     return (R + opr - 1) / opr;
 }
 int xj_horner() { return XjConfig().horner; }
+int xj_fin() { return XjConfig().lfin; }
+int xj_pairs(int R) {
+    if (!XjConfig(R).lfin) return 1;
+    // column pairs per persistent workgroup: every wave slot of the CU (the 128 KiB table allows one
+    // workgroup per CU); VGPRs per wave = the fixed map + the compiler's column / loop registers
+    const XjConfig C(R);
+    const int vgprs = (C.max_vgpr() + 2 + 7) / 8 * 8;
+    const int waves_per_simd = std::max(1, std::min(8, 512 / vgprs));
+    const int roles = xj_roles(R);
+    return std::max(1, std::min(16 / roles, 4 * waves_per_simd / roles));
+}
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                   const std::vector<int32_t>& out_slots) {
@@ -586,6 +694,7 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     k->mod = mod;
     (void)hipGetDevice(&k->device);
     k->roles = xj_roles(R);
+    k->pairs = XjConfig(R).lfin ? xj_pairs(R) : 0;
     if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), "rs_xj") != hipSuccess) return 3;
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));
@@ -594,9 +703,67 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     return 0;
 }
 
+namespace {
+// Per-device T[w] = gamma * w (128 KiB) for the LDS finish, and the CU count for persistent grids.
+struct XjDevState {
+    uint16_t* tab = nullptr;
+    int cus = 0;
+};
+XjDevState* xj_dev_state(int device) {
+    static std::mutex mu;
+    static std::map<int, XjDevState> st;
+    std::lock_guard<std::mutex> lk(mu);
+    XjDevState& d = st[device];
+    if (!d.tab) {
+        const Field& F = field();
+        std::vector<uint16_t> t(65536, 0);
+        for (uint32_t w = 1; w < 65536; ++w) t[w] = F.exp[(F.log[w] + 257u) % kN];
+        void* p = nullptr;
+        if (hipMalloc(&p, t.size() * 2) != hipSuccess) return nullptr;
+        if (hipMemcpy(p, t.data(), t.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        d.tab = static_cast<uint16_t*>(p);
+        if (hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || d.cus < 1)
+            d.cus = 256;
+    }
+    return &d;
+}
+}  // namespace
+
 int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nchunks, hipStream_t st) {
     if (n_stripes <= 0 || nchunks <= 0) return 0;
     static const bool alias = std::getenv("RS_XJ_ALIAS") && std::atoi(std::getenv("RS_XJ_ALIAS"));
+    if (k.pairs > 0) {  // persistent form: one workgroup per CU loops over all (stripe, chunk) columns
+        XjDevState* d = xj_dev_state(k.device);
+        if (!d) return 3;
+        const unsigned block = unsigned(64 * k.roles * k.pairs);
+        for (int64_t s0 = 0; s0 < n_stripes;) {
+            const int64_t ns = std::min<int64_t>(n_stripes - s0, int64_t(0x7fffffff) / nchunks);
+            XJArgs a = a0;
+            if (a.ids) {
+                a.ids += s0;
+            } else {
+                a.src += s0 * a.src_stripe;
+                a.dst += s0 * a.dst_stripe;
+            }
+            if (alias) a.src_stripe = a.dst_stripe = 0;
+            a.tab = d->tab;
+            a.nchunks = uint32_t(nchunks);
+            a.ncols = uint32_t(ns * nchunks);
+            const int64_t want = (int64_t(a.ncols) + k.pairs - 1) / k.pairs;
+            const unsigned grid = unsigned(std::max<int64_t>(1, std::min<int64_t>(d->cus, want)));
+            void* args[] = {&a};
+            hipError_t e = hipModuleLaunchKernel(k.fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr);
+            if (e != hipSuccess) {
+                std::fprintf(stderr, "librs_amd: xj launch: %s\n", hipGetErrorString(e));
+                return 3;
+            }
+            s0 += ns;
+        }
+        return 0;
+    }
     if (alias) {  // diagnostic (wrong results): every stripe reads and writes stripe 0, inputs cache-resident
         XJArgs a = a0;
         a.src_stripe = 0;

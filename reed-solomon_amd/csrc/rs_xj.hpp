@@ -32,13 +32,16 @@ struct XJArgs {
     int64_t dst_stripe;
     int32_t src_sym, dst_sym;  // symbol strides (slot * stride < 2^31)
     const int32_t* ids;        // optional [n_stripes] stripe indices; null = 0..n-1
+    const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch)
+    uint32_t nchunks, ncols;   // persistent form: chunks per stripe, chunks in the launch (set by xj_launch)
 };
 
 struct XjKernel {
     std::shared_ptr<JitModule> mod;
     hipFunction_t fn = nullptr;
     int device = 0;
-    int roles = 0;  // waves per block (8 outputs each)
+    int roles = 0;  // waves per column (opr outputs each)
+    int pairs = 0;  // > 0: persistent kernel (LDS finish), columns per workgroup in flight, grid <= CUs
     std::string name;
 };
 
@@ -68,7 +71,9 @@ int xj_horner();  // generation setting (RS_XJ_HORNER, default 0)
 
 bool xj_supported(int m, int K, int R);
 int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 16)
-int xj_roles(int R);         // waves per block for R outputs
+int xj_roles(int R);         // waves per column for R outputs
+int xj_fin();                // generation setting (RS_XJ_FIN, default 0)
+int xj_pairs(int R);         // columns per workgroup (1 unless the LDS-table finish is on)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots);

@@ -85,3 +85,17 @@ def test_xj_decode_matches_oracle(k, r, kind):
     ref = rcv.copy()
     assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
     assert np.array_equal(got, ref)  # erased repair slots stay zero, as in the reference
+
+
+@pytest.mark.parametrize("k,r", [(10, 4), (128, 32), (13, 11)])
+def test_xj_lds_finish_matches_oracle(k, r, monkeypatch):
+    """fin = 1 (gamma-basis bit-planes, Horner through the LDS table) reproduces the oracle too."""
+    monkeypatch.setenv("RS_XJ_FIN", "1")
+    src = xj_source(k, r)
+    assert "ds_read_u16_d16_hi" in src and "fin1" in src
+    want = _random_stripe(k, r, k * 77 + r)
+    assert oracle_encode(k, r, want) == 0
+    mem = Memory((k + r) * S)
+    mem.b[:k * S] = want[:k].reshape(-1)
+    run_block(src, mem, 0, S, k * S, S)
+    assert np.array_equal(mem.b.reshape(k + r, S)[k:], want[k:])

@@ -103,6 +103,8 @@ class Wave:
                 self.sset(a[0], t)
             elif op == "v_mov_b32":
                 self.vset(a[0], self.val(a[1]))
+            elif op == "v_add_u32":
+                self.vset(a[0], (self.val(a[1]).astype(np.uint64) + self.val(a[2])) & np.uint64(0xFFFFFFFF))
             elif op == "v_xor_b32":
                 self.vset(a[0], self.val(a[1]) ^ self.val(a[2]))
             elif op == "v_and_b32":
@@ -156,6 +158,11 @@ class Wave:
                 addr = self.val(base).astype(np.int64) + int(off.split(":")[1])
                 idx = addr[:, None] + np.arange(4)[None, :]
                 self.vset(a[0], self.lds[idx].copy().view("<u4").reshape(-1))
+            elif op in ("ds_read_u16", "ds_read_u16_d16_hi"):
+                # gfx950 (SRAM-ECC): d16 loads do not preserve the other half -- it is zeroed
+                addr = self.val(a[1]).astype(np.int64)
+                h = (self.lds[addr].astype(np.uint32) | (self.lds[addr + 1].astype(np.uint32) << np.uint32(8)))
+                self.vset(a[0], h << np.uint32(16) if op.endswith("_hi") else h)
             elif op == "buffer_load_dword":
                 assert a[3].endswith("offen"), ln
                 addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
@@ -165,6 +172,24 @@ class Wave:
                 self.mem.store32(addr, self.val(a[0]))
             else:
                 raise NotImplementedError(ln)
+
+
+def gamma_table():
+    """T[w] = gamma * w in GF(2^16) (poly 0x1002D, gamma = alpha^257): the LDS table of the fin = 1
+    kernels, as little-endian bytes."""
+    exp = np.zeros(2 * 65535, np.uint32)
+    x = 1
+    for i in range(65535):
+        exp[i] = x
+        x <<= 1
+        if x & 0x10000:
+            x ^= 0x1002D
+    exp[65535:] = exp[:65535]
+    log = np.zeros(65536, np.int64)
+    log[exp[:65535]] = np.arange(65535)
+    t = np.zeros(65536, np.uint16)
+    t[1:] = exp[log[1:] + 257]
+    return t.astype("<u2").view(np.uint8)
 
 
 class Memory:
@@ -189,6 +214,8 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
     m = re.search(r"\(uint32_t\)role \* (\d+)u", src)
     region = int(m.group(1)) if m else 0
     lds = np.zeros(max(1, region * len(roles)) + 64, np.uint8)
+    if "ds_read_u16_d16_hi" in src:  # LDS finish: the gamma table at LDS address 0
+        lds = gamma_table().copy()
     col = (chunk * 256 + np.arange(64) * 4).astype(np.uint32)
     for w, lines in enumerate(roles):
         lb = w * region
