@@ -40,7 +40,9 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * compiled with hiprtc and cached on disk: 0 = off, 1 = every eligible matrix, 2 = the encode matrix
  * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
  * before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
- * 0 = nibble-table kernels). Returns RS_ERR_INVALID for unknown names or values. */
+ * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
+ * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default).
+ * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);
@@ -58,10 +60,13 @@ int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t sym
                uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream);
 
 /* Per-stripe erasure patterns: is_erased is [n_stripes][k + r] in host memory (stripe s lost the
- * symbols flagged in row s). Stripes are grouped by pattern; each distinct pattern is decoded by one
- * launch over its stripes (decode plans are cached, 16 most recent). Returns RS_ERR_CANNOT_RESTORE
- * without writing anything if any stripe has more than r erasures; stripes without erased
- * information symbols are left untouched. Synchronises `stream` once (stripe-id upload). */
+ * symbols flagged in row s). With few distinct patterns (<= 16, or option batch_plans = 0) stripes are
+ * grouped by pattern and each pattern is decoded by one launch over its stripes (host-built plans,
+ * 16 most recent cached). With more (m <= 8 codes; batch_plans = 1 forces it) every stripe's decode
+ * matrix is built on the device from its mask and one launch applies each stripe's own matrix.
+ * Returns RS_ERR_CANNOT_RESTORE without writing anything if any stripe has more than r erasures;
+ * stripes without erased information symbols are left untouched. Synchronises `stream` once
+ * (upload of the stripe lists / masks). */
 int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t n_stripes,
                      uint64_t symbol_size, const bool* is_erased, void* stream);
 

@@ -50,6 +50,8 @@ namespace {
 
 struct DeviceTables {
     uint32_t* d_ltab = nullptr;  // 2048 dwords, see ApplyArgs::ltab
+    uint16_t* d_log = nullptr;   // [65536] discrete log (per-stripe decode plans)
+    uint8_t* d_g8 = nullptr;     // [256] gamma-basis byte of alpha^(257 e), e < 255
 };
 
 std::mutex g_dev_mu;
@@ -77,6 +79,40 @@ int device_tables(int device, const uint32_t** out) {
         t.d_ltab = static_cast<uint32_t*>(p);
     }
     *out = t.d_ltab;
+    return 0;
+}
+
+// log / gamma-byte tables of the device plan builder (k_plan_m8)
+int plan_tables(int device, const uint16_t** logt, const uint8_t** g8) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    DeviceTables& t = g_dev[device];
+    if (!t.d_log) {
+        const Field& F = field();
+        const Gamma8& g = gamma8();
+        std::vector<uint8_t> gb(256, 0);
+        for (uint32_t e = 0; e < 255; ++e) gb[e] = g.coord(F.exp[257u * e]);
+        void* pl = nullptr;
+        void* pg = nullptr;
+        HIP_TRY(hipMalloc(&pl, 65536 * 2));
+        HIP_TRY(hipMemcpy(pl, F.log, 65536 * 2, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&pg, 256));
+        HIP_TRY(hipMemcpy(pg, gb.data(), 256, hipMemcpyHostToDevice));
+        t.d_log = static_cast<uint16_t*>(pl);
+        t.d_g8 = static_cast<uint8_t*>(pg);
+    }
+    *logt = t.d_log;
+    *g8 = t.d_g8;
+    return 0;
+}
+
+// device scratch that only grows (freed with its owner)
+int grow(void** p, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 256)));
+    cap = bytes;
     return 0;
 }
 
@@ -194,11 +230,16 @@ struct rsg_codec {
     uint64_t* stamps = nullptr;  // device buffer for mode 17 (instrumented timing)
     int32_t* d_ids = nullptr;    // stripe-id lists of rsg_decode_batch
     size_t ids_cap = 0;
+    // rsg_decode_batch with device-built per-stripe plans (k_plan_m8): 0 = host plans per distinct
+    // pattern, 1 = device plans, 2 = device plans when more than kHostPlanGroups patterns (default)
+    int batch_plans = 2;
+    uint16_t* d_elem = nullptr;  // [k + r] slot elements alpha^position
+    void *d_masks = nullptr, *d_kr = nullptr, *d_pin = nullptr, *d_pout = nullptr, *d_pidx = nullptr;
+    size_t masks_cap = 0, kr_cap = 0, pin_cap = 0, pout_cap = 0, pidx_cap = 0;
     ~rsg_codec() {
-        if (d_ids) {
-            (void)hipSetDevice(device);
-            (void)hipFree(d_ids);
-        }
+        (void)hipSetDevice(device);
+        for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx})
+            if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
 };
@@ -287,6 +328,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!std::strcmp(name, "jit")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->jit = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "batch_plans")) {
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        c->batch_plans = int(value);
         return 0;
     }
     return RS_ERR_INVALID;
@@ -434,6 +480,97 @@ extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, u
                     int64_t(symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
 }
 
+// Distinct patterns beyond which rsg_decode_batch builds the decode matrices on the device (the
+// host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
+constexpr size_t kHostPlanGroups = 16;
+
+// rsg_decode_batch for m <= 8 codes with device-built plans: k_plan_m8 turns each selected stripe's
+// erasure mask into its decode matrix (nibble records of the V = 1 kernel), then one V = 1 launch (+
+// the tail kernel) applies every stripe's own plan. Stripes without erased information slots are
+// skipped; the caller has validated every pattern.
+static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                                     uint64_t n_stripes, uint64_t S, const bool* is_erased, hipStream_t st) {
+    const size_t n = size_t(c->k) + c->r;
+    if ((S & 1) || (uintptr_t(base) % 8) || (stripe_stride % 8) || (symbol_stride % 8)) return RS_ERR_INVALID;
+    std::vector<int32_t> ids;
+    std::vector<uint8_t> masks;
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const bool* e = is_erased + s * n;
+        bool info = false;
+        for (size_t i = 0; i < c->k; ++i) info |= e[i];
+        if (!info) continue;
+        ids.push_back(int32_t(s));
+        for (size_t i = 0; i < n; ++i) masks.push_back(e[i] ? 1 : 0);
+    }
+    if (ids.empty()) return 0;
+    const uint16_t* logt = nullptr;
+    const uint8_t* g8 = nullptr;
+    int rc = plan_tables(c->device, &logt, &g8);
+    if (rc) return rc;
+    if (!c->d_elem) {
+        const Field& F = field();
+        std::vector<uint16_t> el(n);
+        for (size_t i = 0; i < n; ++i) el[i] = F.exp[c->positions[i]];
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_elem), el.data(), n * 2))) return rc;
+    }
+    const int64_t nsel = int64_t(ids.size());
+    const int tiles = (std::min<int>(c->k, c->r) + 31) / 32;  // erased information slots <= min(k, r)
+    const int64_t in_stride = int64_t(n) + 16, out_stride = int64_t(tiles) * 32, idx_stride = int64_t(tiles) * n * 64;
+    // plans are built and applied in chunks of stripes: at most 256 MiB of nibble records at a time
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nsel, (int64_t(256) << 20) / (idx_stride * 4)));
+    size_t ids_bytes = c->ids_cap * 4;  // ids_cap counts entries
+    rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
+    c->ids_cap = ids_bytes / 4;
+    if (rc) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, masks.size()))) return rc;
+    if ((rc = grow(&c->d_kr, c->kr_cap, size_t(chunk) * 8))) return rc;
+    if ((rc = grow(&c->d_pin, c->pin_cap, size_t(chunk * in_stride) * 4))) return rc;
+    if ((rc = grow(&c->d_pout, c->pout_cap, size_t(chunk * out_stride) * 4))) return rc;
+    if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(chunk * idx_stride) * 4))) return rc;
+    // the host lists must outlive the copies: upload on the caller's stream, then wait once
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {
+        const int64_t cn = std::min(chunk, nsel - c0);
+        PlanArgs pa{};
+        pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+        pa.elem = c->d_elem;
+        pa.logt = logt;
+        pa.g8 = g8;
+        pa.k = c->k;
+        pa.r = c->r;
+        pa.n = int32_t(n);
+        pa.kr = static_cast<int32_t*>(c->d_kr);
+        pa.pin = static_cast<int32_t*>(c->d_pin);
+        pa.pout = static_cast<int32_t*>(c->d_pout);
+        pa.pidx = static_cast<uint32_t*>(c->d_pidx);
+        pa.in_stride = in_stride;
+        pa.out_stride = out_stride;
+        pa.idx_stride = idx_stride;
+        HIP_TRY(launch_plan_m8(pa, cn, st));
+        V1Args v{};
+        v.src = base;
+        v.src_stripe = stripe_stride;
+        v.src_sym = symbol_stride;
+        v.in_idx = pa.pin;
+        v.dst = base;
+        v.dst_stripe = stripe_stride;
+        v.dst_sym = symbol_stride;
+        v.out_idx = pa.pout;
+        v.ltab = c->d_ltab;
+        v.idx = pa.pidx;
+        v.ids = c->d_ids + c0;
+        v.ps_kr = pa.kr;
+        v.ps_in = in_stride;
+        v.ps_out = out_stride;
+        v.ps_idx = idx_stride;
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+    }
+    c->last_kernel = "apply_m8_v1_ps";
+    return 0;
+}
+
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
@@ -456,6 +593,10 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     if (groups.empty() || !symbol_size) return 0;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (c->m <= 8 && n <= 256 &&
+        (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups)))
+        return decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
+                                         int64_t(symbol_stride), n_stripes, symbol_size, is_erased, st);
     std::vector<int32_t> ids;
     std::vector<size_t> first;
     for (auto& g : groups) {

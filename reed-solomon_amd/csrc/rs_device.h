@@ -115,8 +115,9 @@ constexpr int V1_LDS_WORDS = 2048 + RING_SLOTS * 256;
 // Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile
 // blockIdx.y. Per batch of 4 inputs: wave (i % 4) issues input i's DMA RING_B batches ahead; every
 // wave reads its 4 dwords from the ring, maps them to GF(256)^2 coordinates (LDS byte tables) and
-// runs `step(y, i, tile, acc0_15, acc16_31)` per input; one s_barrier per batch. Outputs go back
-// through L^-1 into 4-byte stores.
+// runs `step(y, i, tile, acc0_15, acc16_31, record)` per input (record: the plan's 64-dword nibble
+// record of (tile, input)); one s_barrier per batch. Outputs go back through L^-1 into 4-byte
+// stores. With per-stripe plans (a.ps_kr) K, R, the slot lists and the records are the stripe's own.
 template <class Step>
 __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&& step) {
     for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
@@ -128,12 +129,22 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     const int64_t stripe = RS_STRIPE(a.ids, local);
     const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
     const int tile = blockIdx.y;
-    const int K = a.K;
+    int K = a.K, R = a.R;
+    const int32_t* in_idx = a.in_idx;
+    const int32_t* out_idx = a.out_idx;
+    const uint32_t* idxb = a.idx;
+    if (a.ps_kr) {  // this stripe's own plan
+        K = sload(a.ps_kr + 2 * local);
+        R = sload(a.ps_kr + 2 * local + 1);
+        if (tile * 32 >= R) return;  // uniform over the block: no barrier is left waiting
+        in_idx += local * a.ps_in;
+        out_idx += local * a.ps_out;
+        idxb += local * a.ps_idx;
+    }
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
     const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
-    const int32_t* in_idx = a.in_idx;
     auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
     const int nb = (K + 3) / 4;
     auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
@@ -166,18 +177,18 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 4 * b + j;
-            if (i < K) step(y[j], i, tile, a0, a1);
+            if (i < K) step(y[j], i, tile, a0, a1, idxb + (size_t(tile) * K + i) * 64);
         }
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
     }
     uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
-    const int rows = min(32, a.R - tile * 32);
+    const int rows = min(32, R - tile * 32);
 #pragma unroll
     for (int p = 0; p < 32; ++p) {
         if (p < rows) {
             const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
-            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(a.out_idx + tile * 32 + p)) * a.dst_sym) =
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out_idx + tile * 32 + p)) * a.dst_sym) =
                 lds_lookup4(lt + 1024, v);
         }
     }

@@ -89,7 +89,7 @@ std::string jit_source(const std::vector<uint8_t>& cg, int K, int R, std::vector
       << "\\n\"\n"
          "\".error \\\"rs_v1jit: lookup block size mismatch\\\"\\n\"\n"
          "\".endif\\n\" ::: \"memory\");\n"
-         "  m8_v1_run(a, lds, [&](uint32_t y, int i, int tile, u32x16& a0, u32x16& a1) {\n"
+         "  m8_v1_run(a, lds, [&](uint32_t y, int i, int tile, u32x16& a0, u32x16& a1, const uint32_t*) {\n"
          "    const int off = sload(a.boff + tile * a.K + i);\n"
          "    const uint32_t k1d = 0x1D1D1D1Du;\n"
          "    uint32_t t0, t1;\n"

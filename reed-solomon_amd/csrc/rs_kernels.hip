@@ -387,8 +387,8 @@ __device__ __forceinline__ void m8_v1_step(uint32_t y, const uint32_t* cp, u32x1
 template <int ABL>
 __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
-    m8_v1_run(a, lds, [&](uint32_t y, int i, int tile, u32x16& a0, u32x16& a1) {
-        m8_v1_step<ABL>(y, a.idx + (size_t(tile) * a.K + i) * 64, a0, a1);
+    m8_v1_run(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
+        m8_v1_step<ABL>(y, rec, a0, a1);
     });
 }
 
@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t
     const int64_t bid = blockIdx.x;
     const int64_t local = bid / a.nchunks;  // launch-local stripe
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const int64_t chunk0 = (a.chunk_base + bid - stripe * a.nchunks) * 2048;
+    const int64_t chunk0 = (a.chunk_base + bid - local * a.nchunks) * 2048;
     const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
     const int64_t avail = a.nbytes - col;
     const int tile = blockIdx.y;
@@ -662,6 +662,164 @@ hipError_t launch_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
     unsigned gx = unsigned(std::min<int64_t>((wps + 255) / 256, 64));
     hipLaunchKernelGGL(k_fingerprint, dim3(gx, unsigned(n_stripes)), dim3(256), 0, st, base, stripe_stride, sym_stride,
                        S, sym0, nsym, n_stripes, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------- per-stripe decode plans (m <= 8)
+// One workgroup per stripe builds that stripe's decode matrix from the closed form (SURVEY.md a-16,
+// same evaluation as gf16.cpp:solve_matrix): with E = erased slots, survivors Q, erased information
+// slots P,
+//   lp[q] = sum_{e in E} log(X_q + X_e),  ld[p] = sum_{e in E, e != p} log(X_p + X_e),
+//   C[p][q] = alpha^(lp[q] - ld[p] - log(X_p + X_q))
+// and writes it straight into the V = 1 kernel's form: per (tile, survivor) a 64-dword record of the
+// coefficients' gamma-basis nibbles, plus the slot lists and (K, R). Every C[p][q] lies in GF(256), so
+// its exponent is a multiple of 257 and g8[exponent / 257] is its gamma-basis byte.
+__global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
+    __shared__ uint16_t qe[256], ee[256], pe[256];
+    __shared__ int32_t qs[256], ps[256];
+    __shared__ uint32_t lp[256], ld[256];
+    __shared__ int cnt[4][3];
+    const int64_t s = blockIdx.x;
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const bool valid = j < a.n;
+    const bool er = valid && a.masks[s * a.n + j] != 0;
+    const uint64_t be = __ballot(er), bq = __ballot(valid && !er), bp = __ballot(er && j < a.k);
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    if (lane == 0) {
+        cnt[w][0] = __popcll(be);
+        cnt[w][1] = __popcll(bq);
+        cnt[w][2] = __popcll(bp);
+    }
+    __syncthreads();
+    int oe = 0, oq = 0, op = 0, t = 0, K = 0, R = 0;
+    for (int v = 0; v < 4; ++v) {
+        if (v < w) oe += cnt[v][0], oq += cnt[v][1], op += cnt[v][2];
+        t += cnt[v][0], K += cnt[v][1], R += cnt[v][2];
+    }
+    const uint16_t xj = valid ? a.elem[j] : 0;
+    if (er) {
+        ee[oe + __popcll(be & below)] = xj;
+        if (j < a.k) {
+            const int i = op + __popcll(bp & below);
+            pe[i] = xj;
+            ps[i] = j;
+        }
+    } else if (valid) {
+        const int i = oq + __popcll(bq & below);
+        qe[i] = xj;
+        qs[i] = j;
+    }
+    __syncthreads();
+    constexpr uint32_t N = 65535u;
+    for (int q = j; q < K; q += 256) {
+        uint32_t acc = 0;
+        for (int e = 0; e < t; ++e) acc += a.logt[qe[q] ^ ee[e]];
+        lp[q] = acc % N;
+    }
+    for (int p = j; p < R; p += 256) {
+        uint32_t acc = 0;
+        for (int e = 0; e < t; ++e)
+            if (ee[e] != pe[p]) acc += a.logt[pe[p] ^ ee[e]];  // elements are distinct: skips p itself
+        ld[p] = acc % N;
+    }
+    __syncthreads();
+    if (j == 0) {
+        a.kr[2 * s] = K;
+        a.kr[2 * s + 1] = R;
+    }
+    int32_t* pin = a.pin + s * a.in_stride;
+    for (int q = j; q < a.in_stride; q += 256) pin[q] = q < K ? qs[q] : 0;
+    int32_t* pout = a.pout + s * a.out_stride;
+    for (int p = j; p < a.out_stride; p += 256) pout[p] = p < R ? ps[p] : 0;
+    uint32_t* rec = a.pidx + s * a.idx_stride;
+    const int ntiles = (R + 31) / 32;
+    for (int e = j; e < ntiles * K * 32; e += 256) {
+        const int tile = e / (K * 32), rem = e - tile * K * 32, i = rem >> 5, jj = rem & 31;
+        const int row = tile * 32 + jj;
+        uint32_t b = 0;
+        if (row < R) {
+            const uint32_t L = (lp[i] + 2 * N - ld[row] - a.logt[pe[row] ^ qe[i]]) % N;
+            b = a.g8[L / 257u];
+        }
+        uint32_t* r = rec + (size_t(tile) * K + i) * 64;
+        r[jj] = b & 15u;
+        r[32 + jj] = b >> 4;
+    }
+}
+
+// Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
+// coefficients from the nibble records, multiplication by masked gamma-multiples.
+__global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0, int64_t nbytes) {
+    __shared__ uint32_t lt[2048];
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+    const int64_t local = blockIdx.x;
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int tile = blockIdx.y;
+    int K = a.K, R = a.R;
+    const int32_t* in_idx = a.in_idx;
+    const int32_t* out_idx = a.out_idx;
+    const uint32_t* idxb = a.idx;
+    if (a.ps_kr) {
+        K = a.ps_kr[2 * local];
+        R = a.ps_kr[2 * local + 1];
+        in_idx += local * a.ps_in;
+        out_idx += local * a.ps_out;
+        idxb += local * a.ps_idx;
+    }
+    const int64_t col = col0 + int64_t(threadIdx.x) * 4;
+    const int64_t avail = nbytes - col;
+    if (tile * 32 >= R || avail <= 0) return;
+    const int rows = min(32, R - tile * 32);
+    const uint8_t* src = a.src + stripe * a.src_stripe + col;
+    uint32_t acc[32];
+#pragma unroll
+    for (int p = 0; p < 32; ++p) acc[p] = 0;
+    for (int i = 0; i < K; ++i) {
+        uint32_t x[1];
+        load_slice<4>(x, src + int64_t(in_idx[i]) * a.src_sym, avail);
+        uint32_t m[8];
+        m[0] = lds_lookup4(lt, x[0]);
+#pragma unroll
+        for (int b = 1; b < 8; ++b) m[b] = xt8(m[b - 1]);
+        const uint32_t* r = idxb + (size_t(tile) * K + i) * 64;
+#pragma unroll
+        for (int p = 0; p < 32; ++p) {
+            if (p < rows) {
+                const uint32_t c = r[p] | (r[32 + p] << 4);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) acc[p] ^= m[b] & (0u - ((c >> b) & 1u));
+            }
+        }
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            const uint32_t y[1] = {lds_lookup4(lt + 1024, acc[p])};
+            store_slice<4>(dst + int64_t(out_idx[tile * 32 + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
+hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0) return hipSuccess;
+    if (a.n > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_plan_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st) {
+    if (n_sel <= 0 || tiles <= 0) return hipSuccess;
+    const int64_t full = nbytes / 1024;
+    if (full > 0) {
+        V1Args f = v;
+        f.nchunks = full;
+        hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+    }
+    if (nbytes % 1024)
+        hipLaunchKernelGGL(k_apply_m8_ps_tail, dim3(unsigned(n_sel), unsigned(tiles)), dim3(256), 0, st, v,
+                           full * 1024, nbytes);
     return hipGetLastError();
 }
 

@@ -31,6 +31,23 @@ struct ApplyArgs {
     const int32_t* ids;      // optional [n_stripes] stripe indices (per-stripe erasure patterns); null = 0..n-1
 };
 
+// Per-stripe decode plans (k_plan_m8): one per selected stripe, from its erasure mask.
+struct PlanArgs {
+    const uint8_t* masks;  // [n_sel][n] 1 = erased
+    const uint16_t* elem;  // [n] X_j = alpha^position of slot j
+    const uint16_t* logt;  // [65536] discrete log (entry 0 unused)
+    const uint8_t* g8;     // [255] gamma-basis byte of alpha^(257 e)
+    int32_t k, r, n;       // n = k + r <= 256
+    int32_t* kr;           // [n_sel][2] survivors K, erased information slots R
+    int32_t* pin;          // [n_sel][in_stride] survivor slots, zero-padded
+    int32_t* pout;         // [n_sel][out_stride] erased information slots, zero-padded
+    uint32_t* pidx;        // [n_sel][idx_stride] V = 1 nibble records, (tile * K + i) * 64
+    int64_t in_stride, out_stride, idx_stride;
+};
+hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st);
+// V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
+hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
+
 int apply_tile_rows(int m, int R);
 // V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff);

@@ -19,6 +19,11 @@ struct V1Args {
     int32_t K, R;
     int64_t nchunks;         // 1 KiB column chunks per symbol processed by this launch
     const int32_t* ids;      // optional [n_stripes] stripe indices; null = 0..n-1
+    // per-stripe plans (rsg_decode_batch with device-built decode matrices), indexed by the
+    // launch-local stripe s: K, R = ps_kr[2s], ps_kr[2s + 1]; in_idx, out_idx and idx advance by
+    // s * ps_in / ps_out / ps_idx elements. Null = one plan for every stripe (K, R above).
+    const int32_t* ps_kr;
+    int64_t ps_in, ps_out, ps_idx;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -207,11 +207,13 @@ def _stream_ptr(stream):
 class Codec:
     """Batched (k, r) engine on one GPU. Buffers are torch uint8 CUDA tensors (or raw pointers)."""
 
-    def __init__(self, k, r, device=0, jit=None, m8_mode=None, xj=None):
+    def __init__(self, k, r, device=0, jit=None, m8_mode=None, xj=None, batch_plans=None):
         """jit: None = library default (2), 0/False = generic kernels only, 1/True = specialise every
         eligible matrix, 2 = encode matrix + decode matrices from their second use.
         xj: specialised kernel family, None = library default (1 = bit-plane XOR kernels, rs_xj.hpp),
-        0 = nibble-table rs_v1jit kernels."""
+        0 = nibble-table rs_v1jit kernels.
+        batch_plans (decode_batch): None = library default (2 = decode matrices built on the device
+        when a batch has more than 16 distinct patterns), 0 = host plans per pattern, 1 = device."""
         self.k, self.r, self.device = k, r, device
         h = P()
         rc = _lib.rsg_codec_create(device, k, r, ctypes.byref(h))
@@ -220,6 +222,8 @@ class Codec:
         self._h = h
         if jit is not None:
             self.set_option("jit", int(jit))
+        if batch_plans is not None:
+            self.set_option("batch_plans", int(batch_plans))
         if m8_mode is not None:
             self.set_option("m8_mode", m8_mode)
         if xj is not None:

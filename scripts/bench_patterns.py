@@ -1,0 +1,76 @@
+"""rsg_decode_batch with a different erasure pattern on every stripe (C3 shape): device-built plans
+(batch_plans=1) against host plans per pattern (batch_plans=0), and the single-pattern decode of the
+same stripes for reference. GB/s counts the algorithmic bytes of each stripe: survivors read
+(k + r - t) + information symbols written (t_info)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd"))
+import rs_amd  # noqa: E402
+
+k, r, S = 128, 32, 65536
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+mode = sys.argv[2] if len(sys.argv) > 2 else "t32info"
+rng = np.random.default_rng(5)
+pats = np.zeros((n, k + r), bool)
+for s in range(n):
+    if mode == "t32info":  # r information erasures, a different set per stripe
+        pats[s, rng.choice(k, r, replace=False)] = True
+    else:  # 1..r erasures anywhere
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+t = pats.sum(1)
+tinfo = pats[:, :k].sum(1)
+alg = float(((k + r - t) + tinfo)[tinfo > 0].sum()) * S
+dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")
+rs_amd.fill_info(dev, k, seed=0x5EED)
+enc = rs_amd.Codec(k, r)
+enc.encode(dev)
+torch.cuda.synchronize()
+
+
+def fp():
+    out = torch.empty(n, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(dev, 0, k, out)
+    return out
+
+
+ref_fp = fp()
+mask = torch.from_numpy(pats).to("cuda")
+
+
+def run(codec, label, reps):
+    times = []
+    for _ in range(reps):
+        dev.masked_fill_(mask[:, :, None], 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        codec.decode_batch(dev, pats)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ok = bool(torch.equal(fp(), ref_fp))
+    ms = float(np.median(times)) * 1e3
+    print(json.dumps({"case": label, "stripes": n, "patterns": mode, "ms": round(ms, 3),
+                      "GBps": round(alg / ms / 1e6, 1), "restored": ok, "kernel": codec.last_kernel}), flush=True)
+
+
+run(rs_amd.Codec(k, r, batch_plans=1), "device_plans", 5)
+run(rs_amd.Codec(k, r, batch_plans=0), "host_plans", 2)
+# the same bytes with one shared pattern (t = r information erasures): generic and specialised kernels
+one = np.zeros(k + r, bool)
+one[np.arange(r) * (k // r)] = True
+for label, kw in (("one_pattern_generic", dict(jit=0)), ("one_pattern_xj", dict())):
+    c = rs_amd.Codec(k, r, **kw)
+    times = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        c.decode(dev, one)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ms = float(np.median(times[1:])) * 1e3
+    print(json.dumps({"case": label, "stripes": n, "ms": round(ms, 3),
+                      "GBps": round(n * (k + r) * S / ms / 1e6, 1), "kernel": c.last_kernel}), flush=True)

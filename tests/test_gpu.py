@@ -201,14 +201,17 @@ def test_fingerprint_matches_cpu_port():
         assert int(fp[s]) == fingerprint_np(host[s], 0, k + r)
 
 
-def test_decode_batch_per_stripe_patterns():
+@pytest.mark.parametrize("plans", [0, 1])
+@pytest.mark.parametrize("S", [8192, 8712])
+def test_decode_batch_per_stripe_patterns(S, plans):
     """rsg_decode_batch: every stripe has its own erasure pattern (information and repair erasures,
-    stripes with nothing to restore, repeated patterns) -- each stripe bit-exact vs the oracle."""
-    k, r, S, n = 128, 32, 8192, 40
+    stripes with nothing to restore, repeated patterns) -- each stripe bit-exact vs the oracle, with
+    host plans per pattern (0) and device-built plans (1); S = 8712 adds tail columns."""
+    k, r, n = 128, 32, 40
     rng = np.random.default_rng(21)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xB7)
-    codec = rs_amd.Codec(k, r)
+    codec = rs_amd.Codec(k, r, batch_plans=plans)
     codec.encode(dev)
     torch.cuda.synchronize()
     full = dev.cpu().numpy()
@@ -274,3 +277,35 @@ def test_xor_kernel_with_tail_columns(S):
         want[er] = 0
         assert oracle_decode(k, r, want, er, int(er.sum())) == 0
         assert np.array_equal(back[s], want), f"decode stripe {s}"
+
+
+@pytest.mark.parametrize("k,r,S,n", [(128, 32, 4096 + 1032, 96), (10, 4, 1024 + 8, 300), (200, 55, 2048, 24)])
+def test_decode_batch_device_plans_distinct_patterns(k, r, S, n):
+    """Every stripe lost a different random set (1..r symbols, information and repair slots): the
+    default policy builds the decode matrices on the device; every stripe is bit-exact vs the oracle
+    and the information symbols come back."""
+    rng = np.random.default_rng(k * 7 + n)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xC3)
+    codec = rs_amd.Codec(k, r)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    pats[0, :] = False
+    pats[0, :r] = True  # r information erasures (largest plan)
+    poisoned = full.copy()
+    poisoned[pats] = 0
+    dev.copy_(torch.from_numpy(poisoned))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert codec.last_kernel == "apply_m8_v1_ps"
+    got = dev.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(got[s, :k], full[s, :k]), f"stripe {s}"
+        if s % 8 == 0:
+            want = poisoned[s].copy()
+            assert oracle_decode(k, r, want, pats[s], int(pats[s].sum())) == 0
+            assert np.array_equal(got[s], want), f"stripe {s}"
