@@ -30,6 +30,8 @@ Variants (all but "full", "split" and "split_mul" give wrong results; they are t
   v1_plain   v1 without gpr-index mode (timing ablation)
   v1_jitcall input step of the matrix-specialised V = 1 kernel (multiples, tables, call into the
              input's generated lookup block)
+  m16_v1     m = 16 input step (k_apply_m16_v1): 16 multiples x * alpha^j, four nibble tables, 256
+             gpr-indexed lookups for 64 outputs (m16_v1_plain: fixed registers, timing only)
 """
 import os
 import sys
@@ -132,6 +134,47 @@ if variant == "v1_jitcall":
             L.extend(table_ops((tl,)))
     L.extend(table_ops((th,)))
     e("s_swappc_b64 s[72:73], s[74:75]")
+    emit(out)
+    sys.exit(0)
+
+if variant in ("m16_v1", "m16_v1_plain"):
+    # m = 16, one dword (two GF(2^16) words) per lane per step (k_apply_m16_v1), 64 outputs per tile:
+    #   T_n v[8 + 16n : 23 + 16n]  nibble table n: entry e = XOR of x * alpha^(4n + b) over the set bits b
+    #   acc v[72:135]               output p in v[72 + p]
+    #   s[40:55] / s[56:71]         two 16-index buffers of the input's 256-dword record
+    # Record of (tile, input): dword 64n + p = 16n + nibble n of output p's coefficient, so every
+    # lookup indexes from v8: s_set_gpr_idx_idx <record dword> retargets src0 of the next v_xor.
+    # x * alpha on packed words with full-rate ops only: u = m & 0x80008000, s = m ^ u, w = u - (u >> 15)
+    # (0x7FFF in every lane whose top bit was set), m * alpha = (s + s) ^ (w & 0x002D002D)
+    # [s + s cannot carry across lanes: s has both top bits clear].
+    T, ACC = 8, 72
+    tv = ("%[t0]", "%[t1]")
+    mreg = lambda j: T + 16 * (j // 4) + slots[j % 4]
+    e("s_load_dwordx16 s[40:55], %[cp], 0x0")
+    e(f"v_mov_b32 v{mreg(0)}, %[y0]")
+    for j in range(1, 16):
+        src, dst = mreg(j - 1), mreg(j)
+        for op in ["v_and_b32 {ta}, 0x80008000, v{src}", "v_lshrrev_b32 {tb}, 15, {ta}",
+                   "v_xor_b32 v{dst}, v{src}, {ta}", "v_sub_u32 {tb}, {ta}, {tb}", "v_add_u32 v{dst}, v{dst}, v{dst}",
+                   "v_bitop3_b32 v{dst}, v{dst}, {tb}, %[k2d] bitop3:0x78"]:
+            e(op.format(ta=tv[0], tb=tv[1], src=src, dst=dst))
+        if j % 4 == 3:
+            L.extend(table_ops((T + 16 * (j // 4),)))
+    idx = variant == "m16_v1"
+    for b in range(16):
+        buf, nxt = (40, 56) if b % 2 == 0 else (56, 40)
+        e("s_waitcnt lgkmcnt(0)")
+        if b + 1 < 16:  # the other buffer's indices were consumed by the previous batch
+            e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (b + 1))}")
+        for l in range(16):
+            q = 16 * b + l
+            n, p = q // 64, q % 64
+            if idx:
+                e(f"s_set_gpr_idx_on s{buf}, gpr_idx(SRC0)" if q == 0 else f"s_set_gpr_idx_idx s{buf + l}")
+            src = T if idx else T + 16 * n + (p * 7 + 3) % 16
+            e(f"v_xor_b32 v{ACC + p}, v{src}, v{ACC + p}")
+    if idx:
+        e("s_set_gpr_idx_off")
     emit(out)
     sys.exit(0)
 

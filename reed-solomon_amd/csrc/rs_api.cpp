@@ -123,7 +123,7 @@ struct DevPlan {
     int32_t* d_in = nullptr;
     int32_t* d_out = nullptr;
     uint32_t* d_coef = nullptr;
-    uint32_t* d_idx = nullptr;  // m8, rt 32: pre-split nibble indices for the asm kernel
+    uint32_t* d_idx = nullptr;  // m8, rt 32: pre-split nibble indices; m16, rt 64: table indices (asm kernels)
     std::vector<uint16_t> matrix;  // R x K, GF(2^16)
     std::vector<int32_t> in_slots, out_slots;
     std::unique_ptr<JitKernel> jit;  // matrix-specialised kernel, if built
@@ -198,6 +198,20 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
                     idx[(size_t(t) * K + i) * 64 + 32 + j] = c >> 4;
                 }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
+    } else if (rt == 64 && size_t(p->ntiles) * K * 1024 <= (size_t(256) << 20)) {
+        // k_apply_m16_v1: per (tile, input) 256 table indices, [64n + j] = 16n + nibble n of output j
+        std::vector<uint32_t> idx(size_t(p->ntiles) * K * 256, 0);
+        for (int t = 0; t < p->ntiles; ++t)
+            for (int i = 0; i < K; ++i) {
+                uint32_t* rec = idx.data() + (size_t(t) * K + i) * 256;
+                for (int n = 0; n < 4; ++n)
+                    for (int j = 0; j < 64; ++j) {
+                        const int row = t * 64 + j;
+                        const uint32_t c = row < R ? M[size_t(row) * K + i] : 0;
+                        rec[64 * n + j] = uint32_t(16 * n) + ((c >> (4 * n)) & 15u);
+                    }
+            }
+        if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
     }
     in_slots.resize(in_slots.size() + 16, 0);  // kernels read slot indices in vectors past the end
     if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
@@ -224,6 +238,7 @@ struct rsg_codec {
     std::map<std::vector<uint8_t>, std::unique_ptr<DevPlan>> dec;
     std::vector<std::vector<uint8_t>> dec_lru;
     int m8_mode = 18;
+    int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
@@ -330,6 +345,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->jit = int(value);
         return 0;
     }
+    if (!std::strcmp(name, "m16_mode")) {
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        c->m16_mode = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "batch_plans")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->batch_plans = int(value);
@@ -392,7 +412,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.K = p.K;
     a.R = p.R;
     a.nbytes = int64_t(S);
-    a.mode = c->m8_mode;
+    a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
     const int nt32 = (p.R + 31) / 32;
@@ -427,7 +447,8 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     // gpr-index kernel families (modes >= 2) always tile 32 rows
     const int rt = p.m == 8 && a.mode >= 2 ? 32 : p.rt;
     c->last_kernel = p.m == 8 ? (std::string("apply_m8_rt") + std::to_string(rt) + "_mode" + std::to_string(a.mode))
-                              : (std::string("apply_m16_rt") + std::to_string(rt));
+                     : (rt == 64 && p.d_idx && a.mode < 2) ? std::string(a.mode ? "apply_m16_v1_plain" : "apply_m16_v1")
+                                                             : (std::string("apply_m16_rt") + std::to_string(rt));
     HIP_TRY(launch_apply(p.m, rt, a, int64_t(n_stripes), st));
     return 0;
 }

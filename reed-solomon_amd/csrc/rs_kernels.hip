@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(256) k_apply_m16(ApplyArgs a) {
     const int64_t bid = blockIdx.x;
     const int64_t local = bid / a.nchunks;  // launch-local stripe
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const int64_t col = (bid - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
+    const int64_t col = (a.chunk_base + bid - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
     const int64_t avail = a.nbytes - col;
     if (avail <= 0) return;
     const int tile = blockIdx.y;
@@ -478,6 +478,98 @@ __global__ void __launch_bounds__(256) k_apply_m16(ApplyArgs a) {
         if (p < rows) {
             uint32_t y[1] = {acc[p]};
             store_slice<4>(dst + int64_t(a.out_idx[tile * RT + p]) * a.dst_sym, y, avail);
+        }
+    }
+}
+
+// --------------------------------------------- m = 16, hand-scheduled step, one dword per lane
+// Same block structure as m8_v1_run (1 KiB column chunk, inputs staged HBM -> LDS by DMA, one
+// s_barrier per batch of 4 inputs), 64 outputs per tile, no coordinate change. Per input the step
+// (csrc/gen_asm.py m16_v1) forms x * alpha^j (j < 16), four nibble tables in v[8:71] and 256
+// lookups, each one s_set_gpr_idx_idx + one v_xor (record: [tile][K][256] table indices).
+template <int ABL>
+__device__ __forceinline__ void m16_v1_step(uint32_t y, const uint32_t* cp, u32x16& a0, u32x16& a1, u32x16& a2,
+                                            u32x16& a3) {
+    const uint32_t k2d = 0x002D002Du;
+    uint32_t t0, t1;
+    u32x16 T0, T1, T2, T3;
+#define RS_M16_V1_OPERANDS                                                                                    \
+    : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "=&{v[8:23]}"(T0),        \
+      "=&{v[24:39]}"(T1), "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), [t0] "=&v"(t0), [t1] "=&v"(t1)                \
+    : [y0] "v"(y), [cp] "s"(cp), [k2d] "v"(k2d)                                                                 \
+    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", \
+      "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71"
+    if constexpr (ABL == 0) {
+        asm volatile(
+#include "gen/m8_idx_asm_m16_v1.inc"
+            RS_M16_V1_OPERANDS);
+    } else {
+        asm volatile(
+#include "gen/m8_idx_asm_m16_v1_plain.inc"
+            RS_M16_V1_OPERANDS);
+    }
+#undef RS_M16_V1_OPERANDS
+}
+
+template <int ABL>
+__global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[RING_SLOTS * 256];
+    const int64_t bid = blockIdx.x;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
+    const int tile = blockIdx.y;
+    const int K = a.K;
+    const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
+    const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
+    const int32_t* in_idx = a.in_idx;
+    auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
+    const int nb = (K + 3) / 4;
+    auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
+        int c = 0;
+        for (int b = lo; b <= hi; ++b)
+            if (b < nb && 4 * b + wave < K) c += 1;
+        return c;
+    };
+    auto wait_mine = [&](int n) {
+        if (n <= 0)
+            wait_vm<0>();
+        else if (n == 1)
+            wait_vm<1>();
+        else if (n == 2)
+            wait_vm<2>();
+        else
+            wait_vm<3>();
+    };
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int b = 0; b < RING_B; ++b)
+        if (4 * b + wave < K) issue(4 * b + wave);
+    wait_mine(mine(1, RING_B - 1));
+    asm volatile("s_barrier" ::: "memory");
+    const uint32_t* rec = a.idx + size_t(tile) * K * 256;
+    for (int b = 0; b < nb; ++b) {
+        const int ib = 4 * (b + RING_B) + wave;
+        if (ib < K) issue(ib);
+        uint32_t y[4];  // slots past K hold stale bytes and are not used
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = ring[((4 * b + j) % RING_SLOTS) * 256 + threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * b + j;
+            if (i < K) m16_v1_step<ABL>(y[j], rec + size_t(i) * 256, a0, a1, a2, a3);
+        }
+        wait_mine(mine(b + 2, b + RING_B));
+        asm volatile("s_barrier" ::: "memory");
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
+    const int rows = min(64, a.R - tile * 64);
+#pragma unroll
+    for (int p = 0; p < 64; ++p) {
+        if (p < rows) {
+            const uint32_t v = p < 16 ? a0[p & 15] : p < 32 ? a1[p & 15] : p < 48 ? a2[p & 15] : a3[p & 15];
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(a.out_idx + tile * 64 + p)) * a.dst_sym) = v;
         }
     }
 }
@@ -614,6 +706,27 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
 
 template <int RT>
 static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
+    if (RT == 64 && a.idx && (a.mode == 0 || a.mode == 1)) {
+        // hand-scheduled kernel over the full 1 KiB chunks (mode 1: fixed-register timing ablation),
+        // the compiled kernel over the rest of each symbol
+        const int64_t full = a.nbytes / 1024;
+        const unsigned tiles = unsigned((a.R + 63) / 64);
+        if (full > 0) {
+            const V1Args v = v1_args(a, full, nullptr);
+            dim3 g(unsigned(n_stripes * full), tiles);
+            if (a.mode == 0)
+                hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
+            else
+                hipLaunchKernelGGL((k_apply_m16_v1<1>), g, dim3(256), 0, st, v);
+        }
+        if (a.nbytes % 1024) {
+            ApplyArgs t = a;
+            t.chunk_base = full;
+            t.nchunks = 1;
+            hipLaunchKernelGGL(k_apply_m16<64>, dim3(unsigned(n_stripes), tiles), dim3(256), 0, st, t);
+        }
+        return hipGetLastError();
+    }
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
     hipLaunchKernelGGL(k_apply_m16<RT>, grid, dim3(256), 0, st, a);
     return hipGetLastError();

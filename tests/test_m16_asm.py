@@ -1,0 +1,64 @@
+"""The hand-scheduled m = 16 input step (reed-solomon_amd/csrc/gen_asm.py variant m16_v1, used by
+k_apply_m16_v1) run by the instruction emulator on CPU: after one step every accumulator must hold
+acc ^ c_p * x for both packed GF(2^16) words of every lane, with c_p taken from the step's index
+record exactly as rs_api.cpp:build_plan lays it out."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+
+from xj_emu import Memory, Wave
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GEN = os.path.join(HERE, "..", "reed-solomon_amd", "csrc", "gen_asm.py")
+
+
+def gf_mul(a, b):
+    """GF(2^16) product, poly 0x1002D (numpy, elementwise)."""
+    a = np.asarray(a, np.uint32).copy()
+    b = np.asarray(b, np.uint32).copy()
+    r = np.zeros(np.broadcast(a, b).shape, np.uint32)
+    for _ in range(16):
+        r ^= np.where(b & 1, a, 0).astype(np.uint32)
+        b >>= 1
+        a = ((a << 1) ^ np.where(a & 0x8000, 0x1002D, 0)).astype(np.uint32) & 0xFFFF
+    return r
+
+
+def step_lines(tmp_path):
+    out = os.path.join(tmp_path, "m16.inc")
+    subprocess.check_call([sys.executable, GEN, out, "m16_v1"])
+    lines = []
+    for ln in open(out):
+        m = re.match(r'^"(.*)\\n\\t"$', ln.strip())
+        if m:
+            lines.append(m.group(1))
+    return lines
+
+
+def test_m16_v1_step_matches_gf_multiply(tmp_path):
+    rng = np.random.default_rng(16)
+    coef = rng.integers(0, 65536, 64, dtype=np.uint32)
+    coef[:4] = [0, 1, 2, 0xFFFF]
+    rec = np.zeros(256, np.uint32)
+    for n in range(4):
+        rec[64 * n:64 * n + 64] = 16 * n + ((coef >> (4 * n)) & 15)
+    mem = Memory(4096)
+    mem.b[1024:2048] = rec.astype("<u4").view(np.uint8)
+    x = rng.integers(0, 2 ** 32, 64, dtype=np.uint64).astype(np.uint32)
+    acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
+    text = "\n".join(step_lines(str(tmp_path)))
+    text = (text.replace("%[t0]", "v200").replace("%[t1]", "v201").replace("%[y0]", "v202")
+            .replace("%[k2d]", "v203").replace("%[cp]", "s[90:91]"))
+    w = Wave(mem, {})
+    w.v[202] = x
+    w.v[203] = 0x002D002D
+    w.v[72:136] = acc0
+    w.s[90], w.s[91] = 1024, 0
+    w.run(text.splitlines(), [])
+    lo, hi = x & 0xFFFF, x >> 16
+    for p in range(64):
+        want = (gf_mul(lo, coef[p]) | (gf_mul(hi, coef[p]) << 16)) ^ acc0[p]
+        assert np.array_equal(w.v[72 + p], want), p

@@ -81,6 +81,30 @@ class Wave:
             a = [x.strip() for x in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
             if op in ("s_nop", "s_waitcnt", "s_branch", "s_getpc_b64", "s_setpc_b64"):
                 continue
+            # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
+            if op == "s_set_gpr_idx_on":
+                assert a[1] == "gpr_idx(SRC0)", ln
+                self.gpr_idx = self.val(a[0]) & 0xFF
+                continue
+            if op == "s_set_gpr_idx_idx":
+                self.gpr_idx = self.val(a[0]) & 0xFF
+                continue
+            if op == "s_set_gpr_idx_off":
+                self.gpr_idx = None
+                continue
+            if getattr(self, "gpr_idx", None) is not None and op.startswith("v_") and len(a) > 1:
+                a[1] = f"v{_vreg(a[1]) + self.gpr_idx}"
+            if op == "s_load_dwordx16":
+                m = re.match(r"s\[(\d+):(\d+)\]", a[0])
+                lo = int(m.group(1))
+                addr = self.pair(a[1]) + int(a[2], 0)
+                words = self.mem.load32(np.uint64(addr) + 4 * np.arange(16, dtype=np.uint64))
+                for w in range(16):
+                    self.s[lo + w] = np.uint64(int(words[w]))
+                continue
+            if op == "v_sub_u32":
+                self.vset(a[0], (self.val(a[1]).astype(np.int64) - self.val(a[2])) & 0xFFFFFFFF)
+                continue
             if op == "s_swappc_b64":
                 self.run(finish, finish)
             elif op == "s_mov_b32":
