@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--r", type=int, default=32)
     ap.add_argument("--symbol", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c", "m16p"],
                     help="auto = library default policy (matrix-specialised kernels, generic fallback)")
     ap.add_argument("--cpu-stripes", type=int, default=128, help="CPU-baseline sample (stripes, resident)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (passes repeat)")
@@ -197,10 +197,10 @@ def main():
     erased = rs_amd.bench_pattern(k, r)
     t = int(erased.sum())
     opts = {"auto": {}, "jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(jit=0, m8_mode=18), "idx": dict(jit=0, m8_mode=2),
-            "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1), "m16c": {}}[args.kernel]
+            "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1), "m16c": {}, "m16p": {}}[args.kernel]
     codec = rs_amd.Codec(k, r, device=local, **opts)
-    if args.kernel == "m16c":  # GF(2^16) codes: the compiled generic kernel instead of the asm one
-        codec.set_option("m16_mode", 2)
+    if args.kernel in ("m16c", "m16p"):  # GF(2^16) codes: compiled kernel / asm timing ablation (wrong results)
+        codec.set_option("m16_mode", 2 if args.kernel == "m16c" else 1)
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     stripe0, _ = rs_dist.weak_shard(n, rank)  # this rank's global stripe ids: [stripe0, stripe0 + n)

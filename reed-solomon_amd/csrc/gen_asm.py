@@ -141,38 +141,69 @@ if variant in ("m16_v1", "m16_v1_plain"):
     # m = 16, one dword (two GF(2^16) words) per lane per step (k_apply_m16_v1), 64 outputs per tile:
     #   T_n v[8 + 16n : 23 + 16n]  nibble table n: entry e = XOR of x * alpha^(4n + b) over the set bits b
     #   acc v[72:135]               output p in v[72 + p]
-    #   s[40:55] / s[56:71]         two 16-index buffers of the input's 256-dword record
-    # Record of (tile, input): dword 64n + p = 16n + nibble n of output p's coefficient, so every
-    # lookup indexes from v8: s_set_gpr_idx_idx <record dword> retargets src0 of the next v_xor.
-    # x * alpha on packed words with full-rate ops only: u = m & 0x80008000, s = m ^ u, w = u - (u >> 15)
-    # (0x7FFF in every lane whose top bit was set), m * alpha = (s + s) ^ (w & 0x002D002D)
-    # [s + s cannot carry across lanes: s has both top bits clear].
+    #   s[40:55] / s[56:71]         two 16-dword buffers, one nibble plane of the record each;
+    #   s72 scratch, s73 = 0xFFFEFFFE
+    # Record of (tile, input): 64 dwords, byte 64n + p = 16n + nibble n of output p, so every lookup
+    # indexes from v8; s_set_gpr_idx_idx takes bits [7:0] of its operand, the other bytes come down
+    # with one s_lshr_b32. Plane n + 1 (or the next input's plane 0: the record array is padded by one
+    # input) loads while plane n is consumed; this input's plane 0 was requested by the previous step
+    # (or by the kernel before the first one) and arrives in s[40:55].
+    # Plane n reads only table T_n, so T_(n+1) is built while plane n's lookups run. In gpr-index mode
+    # only VGPR src0 operands are offset, so every building op keeps src0 a constant or an SGPR:
+    #   x * alpha on packed words: ((x << 1) & 0xFFFEFFFE) ^ (((x >> 15) & 0x10001) * 0x2D)
+    #   table XORs as v_bitop3_b32 with a constant first operand (truth table 0x66 = src1 ^ src2).
     T, ACC = 8, 72
-    tv = ("%[t0]", "%[t1]")
+    ta, tb = "%[t0]", "%[t1]"
     mreg = lambda j: T + 16 * (j // 4) + slots[j % 4]
-    e("s_load_dwordx16 s[40:55], %[cp], 0x0")
-    e(f"v_mov_b32 v{mreg(0)}, %[y0]")
-    for j in range(1, 16):
+
+    def xt(j):  # multiple j from multiple j - 1
         src, dst = mreg(j - 1), mreg(j)
-        for op in ["v_and_b32 {ta}, 0x80008000, v{src}", "v_lshrrev_b32 {tb}, 15, {ta}",
-                   "v_xor_b32 v{dst}, v{src}, {ta}", "v_sub_u32 {tb}, {ta}, {tb}", "v_add_u32 v{dst}, v{dst}, v{dst}",
-                   "v_bitop3_b32 v{dst}, v{dst}, {tb}, %[k2d] bitop3:0x78"]:
-            e(op.format(ta=tv[0], tb=tv[1], src=src, dst=dst))
-        if j % 4 == 3:
-            L.extend(table_ops((T + 16 * (j // 4),)))
+        return [f"v_lshrrev_b32 {ta}, 15, v{src}", f"v_and_b32 {ta}, 0x10001, {ta}", f"v_mul_u32_u24 {ta}, 45, {ta}",
+                f"v_lshlrev_b32 {tb}, 1, v{src}", f"v_bitop3_b32 v{dst}, s73, {tb}, {ta} bitop3:0x6a"]
+
+    def tab(b):
+        ops = [f"v_mov_b32 v{b}, 0"]
+        pairs = [(3, 1, 2), (5, 4, 1), (6, 4, 2), (7, 4, 3)] + [(8 + k, 8, k) for k in range(1, 8)]
+        ops += [f"v_bitop3_b32 v{b + d}, 0, v{b + x}, v{b + y} bitop3:0x66" for d, x, y in pairs]
+        return ops
+
+    def build(n):  # table n from multiple 4n - 1 (or the input for n = 0)
+        ops = [f"v_mov_b32 v{mreg(0)}, %[y0]"] if n == 0 else xt(4 * n)
+        for j in range(4 * n + 1, 4 * n + 4):
+            ops += xt(j)
+        return ops + tab(T + 16 * n)
+
+    e("s_mov_b32 s73, 0xfffefffe")
+    L.extend(build(0))
     idx = variant == "m16_v1"
-    for b in range(16):
-        buf, nxt = (40, 56) if b % 2 == 0 else (56, 40)
+    for n in range(4):
+        buf, nxt = (40, 56) if n % 2 == 0 else (56, 40)
         e("s_waitcnt lgkmcnt(0)")
-        if b + 1 < 16:  # the other buffer's indices were consumed by the previous batch
-            e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (b + 1))}")
-        for l in range(16):
-            q = 16 * b + l
-            n, p = q // 64, q % 64
+        e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (n + 1))}")
+        look = []
+        for l in range(64):
+            w, b = divmod(l, 4)
+            grp = []
             if idx:
-                e(f"s_set_gpr_idx_on s{buf}, gpr_idx(SRC0)" if q == 0 else f"s_set_gpr_idx_idx s{buf + l}")
-            src = T if idx else T + 16 * n + (p * 7 + 3) % 16
-            e(f"v_xor_b32 v{ACC + p}, v{src}, v{ACC + p}")
+                if b == 0:
+                    sreg = f"s{buf + w}"
+                else:
+                    grp.append(f"s_lshr_b32 s72, s{buf + w}, {8 * b}")
+                    sreg = "s72"
+                grp.append(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if n == 0 and l == 0 else f"s_set_gpr_idx_idx {sreg}")
+            src = T if idx else T + 16 * n + (l * 7 + 3) % 16
+            grp.append(f"v_xor_b32 v{ACC + l}, v{src}, v{ACC + l}")
+            look.append(grp)
+        other = build(n + 1) if n < 3 else []
+        # spread the next table's ops over the 64 lookups (after each lookup's v_xor)
+        k = 0
+        for l, grp in enumerate(look):
+            L.extend(grp)
+            want = (l + 1) * len(other) // 64
+            while k < want:
+                e(other[k])
+                k += 1
+        L.extend(other[k:])
     if idx:
         e("s_set_gpr_idx_off")
     emit(out)

@@ -486,19 +486,21 @@ __global__ void __launch_bounds__(256) k_apply_m16(ApplyArgs a) {
 // Same block structure as m8_v1_run (1 KiB column chunk, inputs staged HBM -> LDS by DMA, one
 // s_barrier per batch of 4 inputs), 64 outputs per tile, no coordinate change. Per input the step
 // (csrc/gen_asm.py m16_v1) forms x * alpha^j (j < 16), four nibble tables in v[8:71] and 256
-// lookups, each one s_set_gpr_idx_idx + one v_xor (record: [tile][K][256] table indices).
+// lookups, each one s_set_gpr_idx_idx + one v_xor (record: [tile][K + 1][64] dwords of packed
+// byte indices; s[40:55] carries the current plane from one step to the next).
 template <int ABL>
-__device__ __forceinline__ void m16_v1_step(uint32_t y, const uint32_t* cp, u32x16& a0, u32x16& a1, u32x16& a2,
-                                            u32x16& a3) {
+__device__ __forceinline__ void m16_v1_step(uint32_t y, const uint32_t* cp, u32x16& plane, u32x16& a0, u32x16& a1,
+                                            u32x16& a2, u32x16& a3) {
     const uint32_t k2d = 0x002D002Du;
     uint32_t t0, t1;
     u32x16 T0, T1, T2, T3;
 #define RS_M16_V1_OPERANDS                                                                                    \
     : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "=&{v[8:23]}"(T0),        \
-      "=&{v[24:39]}"(T1), "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), [t0] "=&v"(t0), [t1] "=&v"(t1)                \
+      "=&{v[24:39]}"(T1), "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), [t0] "=&v"(t0), [t1] "=&v"(t1),               \
+      "+{s[40:55]}"(plane)                                                                                       \
     : [y0] "v"(y), [cp] "s"(cp), [k2d] "v"(k2d)                                                                 \
-    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", \
-      "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71"
+    : "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
+      "s72", "s73"
     if constexpr (ABL == 0) {
         asm volatile(
 #include "gen/m8_idx_asm_m16_v1.inc"
@@ -548,7 +550,11 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
         if (4 * b + wave < K) issue(4 * b + wave);
     wait_mine(mine(1, RING_B - 1));
     asm volatile("s_barrier" ::: "memory");
-    const uint32_t* rec = a.idx + size_t(tile) * K * 256;
+    // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
+    // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
+    const uint32_t* rec = a.idx + size_t(tile) * (K + 1) * 64;
+    u32x16 plane;  // plane 0 of the next step's record, requested one step ahead (s[40:55] in the asm)
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");
     for (int b = 0; b < nb; ++b) {
         const int ib = 4 * (b + RING_B) + wave;
         if (ib < K) issue(ib);
@@ -558,7 +564,7 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 4 * b + j;
-            if (i < K) m16_v1_step<ABL>(y[j], rec + size_t(i) * 256, a0, a1, a2, a3);
+            if (i < K) m16_v1_step<ABL>(y[j], rec + size_t(i) * 64, plane, a0, a1, a2, a3);
         }
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");

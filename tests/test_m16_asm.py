@@ -42,11 +42,11 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     rng = np.random.default_rng(16)
     coef = rng.integers(0, 65536, 64, dtype=np.uint32)
     coef[:4] = [0, 1, 2, 0xFFFF]
-    rec = np.zeros(256, np.uint32)
+    rec = np.zeros(256, np.uint8)  # packed as rs_api.cpp:build_plan: byte 64n + p
     for n in range(4):
         rec[64 * n:64 * n + 64] = 16 * n + ((coef >> (4 * n)) & 15)
     mem = Memory(4096)
-    mem.b[1024:2048] = rec.astype("<u4").view(np.uint8)
+    mem.b[1024:1280] = rec
     x = rng.integers(0, 2 ** 32, 64, dtype=np.uint64).astype(np.uint32)
     acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
     text = "\n".join(step_lines(str(tmp_path)))
@@ -57,7 +57,7 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     w.v[203] = 0x002D002D
     w.v[72:136] = acc0
     w.s[90], w.s[91] = 1024, 0
-    w.run(text.splitlines(), [])
+    w.run(["s_load_dwordx16 s[40:55], s[90:91], 0x0"] + text.splitlines(), [])  # the kernel's first-plane load
     lo, hi = x & 0xFFFF, x >> 16
     for p in range(64):
         want = (gf_mul(lo, coef[p]) | (gf_mul(hi, coef[p]) << 16)) ^ acc0[p]

@@ -93,7 +93,9 @@ class Wave:
                 self.gpr_idx = None
                 continue
             if getattr(self, "gpr_idx", None) is not None and op.startswith("v_") and len(a) > 1:
-                a[1] = f"v{_vreg(a[1]) + self.gpr_idx}"
+                # only a VGPR src0 is offset; constants and SGPRs in src0 are not
+                if re.fullmatch(r"v\d+", a[1]):
+                    a[1] = f"v{_vreg(a[1]) + self.gpr_idx}"
             if op == "s_load_dwordx16":
                 m = re.match(r"s\[(\d+):(\d+)\]", a[0])
                 lo = int(m.group(1))
@@ -109,6 +111,8 @@ class Wave:
                 self.run(finish, finish)
             elif op == "s_mov_b32":
                 self.sset(a[0], self.val(a[1]))
+            elif op == "s_lshr_b32":
+                self.sset(a[0], self.val(a[1]) >> (self.val(a[2]) & 31))
             elif op == "s_and_b32":
                 self.sset(a[0], self.val(a[1]) & self.val(a[2]))
             elif op == "s_mul_i32":
@@ -133,6 +137,8 @@ class Wave:
                 self.vset(a[0], self.val(a[1]) ^ self.val(a[2]))
             elif op == "v_and_b32":
                 self.vset(a[0], np.uint32(self.val(a[1])) & self.val(a[2]))
+            elif op == "v_lshlrev_b32":
+                self.vset(a[0], (self.val(a[2]).astype(np.uint64) << np.uint64(self.val(a[1]) & 31)) & np.uint64(0xFFFFFFFF))
             elif op == "v_lshrrev_b32":
                 self.vset(a[0], self.val(a[2]) >> np.uint32(self.val(a[1])))
             elif op == "v_mul_u32_u24":
