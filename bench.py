@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="skip verification/CPU legs (profilers)")
+    ap.add_argument("--scatter", type=int, default=0, metavar="STRIPES",
+                    help="N>1: also time an RCCL scatter of STRIPES stripes per rank from rank 0 (and the gather of "
+                         "their repair symbols back), outside the timed region; reported as 'scatter'")
     return ap.parse_args()
 
 
@@ -183,6 +186,33 @@ def cpu_baseline(args, erased, gpu_sample):
                        f"passes, {threads} threads, {t_enc + t_dec:.1f} s"), parity
 
 
+# ------------------------------------------------------------------- stripes from one rank
+def scatter_leg(args, rank, world, dev):
+    """Stripes that originate on rank 0 (--scatter STRIPES per rank): RCCL scatter of the information
+    symbols to their owners (rs_dist.scatter_stripes, one P2P group, one xGMI link per peer) and the
+    gather of the repair symbols back. Timed on its own (barrier-bracketed, max over ranks); never
+    part of `value`."""
+    k, r, S, m = args.k, args.r, args.symbol, args.scatter
+    src = torch.empty((world * m if rank == 0 else 1, k, S), dtype=torch.uint8, device=dev)
+    if rank == 0:
+        src.random_(0, 256)
+    info = torch.empty((m, k, S), dtype=torch.uint8, device=dev)
+    rep = torch.randint(0, 256, (m, r, S), dtype=torch.uint8, device=dev)
+    back = torch.empty((world * m if rank == 0 else 1, r, S), dtype=torch.uint8, device=dev)
+    rs_dist.scatter_stripes(src, info)  # warm-up (communicator and P2P channel setup)
+    with rs_dist.TimedRegion(dev) as t_sc:
+        rs_dist.scatter_stripes(src, info)
+    with rs_dist.TimedRegion(dev) as t_ga:
+        rs_dist.gather_stripes(rep, back)
+    moved_sc = (world - 1) * m * k * S
+    moved_ga = (world - 1) * m * r * S
+    ok = rank != 0 or torch.equal(info, src[:m])
+    ok = rs_dist.max_over_ranks(0.0 if ok else 1.0, dev) == 0.0
+    return {"stripes_per_rank": m, "scatter_GBps": round(moved_sc / t_sc.max_elapsed / 1e9, 1),
+            "gather_GBps": round(moved_ga / t_ga.max_elapsed / 1e9, 1), "scatter_ms": round(t_sc.max_elapsed * 1e3, 3),
+            "gather_ms": round(t_ga.max_elapsed * 1e3, 3), "check": "ok" if ok else "MISMATCH"}
+
+
 # ------------------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -256,6 +286,8 @@ def main():
             gpu_sample = stripes[: args.cpu_stripes].cpu().numpy()
         parity = "roundtrip-ok" if ok else "ROUNDTRIP-MISMATCH"
 
+    scatter = scatter_leg(args, rank, world, dev) if args.scatter > 0 and world > 1 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.profile_only:
         cpu, cpu_ok = cpu_baseline(args, erased, gpu_sample)
@@ -289,6 +321,8 @@ def main():
         "cpu_baseline": cpu,
         "parity": parity,
     }
+    if scatter is not None:
+        line["scatter"] = scatter
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

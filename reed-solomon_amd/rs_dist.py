@@ -6,6 +6,12 @@ touches the data path. The only collectives are the barriers that bracket a time
 MAX reduction of the elapsed time (the job is as slow as its slowest rank), plus an optional XOR
 combination of per-stripe fingerprints for verification. Backend "nccl" (RCCL over xGMI) on GPUs,
 "gloo" for the CPU tests.
+
+When the stripes originate on one rank (shards arriving from a file or socket on one host process),
+`scatter_stripes` moves every rank's contiguous shard with one batch of point-to-point sends from
+the root -- RCCL runs the batch as one group, so each peer's shard travels on its own xGMI link --
+and `gather_stripes` brings results back the same way. bench.py times this separately (--scatter);
+it is never part of the device-resident number.
 """
 import os
 import time
@@ -86,3 +92,43 @@ def xor_over_ranks(fp):
     for p in parts[1:]:
         out ^= p
     return out
+
+
+def scatter_stripes(src, dst, root=0):
+    """Root's `src` [world * n, ...] -> every rank's `dst` [n, ...] (rank g gets rows [g*n, (g+1)*n)).
+    One batch of isend (root) / irecv (others); `src` is ignored on non-root ranks."""
+    if not _active():
+        dst.copy_(src[: dst.shape[0]])
+        return
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = dst.shape[0]
+    if rank == root:
+        ops = [dist.P2POp(dist.isend, src[g * n:(g + 1) * n].contiguous(), g) for g in range(world) if g != root]
+        reqs = dist.batch_isend_irecv(ops)
+        dst.copy_(src[root * n:(root + 1) * n])
+    else:
+        reqs = dist.batch_isend_irecv([dist.P2POp(dist.irecv, dst, root)])
+    for q in reqs:
+        q.wait()
+
+
+def gather_stripes(src, dst, root=0):
+    """Every rank's `src` [n, ...] -> root's `dst` [world * n, ...] (inverse of scatter_stripes)."""
+    if not _active():
+        dst[: src.shape[0]].copy_(src)
+        return
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = src.shape[0]
+    if rank == root:
+        views = {g: dst[g * n:(g + 1) * n] for g in range(world) if g != root}
+        bufs = {g: (v if v.is_contiguous() else torch.empty_like(v)) for g, v in views.items()}
+        reqs = dist.batch_isend_irecv([dist.P2POp(dist.irecv, bufs[g], g) for g in bufs])
+        dst[root * n:(root + 1) * n].copy_(src)
+        for q in reqs:
+            q.wait()
+        for g, b in bufs.items():
+            if b is not views[g]:
+                views[g].copy_(b)
+    else:
+        for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, src.contiguous(), root)]):
+            q.wait()

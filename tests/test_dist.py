@@ -92,3 +92,51 @@ def test_two_ranks_gloo():
     assert res[0][4] < res[1][4]
     assert all(abs(r[5] - res[1][4]) < 1e-9 for r in res), "TimedRegion must report the max over ranks"
     assert res[0][5] >= 0.3
+
+
+def _scatter_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = PER_RANK
+        src = torch.zeros((world * n, K + R, S), dtype=torch.uint8)
+        if rank == 0:  # the stripes originate on rank 0
+            for s in range(world * n):
+                src[s, :K] = torch.from_numpy(gen_info(SEED, s, K * S).reshape(K, S))
+        mine = torch.empty((n, K + R, S), dtype=torch.uint8)
+        rs_dist.scatter_stripes(src, mine, root=0)
+        first, _ = rs_dist.weak_shard(n, rank)
+        ok = all(np.array_equal(mine[i, :K].numpy(), gen_info(SEED, first + i, K * S).reshape(K, S))
+                 for i in range(n))
+        buf = mine.numpy()
+        for i in range(n):  # encode the shard, results go back to rank 0
+            assert oracle_encode(K, R, buf[i]) == 0
+        back = torch.zeros((world * n, K + R, S), dtype=torch.uint8)
+        rs_dist.gather_stripes(torch.from_numpy(buf), back, root=0)
+        q.put((rank, ok, back.numpy()[:, K:].tobytes() if rank == 0 else b""))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scatter_gather_from_rank0_gloo():
+    """Stripes that originate on rank 0 reach their owners (scatter_stripes), are encoded there and
+    the repair symbols come back to rank 0 (gather_stripes) equal to a single-process encode."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(g, 2, port, q)) for g in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = sorted((q.get(timeout=10) for _ in procs), key=lambda t: t[0])
+    assert all(r[1] for r in res), "a rank received the wrong shard"
+    want = []
+    for s in range(2 * PER_RANK):
+        buf = np.zeros((K + R, S), np.uint8)
+        buf[:K] = gen_info(SEED, s, K * S).reshape(K, S)
+        assert oracle_encode(K, R, buf) == 0
+        want.append(buf[K:])
+    assert res[0][2] == np.stack(want).tobytes()
