@@ -62,3 +62,47 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     for p in range(64):
         want = (gf_mul(lo, coef[p]) | (gf_mul(hi, coef[p]) << 16)) ^ acc0[p]
         assert np.array_equal(w.v[72 + p], want), p
+
+
+def gf256_mul_bytes(x, c):
+    """Each byte of the uint32 array x times c in GF(256) with gamma's minimal polynomial 0x11D."""
+    out = np.zeros_like(x)
+    for b in range(4):
+        v = (x >> np.uint32(8 * b)) & np.uint32(0xFF)
+        r = np.zeros_like(v)
+        cc = int(c)
+        for _ in range(8):
+            if cc & 1:
+                r ^= v
+            cc >>= 1
+            v = ((v << np.uint32(1)) ^ np.where(v & 0x80, 0x11D, 0).astype(np.uint32)) & np.uint32(0xFF)
+        out |= r << np.uint32(8 * b)
+    return out
+
+
+def test_m8_v1_step_matches_gf256_multiply(tmp_path):
+    """k_apply_m8_v1's input step (gen_asm.py variant v1): acc_p ^= c_p * y byte-wise in GF(256),
+    c_p from the (lo, hi) nibble record of rs_api.cpp:build_plan."""
+    out = os.path.join(str(tmp_path), "v1.inc")
+    subprocess.check_call([sys.executable, GEN, out, "v1"])
+    lines = [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(out) if ln.startswith('"')]
+    rng = np.random.default_rng(8)
+    coef = rng.integers(0, 256, 32, dtype=np.uint32)
+    coef[:3] = [0, 1, 255]
+    rec = np.zeros(64, np.uint32)
+    rec[:32], rec[32:] = coef & 15, coef >> 4
+    mem = Memory(4096)
+    mem.b[1024:1280] = rec.astype("<u4").view(np.uint8)
+    y = rng.integers(0, 2 ** 32, 64, dtype=np.uint64).astype(np.uint32)
+    acc0 = rng.integers(0, 2 ** 32, (32, 64), dtype=np.uint64).astype(np.uint32)
+    text = "\n".join(lines)
+    text = (text.replace("%[t0]", "v200").replace("%[t1]", "v201").replace("%[y0]", "v202")
+            .replace("%[k1d]", "v203").replace("%[cp]", "s[90:91]"))
+    w = Wave(mem, {})
+    w.v[202] = y
+    w.v[203] = 0x1D1D1D1D
+    w.v[40:72] = acc0
+    w.s[90], w.s[91] = 1024, 0
+    w.run(text.splitlines(), [])
+    for p in range(32):
+        assert np.array_equal(w.v[40 + p], gf256_mul_bytes(y, coef[p]) ^ acc0[p]), p

@@ -161,6 +161,14 @@ class Wave:
                 lo = ((x & 0xFFFF) + (y & 0xFFFF)) & 0xFFFF
                 hi = ((x >> 16) + (y >> 16)) & 0xFFFF
                 self.vset(a[0], lo | (hi << np.uint32(16)))
+            elif op == "v_pk_mul_lo_u16":
+                src1, mod = a[2].split()
+                assert mod == "op_sel_hi:[0,1]", ln  # src0's low half for both lanes
+                c = self.val(a[1]) & 0xFFFF
+                x = self.val(src1)
+                lo = ((x & 0xFFFF).astype(np.uint64) * c) & 0xFFFF
+                hi = ((x >> 16).astype(np.uint64) * c) & 0xFFFF
+                self.vset(a[0], (lo | (hi << np.uint64(16))).astype(np.uint32))
             elif op == "v_pk_ashrrev_i16":
                 src, mod = a[2].split()
                 assert mod == "op_sel_hi:[0,1]", ln  # shift count from the low half for both lanes
