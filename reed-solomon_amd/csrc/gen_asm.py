@@ -142,10 +142,11 @@ if variant in ("m16_v1", "m16_v1_plain"):
     #   T_n v[8 + 16n : 23 + 16n]  nibble table n: entry e = XOR of x * alpha^(4n + b) over the set bits b
     #   acc v[72:135]               output p in v[72 + p]
     #   s[40:55] / s[56:71]         two 16-dword buffers, one nibble plane of the record each;
-    #   s72 scratch, s73 = 0xFFFEFFFE
-    # Record of (tile, input): 64 dwords, byte 64n + p = 16n + nibble n of output p, so every lookup
-    # indexes from v8; s_set_gpr_idx_idx takes bits [7:0] of its operand, the other bytes come down
-    # with one s_lshr_b32. Plane n + 1 (or the next input's plane 0: the record array is padded by one
+    #   s[72:73] scratch pair, s74 = 0xFFFEFFFE
+    # Record of (tile, input): 64 dwords, 16 per plane; lookup l of plane n (output l) takes its index
+    # 16n + nibble n from byte (l % 8) // 2 of plane dword 2 (l // 8) + l % 2, so every lookup indexes
+    # from v8; s_set_gpr_idx_idx takes bits [7:0] of its operand, and one s_lshr_b64 of a dword pair
+    # brings the next byte of both dwords down (3 shifts per 8 lookups). Plane n + 1 (or the next input's plane 0: the record array is padded by one
     # input) loads while plane n is consumed; this input's plane 0 was requested by the previous step
     # (or by the kernel before the first one) and arrives in s[40:55].
     # Plane n reads only table T_n, so T_(n+1) is built while plane n's lookups run. In gpr-index mode
@@ -159,7 +160,7 @@ if variant in ("m16_v1", "m16_v1_plain"):
     def xt(j):  # multiple j from multiple j - 1
         src, dst = mreg(j - 1), mreg(j)
         return [f"v_lshrrev_b32 {ta}, 15, v{src}", f"v_and_b32 {ta}, 0x10001, {ta}", f"v_mul_u32_u24 {ta}, 45, {ta}",
-                f"v_lshlrev_b32 {tb}, 1, v{src}", f"v_bitop3_b32 v{dst}, s73, {tb}, {ta} bitop3:0x6a"]
+                f"v_lshlrev_b32 {tb}, 1, v{src}", f"v_bitop3_b32 v{dst}, s74, {tb}, {ta} bitop3:0x6a"]
 
     def tab(b):
         ops = [f"v_mov_b32 v{b}, 0"]
@@ -173,7 +174,7 @@ if variant in ("m16_v1", "m16_v1_plain"):
             ops += xt(j)
         return ops + tab(T + 16 * n)
 
-    e("s_mov_b32 s73, 0xfffefffe")
+    e("s_mov_b32 s74, 0xfffefffe")
     L.extend(build(0))
     idx = variant == "m16_v1"
     for n in range(4):
@@ -182,14 +183,18 @@ if variant in ("m16_v1", "m16_v1_plain"):
         e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (n + 1))}")
         look = []
         for l in range(64):
-            w, b = divmod(l, 4)
+            # lookup l of the plane: dword pair m = l // 8 of the buffer, byte b = (l % 8) // 2 of dword
+            # 2m + (l % 2); one s_lshr_b64 of the pair brings byte b of both dwords down to bits [7:0]
+            m, r8 = divmod(l, 8)
+            b, h = divmod(r8, 2)
             grp = []
             if idx:
                 if b == 0:
-                    sreg = f"s{buf + w}"
+                    sreg = f"s{buf + 2 * m + h}"
                 else:
-                    grp.append(f"s_lshr_b32 s72, s{buf + w}, {8 * b}")
-                    sreg = "s72"
+                    if h == 0:
+                        grp.append(f"s_lshr_b64 s[72:73], s[{buf + 2 * m}:{buf + 2 * m + 1}], {8 * b}")
+                    sreg = f"s{72 + h}"
                 grp.append(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if n == 0 and l == 0 else f"s_set_gpr_idx_idx {sreg}")
             src = T if idx else T + 16 * n + (l * 7 + 3) % 16
             grp.append(f"v_xor_b32 v{ACC + l}, v{src}, v{ACC + l}")

@@ -199,8 +199,9 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
                 }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
     } else if (rt == 64 && size_t(p->ntiles) * (K + 1) * 256 <= (size_t(256) << 20)) {
-        // k_apply_m16_v1: per (tile, input) 256 byte-sized table indices packed in 64 dwords, byte
-        // 64n + j = 16n + nibble n of output j's coefficient; one padding record per tile. (One index
+        // k_apply_m16_v1: per (tile, input) 256 byte-sized table indices packed in 64 dwords (16 per
+        // nibble plane n; output j's index 16n + nibble n in byte (j % 8) / 2 of the plane's dword
+        // 2 (j / 8) + j % 2, the order the kernel's s_lshr_b64 extraction walks); one padding record. (One index
         // per dword would save the kernel's byte shifts but quadruples the record stream: measured
         // 13.4 vs 23.6 GB/s at C5.)
         std::vector<uint32_t> idx(size_t(p->ntiles) * (K + 1) * 64, 0);
@@ -208,10 +209,11 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
             for (int i = 0; i < K; ++i) {
                 uint8_t* rec = reinterpret_cast<uint8_t*>(idx.data() + (size_t(t) * (K + 1) + i) * 64);
                 for (int n = 0; n < 4; ++n)
-                    for (int j = 0; j < 64; ++j) {
+                    for (int j = 0; j < 64; ++j) {  // plane dword 2 (j / 8) + j % 2, byte (j % 8) / 2
                         const int row = t * 64 + j;
                         const uint32_t c = row < R ? M[size_t(row) * K + i] : 0;
-                        rec[64 * n + j] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
+                        const int dw = 16 * n + 2 * (j / 8) + (j % 2), by = (j % 8) / 2;
+                        rec[4 * dw + by] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
                     }
             }
         if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;

@@ -500,7 +500,7 @@ __device__ __forceinline__ void m16_v1_step(uint32_t y, const uint32_t* cp, u32x
       "+{s[40:55]}"(plane)                                                                                       \
     : [y0] "v"(y), [cp] "s"(cp), [k2d] "v"(k2d)                                                                 \
     : "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
-      "s72", "s73"
+      "s72", "s73", "s74"
     if constexpr (ABL == 0) {
         asm volatile(
 #include "gen/m8_idx_asm_m16_v1.inc"

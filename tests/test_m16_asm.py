@@ -42,9 +42,10 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     rng = np.random.default_rng(16)
     coef = rng.integers(0, 65536, 64, dtype=np.uint32)
     coef[:4] = [0, 1, 2, 0xFFFF]
-    rec = np.zeros(256, np.uint8)  # packed as rs_api.cpp:build_plan: byte 64n + p
+    rec = np.zeros(256, np.uint8)  # packed as rs_api.cpp:build_plan
     for n in range(4):
-        rec[64 * n:64 * n + 64] = 16 * n + ((coef >> (4 * n)) & 15)
+        for j in range(64):
+            rec[4 * (16 * n + 2 * (j // 8) + j % 2) + (j % 8) // 2] = 16 * n + ((coef[j] >> (4 * n)) & 15)
     mem = Memory(4096)
     mem.b[1024:1280] = rec
     x = rng.integers(0, 2 ** 32, 64, dtype=np.uint64).astype(np.uint32)
