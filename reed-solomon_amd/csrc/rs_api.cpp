@@ -256,8 +256,13 @@ struct rsg_codec {
     uint16_t* d_elem = nullptr;  // [k + r] slot elements alpha^position
     void *d_masks = nullptr, *d_kr = nullptr, *d_pin = nullptr, *d_pout = nullptr, *d_pidx = nullptr;
     size_t masks_cap = 0, kr_cap = 0, pin_cap = 0, pout_cap = 0, pidx_cap = 0;
+    // the scratch above is reused by every rsg_decode_batch call: the event marks the end of the last
+    // call's launches (which may be on another stream) and is waited for before the next overwrite
+    hipEvent_t scratch_ev = nullptr;
+    bool scratch_pending = false;
     ~rsg_codec() {
         (void)hipSetDevice(device);
+        if (scratch_ev) (void)hipEventDestroy(scratch_ev);
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx})
             if (p) (void)hipFree(p);
     }
@@ -506,6 +511,19 @@ extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, u
                     int64_t(symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
 }
 
+// rsg_decode_batch scratch: wait until the previous call's launches are done with it / mark this one's
+static int scratch_acquire(rsg_codec_t* c) {
+    if (c->scratch_pending) HIP_TRY(hipEventSynchronize(c->scratch_ev));
+    c->scratch_pending = false;
+    return 0;
+}
+static int scratch_release(rsg_codec_t* c, hipStream_t st) {
+    if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->scratch_ev, st));
+    c->scratch_pending = true;
+    return 0;
+}
+
 // Distinct patterns beyond which rsg_decode_batch builds the decode matrices on the device (the
 // host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
 constexpr size_t kHostPlanGroups = 16;
@@ -529,9 +547,11 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
         for (size_t i = 0; i < n; ++i) masks.push_back(e[i] ? 1 : 0);
     }
     if (ids.empty()) return 0;
+    int rc = scratch_acquire(c);
+    if (rc) return rc;
     const uint16_t* logt = nullptr;
     const uint8_t* g8 = nullptr;
-    int rc = plan_tables(c->device, &logt, &g8);
+    rc = plan_tables(c->device, &logt, &g8);
     if (rc) return rc;
     if (!c->d_elem) {
         const Field& F = field();
@@ -594,7 +614,7 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
         HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
     }
     c->last_kernel = "apply_m8_v1_ps";
-    return 0;
+    return scratch_release(c, st);
 }
 
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
@@ -629,6 +649,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         first.push_back(ids.size());
         ids.insert(ids.end(), g.second.begin(), g.second.end());
     }
+    if (int rc = scratch_acquire(c)) return rc;
     if (ids.size() > c->ids_cap) {
         if (c->d_ids) (void)hipFree(c->d_ids);
         c->d_ids = nullptr;
@@ -653,7 +674,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         if (rc) return rc;
         ++gi;
     }
-    return 0;
+    return scratch_release(c, st);
 }
 
 extern "C" int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size,

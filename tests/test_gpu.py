@@ -347,3 +347,36 @@ def test_m16_kernels_vs_oracle(S, mode):
         assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
         assert np.array_equal(out[s], ref)
         assert np.array_equal(out[s, :k], got[s, :k])
+
+
+@pytest.mark.parametrize("plans", [0, 1])
+def test_decode_batch_back_to_back_streams(plans):
+    """Two rsg_decode_batch calls issued back to back on different streams (the second call reuses
+    the codec's device scratch while the first may still run): both batches restore bit-exactly."""
+    k, r, S, n = 128, 32, 8192, 48
+    rng = np.random.default_rng(33 + plans)
+    codec = rs_amd.Codec(k, r, batch_plans=plans)
+    bufs, fulls, pats = [], [], []
+    for b in range(2):
+        dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+        rs_amd.fill_info(dev, k, seed=0x51 + b)
+        codec.encode(dev)
+        torch.cuda.synchronize()
+        full = dev.cpu().numpy()
+        pat = np.zeros((n, k + r), bool)
+        for s in range(n):
+            pat[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+        poisoned = full.copy()
+        poisoned[pat] = 0
+        dev.copy_(torch.from_numpy(poisoned))
+        bufs.append(dev)
+        fulls.append(full)
+        pats.append(pat)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for b in range(2):
+        assert codec.decode_batch(bufs[b], pats[b], stream=streams[b]) == 0
+    torch.cuda.synchronize()
+    for b in range(2):
+        got = bufs[b].cpu().numpy()
+        assert np.array_equal(got[:, :k], fulls[b][:, :k]), f"batch {b}"
