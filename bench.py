@@ -30,20 +30,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "reed-solomon_amd"))
 import rs_amd  # noqa: E402  (raises if librs_amd.so is missing: no fallback)
 import rs_dist  # noqa: E402
+from srchash import kernel_src_hash  # noqa: E402
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")  # scripts/traffic.py output
-
-
-def kernel_src_hash():
-    """Identifies the kernel build a traffic measurement belongs to (hash of the kernel sources)."""
-    import hashlib
-    h = hashlib.sha256()
-    for f in ("csrc/rs_kernels.hip", "csrc/gen_asm.py", "csrc/rs_device.h", "csrc/rs_xj.cpp"):
-        with open(os.path.join(REPO, "reed-solomon_amd", f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
 
 
 def measured_traffic(kernel, cfg):
@@ -55,7 +46,7 @@ def measured_traffic(kernel, cfg):
     except (OSError, ValueError):
         return None
     family = lambda name: str(name).split("[")[0]  # specialised kernels carry a matrix hash suffix
-    if family(t.get("bench_kernel")) != family(kernel) or t.get("config") != cfg or t.get("src_hash") != kernel_src_hash():
+    if family(t.get("bench_kernel")) != family(kernel) or t.get("config") != cfg or t.get("src_hash") != kernel_src_hash(kernel):
         return None
     return int(t["traffic_bytes"])
 SEED = 0x5EED

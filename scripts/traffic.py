@@ -31,12 +31,9 @@ write = per_dispatch(wd, "WRITE_SIZE", kern)
 med = lambda v: v[len(v) // 2]
 fetch_b = med(fetch) * 1024 * 2
 write_b = med(write) * 1024
-import hashlib
-h = hashlib.sha256()
-for f in ("csrc/rs_kernels.hip", "csrc/gen_asm.py", "csrc/rs_device.h", "csrc/rs_xj.cpp"):
-    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd", f), "rb") as fh:
-        h.update(fh.read())
-print(json.dumps({"src_hash": h.hexdigest()[:16], "kernel": kern, "bench_kernel": bench_kernel, "config": cfg,
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd"))
+from srchash import kernel_src_hash  # noqa: E402
+print(json.dumps({"src_hash": kernel_src_hash(bench_kernel), "kernel": kern, "bench_kernel": bench_kernel, "config": cfg,
                   "fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
                   "dispatches": [len(fetch), len(write)],
                   "raw_kib": {"FETCH_SIZE": med(fetch), "WRITE_SIZE": med(write)}}, indent=1))
