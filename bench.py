@@ -129,11 +129,11 @@ def cpu_baseline(args, erased, gpu_sample):
                     errs.append(lib.rs_restore_symbols(rs, k, r, ctypes.byref(rcv), er.ctypes.data, t))
             lib.rs_destroy(rs)
 
-        def run(dec):
-            nt = min(args.cpu_threads, n)
+        def run(dec, nt=None, cnt=n):
+            nt = min(args.cpu_threads if nt is None else nt, cnt)
             errs, ths = [], []
             for i in range(nt):
-                th = threading.Thread(target=work, args=(n * i // nt, n * (i + 1) // nt, dec, errs))
+                th = threading.Thread(target=work, args=(cnt * i // nt, cnt * (i + 1) // nt, dec, errs))
                 ths.append(th)
             t0 = time.perf_counter()
             for th in ths:
@@ -147,12 +147,13 @@ def cpu_baseline(args, erased, gpu_sample):
         o = oracle()
         er = np.ascontiguousarray(erased, np.bool_)
 
-        def run(dec):
+        def run(dec, nt=None, cnt=n):
+            nt = args.cpu_threads if nt is None else nt
             t0 = time.perf_counter()
             if dec:
-                rc = o.orc_decode_many(k, r, S, stripes.ctypes.data, n, er.ctypes.data, t, args.cpu_threads)
+                rc = o.orc_decode_many(k, r, S, stripes.ctypes.data, cnt, er.ctypes.data, t, nt)
             else:
-                rc = o.orc_encode_many(k, r, S, stripes.ctypes.data, n, args.cpu_threads)
+                rc = o.orc_encode_many(k, r, S, stripes.ctypes.data, cnt, nt)
             assert rc == 0
             return time.perf_counter() - t0
 
@@ -172,9 +173,16 @@ def cpu_baseline(args, erased, gpu_sample):
     bytes_total = n * ((k + r) * p_enc + (k + t) * p_dec) * S
     gbs = bytes_total / (t_enc + t_dec) / 1e9
     threads = min(args.cpu_threads, n)
-    return dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind,
+    # single core, same code, a few stripes (all-core and single-core rates)
+    c1 = min(n, 4)
+    t1e, t1d = run(False, 1, c1), 0.0
+    stripes[:c1, erased] = 0
+    t1d = run(True, 1, c1)
+    gbs1 = c1 * ((k + r) + (k + t)) * S / (t1e + t1d) / 1e9
+    return dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind, single_core=round(gbs1, 4),
                 sample=f"{n} resident stripes of k={k} r={r} S={S}: {p_enc} encode + {p_dec} decode (t={t}) "
-                       f"passes, {threads} threads, {t_enc + t_dec:.1f} s"), parity
+                       f"passes, {threads} threads, {t_enc + t_dec:.1f} s; single_core: {c1} stripes, "
+                       f"1 thread, {t1e + t1d:.1f} s"), parity
 
 
 # ------------------------------------------------------------------- stripes from one rank
