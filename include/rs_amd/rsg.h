@@ -41,7 +41,9 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
  * before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
  * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
- * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default).
+ * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default), "m16_mode"
+ * (GF(2^16) codes: 0 = hand-scheduled gpr-index kernel for more than 32 outputs, the default; 1 = its
+ * timing ablation; 2 = the compiled kernel).
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
