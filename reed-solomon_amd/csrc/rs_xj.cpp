@@ -126,7 +126,7 @@ const XjBasis& xj_basis(int horner) {
 }
 
 bool xj_supported(int m, int K, int R) {
-    return m <= 8 && K >= 1 && R >= 1 && R <= xj_outputs_per_role() * kXjMaxRoles && K * R <= kXjMaxWork;
+    return m <= 8 && K >= 1 && R >= 1 && xj_roles(R) <= xj_max_roles(R) && K * R <= kXjMaxWork;
 }
 
 // --------------------------------------------------------------------------- code generator
@@ -663,15 +663,18 @@ int xj_roles(int R) {
 }
 int xj_horner() { return XjConfig().horner; }
 int xj_fin() { return XjConfig().lfin; }
+int xj_max_roles(int R) {
+    // all role waves of a column are one workgroup, so they must fit one CU at the layout's VGPR
+    // footprint (fixed map + the compiler's column register, 8-register granules): 12 at 16 outputs
+    const XjConfig C(R);
+    const int vgprs = (C.max_vgpr() + 2 + 7) / 8 * 8;
+    return std::min(kXjMaxRoles, 4 * std::max(1, std::min(8, 512 / vgprs)));
+}
 int xj_pairs(int R) {
     if (!XjConfig(R).lfin) return 1;
     // column pairs per persistent workgroup: every wave slot of the CU (the 128 KiB table allows one
     // workgroup per CU); VGPRs per wave = the fixed map + the compiler's column / loop registers
-    const XjConfig C(R);
-    const int vgprs = (C.max_vgpr() + 2 + 7) / 8 * 8;
-    const int waves_per_simd = std::max(1, std::min(8, 512 / vgprs));
-    const int roles = xj_roles(R);
-    return std::max(1, std::min(16 / roles, 4 * waves_per_simd / roles));
+    return std::max(1, xj_max_roles(R) / xj_roles(R));
 }
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,

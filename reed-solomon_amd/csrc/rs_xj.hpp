@@ -72,6 +72,7 @@ int xj_horner();  // generation setting (RS_XJ_HORNER, default 0)
 bool xj_supported(int m, int K, int R);
 int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 16)
 int xj_roles(int R);         // waves per column for R outputs
+int xj_max_roles(int R);     // role waves that fit one CU at the layout's VGPR footprint
 int xj_fin();                // generation setting (RS_XJ_FIN, default 0)
 int xj_pairs(int R);         // columns per workgroup (1 unless the LDS-table finish is on)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
