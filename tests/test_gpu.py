@@ -426,3 +426,38 @@ def test_xor_kernel_shapes_vs_oracle(k, r):
         ref = poisoned[s].copy()
         assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
         assert np.array_equal(out[s], ref), f"stripe {s}"
+
+
+@pytest.mark.parametrize("k,r,S", [(250, 33, 1024), (300, 64, 2048 + 40), (200, 65, 1024 + 1000), (1000, 100, 2048),
+                                   (400, 129, 3072 + 4)])
+def test_m16_kernel_shapes_vs_oracle(k, r, S):
+    """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
+    1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle."""
+    rng = np.random.default_rng(k + 7 * r + S)
+    n = 2
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    assert codec.subfield == 16
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    assert codec.last_kernel == "apply_m16_v1"
+    got = dev.cpu().numpy()
+    want = host.copy()
+    for s in range(n):
+        assert oracle_encode(k, r, want[s]) == 0
+    assert np.array_equal(got, want)
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k, min(k, r), replace=False)] = True  # r information erasures: the largest decode
+    poisoned = got.copy()
+    poisoned[:, er] = 0
+    dev.copy_(torch.from_numpy(poisoned))
+    codec.decode(dev, er)
+    torch.cuda.synchronize()
+    out = dev.cpu().numpy()
+    assert np.array_equal(out[:, :k], got[:, :k])
+    for s in range(n):
+        ref = poisoned[s].copy()
+        assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
+        assert np.array_equal(out[s], ref)
