@@ -256,6 +256,8 @@ struct rsg_codec {
     uint16_t* d_elem = nullptr;  // [k + r] slot elements alpha^position
     void *d_masks = nullptr, *d_kr = nullptr, *d_pin = nullptr, *d_pout = nullptr, *d_pidx = nullptr;
     size_t masks_cap = 0, kr_cap = 0, pin_cap = 0, pout_cap = 0, pidx_cap = 0;
+    void* d_partial = nullptr;  // split-K partial products of small m = 16 launches
+    size_t partial_cap = 0;
     // the scratch above is reused by every rsg_decode_batch call: the event marks the end of the last
     // call's launches (which may be on another stream) and is waited for before the next overwrite
     hipEvent_t scratch_ev = nullptr;
@@ -263,7 +265,8 @@ struct rsg_codec {
     ~rsg_codec() {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
-        for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx})
+        for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
+                        d_partial})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -370,6 +373,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
 
 extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->last_kernel.c_str() : "none"; }
 
+static int scratch_acquire(rsg_codec_t* c);
+static int scratch_release(rsg_codec_t* c, hipStream_t st);
+
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
                     const int32_t* d_ids = nullptr) {
@@ -425,6 +431,15 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
+    if (p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) {  // split-K scratch for small m = 16 grids
+        int64_t need = 0;
+        if (m16_kslices(a, int64_t(n_stripes), &need) > 1) {
+            if (int rc = scratch_acquire(c)) return rc;
+            if (int rc = grow(&c->d_partial, c->partial_cap, size_t(need))) return rc;
+            a.scratch = static_cast<uint32_t*>(c->d_partial);
+            a.scratch_bytes = int64_t(c->partial_cap);
+        }
+    }
     const int nt32 = (p.R + 31) / 32;
     if (xj_ok && p.xj) {
         XJArgs x{};
@@ -460,6 +475,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
                      : (rt == 64 && p.d_idx && a.mode < 2) ? std::string(a.mode ? "apply_m16_v1_plain" : "apply_m16_v1")
                                                              : (std::string("apply_m16_rt") + std::to_string(rt));
     HIP_TRY(launch_apply(p.m, rt, a, int64_t(n_stripes), st));
+    if (a.scratch) return scratch_release(c, st);  // split-K partials in flight on st
     return 0;
 }
 

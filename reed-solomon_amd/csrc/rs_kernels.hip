@@ -521,12 +521,15 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     const int64_t stripe = RS_STRIPE(a.ids, local);
     const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
     const int tile = blockIdx.y;
-    const int K = a.K;
+    const int slice = blockIdx.z;
+    // split-K: this workgroup takes inputs [i0, i0 + K) of the full list
+    const int i0 = a.kslices > 1 ? int(int64_t(a.K) * slice / a.kslices) : 0;
+    const int K = a.kslices > 1 ? int(int64_t(a.K) * (slice + 1) / a.kslices) - i0 : a.K;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
     const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
-    const int32_t* in_idx = a.in_idx;
+    const int32_t* in_idx = a.in_idx + i0;
     auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
     const int nb = (K + 3) / 4;
     auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
@@ -552,7 +555,7 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     asm volatile("s_barrier" ::: "memory");
     // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
     // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
-    const uint32_t* rec = a.idx + size_t(tile) * (K + 1) * 64;
+    const uint32_t* rec = a.idx + (size_t(tile) * (a.K + 1) + i0) * 64;
     u32x16 plane;  // plane 0 of the next step's record, requested one step ahead (s[40:55] in the asm)
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");
     for (int b = 0; b < nb; ++b) {
@@ -569,8 +572,16 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
     }
-    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
     const int rows = min(64, a.R - tile * 64);
+    if (a.kslices > 1) {  // partial products: [slice][stripe][tile * 64 + p][chunk dwords]
+        const int64_t nloc = gridDim.x / a.nchunks, rpad = int64_t(gridDim.y) * 64, cw = a.nchunks * 256;
+        uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 64) * cw + (chunk0 >> 2) + threadIdx.x;
+#pragma unroll
+        for (int p = 0; p < 64; ++p)
+            if (p < rows) part[p * cw] = p < 16 ? a0[p & 15] : p < 32 ? a1[p & 15] : p < 48 ? a2[p & 15] : a3[p & 15];
+        return;
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
 #pragma unroll
     for (int p = 0; p < 64; ++p) {
         if (p < rows) {
@@ -578,6 +589,19 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
             *reinterpret_cast<uint32_t*>(dst + int64_t(sload(a.out_idx + tile * 64 + p)) * a.dst_sym) = v;
         }
     }
+}
+
+// Split-K reduction: output row `row` of launch-local stripe blockIdx.y, dwords [0, cw) of the full
+// 1 KiB chunks = XOR of the kslices partials.
+__global__ void __launch_bounds__(256) k_xor_slices(V1Args a, int64_t nloc, int64_t rpad, int64_t cw) {
+    const int64_t local = blockIdx.y;
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;  // row * cw + dword
+    if (e >= int64_t(a.R) * cw) return;
+    const int64_t row = e / cw, c = e - row * cw;
+    uint32_t v = 0;
+    for (int sl = 0; sl < a.kslices; ++sl) v ^= a.partial[((sl * nloc + local) * rpad + row) * cw + c];
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    *reinterpret_cast<uint32_t*>(a.dst + stripe * a.dst_stripe + int64_t(a.out_idx[row]) * a.dst_sym + 4 * c) = v;
 }
 
 // ------------------------------------------------------------------------ synthetic inputs
@@ -718,12 +742,19 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
         const int64_t full = a.nbytes / 1024;
         const unsigned tiles = unsigned((a.R + 63) / 64);
         if (full > 0) {
-            const V1Args v = v1_args(a, full, nullptr);
-            dim3 g(unsigned(n_stripes * full), tiles);
+            V1Args v = v1_args(a, full, nullptr);
+            v.kslices = m16_kslices(a, n_stripes, nullptr);
+            v.partial = a.scratch;
+            dim3 g(unsigned(n_stripes * full), tiles, unsigned(v.kslices));
             if (a.mode == 0)
                 hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
             else
                 hipLaunchKernelGGL((k_apply_m16_v1<1>), g, dim3(256), 0, st, v);
+            if (v.kslices > 1) {
+                const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
+                hipLaunchKernelGGL(k_xor_slices, dim3(unsigned((rows + 255) / 256), unsigned(n_stripes)), dim3(256), 0,
+                                   st, v, int64_t(n_stripes), int64_t(tiles) * 64, cw);
+            }
         }
         if (a.nbytes % 1024) {
             ApplyArgs t = a;
@@ -736,6 +767,20 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
     hipLaunchKernelGGL(k_apply_m16<RT>, grid, dim3(256), 0, st, a);
     return hipGetLastError();
+}
+
+int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes) {
+    // split K when the grid would leave most CUs idle (one workgroup walks all K inputs serially):
+    // aim for >= 512 workgroups, slices of >= 64 inputs, at most 32 slices, within the scratch
+    const int64_t full = a.nbytes / 1024, tiles = (a.R + 63) / 64;
+    const int64_t blocks = n_stripes * full * tiles;
+    if (blocks <= 0 || blocks >= 256) return 1;
+    int64_t s = std::min<int64_t>({(512 + blocks - 1) / blocks, int64_t(a.K) / 64, 32});
+    const int64_t per = n_stripes * tiles * 64 * full * 1024;  // partial bytes per slice
+    if (!scratch_bytes) s = std::min<int64_t>(s, per > 0 ? a.scratch_bytes / per : 0);
+    if (s < 2) return 1;
+    if (scratch_bytes) *scratch_bytes = s * per;
+    return int(s);
 }
 
 int apply_tile_rows(int m, int R) {

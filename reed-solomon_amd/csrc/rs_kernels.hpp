@@ -29,7 +29,11 @@ struct ApplyArgs {
                              //   1 = SGPR-masked multiples, 2 = hand-scheduled gpr-index block (RT=32)
     uint64_t* stamps;        // mode 17 (instrumented): [blocks * 4 waves][4] phase cycle counters
     const int32_t* ids;      // optional [n_stripes] stripe indices (per-stripe erasure patterns); null = 0..n-1
+    uint32_t* scratch;       // m = 16 split-K partials (codec-owned), scratch_bytes long; may be null
+    int64_t scratch_bytes;
 };
+// input slices of the split-K m = 16 launch over n_stripes (1 = no split) and the scratch it needs
+int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes);
 
 // Per-stripe decode plans (k_plan_m8): one per selected stripe, from its erasure mask.
 struct PlanArgs {

@@ -24,6 +24,11 @@ struct V1Args {
     // s * ps_in / ps_out / ps_idx elements. Null = one plan for every stripe (K, R above).
     const int32_t* ps_kr;
     int64_t ps_in, ps_out, ps_idx;
+    // split-K (k_apply_m16_v1 on small grids): blockIdx.z = input slice of kslices; each slice XORs
+    // its partial products into partial[slice][stripe][tile * 64 + row][chunk dwords], which
+    // k_xor_slices reduces into the outputs. kslices <= 1: direct stores.
+    int32_t kslices;
+    uint32_t* partial;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -429,10 +429,11 @@ def test_xor_kernel_shapes_vs_oracle(k, r):
 
 
 @pytest.mark.parametrize("k,r,S", [(250, 33, 1024), (300, 64, 2048 + 40), (200, 65, 1024 + 1000), (1000, 100, 2048),
-                                   (400, 129, 3072 + 4)])
+                                   (400, 129, 3072 + 4), (2000, 100, 1024)])
 def test_m16_kernel_shapes_vs_oracle(k, r, S):
     """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
-    1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle."""
+    1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle. Two
+    stripes make small grids, so every case also runs split-K (k=2000: 31 input slices)."""
     rng = np.random.default_rng(k + 7 * r + S)
     n = 2
     host = np.zeros((n, k + r, S), np.uint8)
