@@ -43,7 +43,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
  * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default), "m16_mode"
  * (GF(2^16) codes: 0 = hand-scheduled gpr-index kernel for more than 32 outputs, the default; 1 = its
- * timing ablation; 2 = the compiled kernel).
+ * timing ablation; 2 = the compiled kernel), "m16_plans" (GF(2^16) coding matrices: 0 = built on the
+ * host, 1 = on the device, 2 = on the device from 64K coefficients, the default; rebuilds the encode plan).
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */

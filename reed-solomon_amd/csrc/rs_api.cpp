@@ -50,7 +50,8 @@ namespace {
 
 struct DeviceTables {
     uint32_t* d_ltab = nullptr;  // 2048 dwords, see ApplyArgs::ltab
-    uint16_t* d_log = nullptr;   // [65536] discrete log (per-stripe decode plans)
+    uint16_t* d_log = nullptr;   // [65536] discrete log (device-built plans)
+    uint16_t* d_exp = nullptr;   // [65536] alpha^i (entry 65535 = 1)
     uint8_t* d_g8 = nullptr;     // [256] gamma-basis byte of alpha^(257 e), e < 255
 };
 
@@ -83,7 +84,7 @@ int device_tables(int device, const uint32_t** out) {
 }
 
 // log / gamma-byte tables of the device plan builder (k_plan_m8)
-int plan_tables(int device, const uint16_t** logt, const uint8_t** g8) {
+int plan_tables(int device, const uint16_t** logt, const uint8_t** g8, const uint16_t** expt = nullptr) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     DeviceTables& t = g_dev[device];
     if (!t.d_log) {
@@ -91,17 +92,24 @@ int plan_tables(int device, const uint16_t** logt, const uint8_t** g8) {
         const Gamma8& g = gamma8();
         std::vector<uint8_t> gb(256, 0);
         for (uint32_t e = 0; e < 255; ++e) gb[e] = g.coord(F.exp[257u * e]);
+        std::vector<uint16_t> ex(65536);
+        for (uint32_t e = 0; e < 65536; ++e) ex[e] = F.exp[e % kN];
         void* pl = nullptr;
+        void* pe = nullptr;
         void* pg = nullptr;
         HIP_TRY(hipMalloc(&pl, 65536 * 2));
         HIP_TRY(hipMemcpy(pl, F.log, 65536 * 2, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&pe, 65536 * 2));
+        HIP_TRY(hipMemcpy(pe, ex.data(), 65536 * 2, hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&pg, 256));
         HIP_TRY(hipMemcpy(pg, gb.data(), 256, hipMemcpyHostToDevice));
         t.d_log = static_cast<uint16_t*>(pl);
+        t.d_exp = static_cast<uint16_t*>(pe);
         t.d_g8 = static_cast<uint8_t*>(pg);
     }
     *logt = t.d_log;
     *g8 = t.d_g8;
+    if (expt) *expt = t.d_exp;
     return 0;
 }
 
@@ -233,6 +241,77 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
 }  // namespace
 
 // ============================================================================ codec
+// m = 16 plan built on the device (k_plan16_*): same kernels' formats as build_plan, from the target
+// / source position lists instead of a host matrix (a C5 decode plan is 4M coefficients and 16 MiB of
+// index records: tens of ms on the host, well under one on the GPU). Synchronous, like build_plan.
+int build_plan_m16_device(int device, const std::vector<uint16_t>& targets, const std::vector<int>& emit,
+                          const std::vector<uint16_t>& sources, std::vector<int32_t> in_slots,
+                          std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out) {
+    const Field& F = field();
+    const int K = int(sources.size()), R = int(emit.size()), d = int(targets.size());
+    auto p = std::make_unique<DevPlan>();
+    p->device = device;
+    p->m = 16;
+    p->K = K;
+    p->R = R;
+    p->rt = apply_tile_rows(16, std::max(R, 1));
+    p->ntiles = (R + p->rt - 1) / p->rt;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    int rc = plan_tables(device, &logt, &g8, &expt);
+    if (rc) return rc;
+    const size_t coef_bytes = size_t(p->ntiles) * K * (p->rt / 2) * 4;
+    const size_t rec_bytes = size_t(p->ntiles) * (K + 1) * 256;
+    const bool records = p->rt == 64 && rec_bytes <= (size_t(256) << 20);
+    std::vector<uint16_t> y(static_cast<size_t>(K)), x(static_cast<size_t>(d));
+    for (int q = 0; q < K; ++q) y[size_t(q)] = F.exp[sources[size_t(q)]];
+    for (int e = 0; e < d; ++e) x[size_t(e)] = F.exp[targets[size_t(e)]];
+    void *d_y = nullptr, *d_x = nullptr, *d_emit = nullptr, *d_lp = nullptr, *d_ld = nullptr;
+    struct Tmp {  // temporaries of the build, freed on every return
+        void** v[5];
+        ~Tmp() {
+            for (void** q : v)
+                if (*q) (void)hipFree(*q);
+        }
+    } tmp{{&d_y, &d_x, &d_emit, &d_lp, &d_ld}};
+    if ((rc = upload(&d_y, y.data(), y.size() * 2)) || (rc = upload(&d_x, x.data(), x.size() * 2)) ||
+        (rc = upload(&d_emit, emit.data(), emit.size() * 4)))
+        return rc;
+    HIP_TRY(hipMalloc(&d_lp, std::max<size_t>(size_t(K) * 4, 16)));
+    HIP_TRY(hipMalloc(&d_ld, std::max<size_t>(size_t(R) * 4, 16)));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_coef), std::max<size_t>(coef_bytes, 16)));
+    HIP_TRY(hipMemsetAsync(p->d_coef, 0, coef_bytes, nullptr));
+    if (records) {
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_idx), rec_bytes));
+        HIP_TRY(hipMemsetAsync(p->d_idx, 0, rec_bytes, nullptr));
+    }
+    Plan16Args a{};
+    a.src_el = static_cast<const uint16_t*>(d_y);
+    a.tgt_el = static_cast<const uint16_t*>(d_x);
+    a.emit = static_cast<const int32_t*>(d_emit);
+    a.logt = logt;
+    a.expt = expt;
+    a.lp = static_cast<uint32_t*>(d_lp);
+    a.ld = static_cast<uint32_t*>(d_ld);
+    a.coef = p->d_coef;
+    a.rec = records ? reinterpret_cast<uint8_t*>(p->d_idx) : nullptr;
+    a.K = K;
+    a.d = d;
+    a.R = R;
+    a.rt = p->rt;
+    HIP_TRY(launch_plan_m16(a, nullptr));
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    out_slots.resize(std::max(size_t(p->ntiles) * p->rt, size_t((R + 31) / 32) * 32), 0);
+    in_slots.resize(in_slots.size() + 16, 0);
+    if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
+    if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
+    in_slots.resize(size_t(K));
+    p->in_slots = std::move(in_slots);
+    p->out_slots = std::move(out_slots);
+    out = std::move(p);
+    return 0;
+}
+
 struct rsg_codec {
     int device = 0;
     uint16_t k = 0, r = 0;
@@ -244,6 +323,7 @@ struct rsg_codec {
     std::vector<std::vector<uint8_t>> dec_lru;
     int m8_mode = 18;
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
+    int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
@@ -272,11 +352,14 @@ struct rsg_codec {
     std::string last_kernel = "none";
 };
 
-static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r, const bool* erased,
-                        std::vector<uint16_t>& M, std::vector<int32_t>& in_slots, std::vector<int32_t>& out_slots) {
+// Target / source position lists of the encode (erased == NULL) or decode matrix, and their slots.
+static void codec_lists(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r, const bool* erased,
+                        std::vector<uint16_t>& targets, std::vector<int>& emit, std::vector<uint16_t>& sources,
+                        std::vector<int32_t>& in_slots, std::vector<int32_t>& out_slots) {
     const size_t n = size_t(k) + r;
-    std::vector<uint16_t> targets, sources;
-    std::vector<int> emit;
+    targets.clear();
+    emit.clear();
+    sources.clear();
     in_slots.clear();
     out_slots.clear();
     if (!erased) {
@@ -294,8 +377,29 @@ static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r
             }
         }
     }
+}
+
+static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r, const bool* erased,
+                        std::vector<uint16_t>& M, std::vector<int32_t>& in_slots, std::vector<int32_t>& out_slots) {
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    codec_lists(pos, k, r, erased, targets, emit, sources, in_slots, out_slots);
     M = solve_matrix(targets, emit, sources);
     return 0;
+}
+
+// The device plan of the encode (erased == NULL) or decode matrix: GF(2^16) codes with large matrices
+// are built on the device, everything else from the host matrix.
+static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out) {
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
+    const int K = int(in.size()), R = int(outs.size());
+    if (c->m > 8 && R > 0 && (c->m16_plans == 1 || (c->m16_plans == 2 && int64_t(K) * R >= (int64_t(1) << 16))))
+        return build_plan_m16_device(c->device, targets, emit, sources, std::move(in), std::move(outs), out);
+    std::vector<uint16_t> M = solve_matrix(targets, emit, sources);
+    return build_plan(c->device, c->m, std::move(M), K, R, std::move(in), std::move(outs), out);
 }
 
 extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t** out) {
@@ -320,10 +424,7 @@ extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t*
     c->m = subfield_degree(c->positions);
     int rc = device_tables(device, &c->d_ltab);
     if (rc) return rc;
-    std::vector<uint16_t> M;
-    std::vector<int32_t> in, outs;
-    codec_matrix(c->positions, k, r, nullptr, M, in, outs);
-    if ((rc = build_plan(device, c->m, std::move(M), k, r, std::move(in), std::move(outs), c->enc))) return rc;
+    if ((rc = make_plan(c.get(), nullptr, c->enc))) return rc;
     *out = c.release();
     return 0;
 }
@@ -361,6 +462,20 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!std::strcmp(name, "m16_mode")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->m16_mode = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m16_plans")) {
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        c->m16_plans = int(value);
+        c->dec.clear();  // plans are rebuilt under the new setting: decode plans on use, encode now
+        c->dec_lru.clear();
+        if (c->m > 8) {
+            HIP_TRY(hipSetDevice(c->device));
+            HIP_TRY(hipDeviceSynchronize());  // the old encode plan may still be in use
+            std::unique_ptr<DevPlan> e;
+            if (int rc = make_plan(c, nullptr, e)) return rc;
+            c->enc = std::move(e);
+        }
         return 0;
     }
     if (!std::strcmp(name, "batch_plans")) {
@@ -497,13 +612,8 @@ static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPla
     if (cnt != t) return RS_ERR_INVALID;
     auto it = c->dec.find(key);
     if (it == c->dec.end()) {
-        std::vector<uint16_t> M;
-        std::vector<int32_t> in, outs;
-        codec_matrix(c->positions, c->k, c->r, is_erased, M, in, outs);
         std::unique_ptr<DevPlan> p;
-        const int R = int(outs.size()), K = int(in.size());
-        int rc = build_plan(c->device, c->m, std::move(M), K, R, std::move(in), std::move(outs), p);
-        if (rc) return rc;
+        if (int rc = make_plan(c, is_erased, p)) return rc;
         if (c->dec_lru.size() >= 16) {
             c->dec.erase(c->dec_lru.front());
             c->dec_lru.erase(c->dec_lru.begin());

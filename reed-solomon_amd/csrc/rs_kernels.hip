@@ -966,6 +966,49 @@ __global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0
     }
 }
 
+// ------------------------------------------------------------ GF(2^16) plans on the device
+__global__ void __launch_bounds__(256) k_plan16_sums(Plan16Args a) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    constexpr uint32_t N = 65535u;
+    if (i < a.K) {  // lp[q] = sum_e log(Y_q + X_e)
+        const uint16_t y = a.src_el[i];
+        uint32_t acc = 0;
+        for (int e = 0; e < a.d; ++e) acc += a.logt[y ^ a.tgt_el[e]];
+        a.lp[i] = acc % N;
+    } else if (i < int64_t(a.K) + a.R) {  // ld[p] = sum_{e != p} log(X_p + X_e)
+        const int p = int(i - a.K), self = a.emit[p];
+        const uint16_t x = a.tgt_el[self];
+        uint32_t acc = 0;
+        for (int e = 0; e < a.d; ++e)
+            if (e != self) acc += a.logt[x ^ a.tgt_el[e]];
+        a.ld[p] = acc % N;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_plan16_fill(Plan16Args a) {
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;  // row * K + i
+    if (e >= int64_t(a.R) * a.K) return;
+    const int row = int(e / a.K), i = int(e - int64_t(row) * a.K);
+    constexpr uint32_t N = 65535u;
+    const uint32_t L = (a.lp[i] + 2 * N - a.ld[row] - a.logt[a.tgt_el[a.emit[row]] ^ a.src_el[i]]) % N;
+    const uint32_t c = a.expt[L];
+    const int t = row / a.rt, j = row - t * a.rt;
+    reinterpret_cast<uint16_t*>(a.coef)[(int64_t(t) * a.K + i) * a.rt + j] = uint16_t(c);
+    if (a.rec) {  // k_apply_m16_v1 record byte of (plane n, output j): see rs_api.cpp:build_plan
+        const int t64 = row >> 6, j64 = row & 63;
+        uint8_t* r = a.rec + (int64_t(t64) * (a.K + 1) + i) * 256;
+        for (int n = 0; n < 4; ++n)
+            r[4 * (16 * n + 2 * (j64 >> 3) + (j64 & 1)) + ((j64 & 7) >> 1)] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
+    }
+}
+
+hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st) {
+    const int64_t nsum = int64_t(a.K) + a.R, nfill = int64_t(a.R) * a.K;
+    if (nsum > 0) hipLaunchKernelGGL(k_plan16_sums, dim3(unsigned((nsum + 255) / 256)), dim3(256), 0, st, a);
+    if (nfill > 0) hipLaunchKernelGGL(k_plan16_fill, dim3(unsigned((nfill + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
     if (n_sel <= 0) return hipSuccess;
     if (a.n > 256) return hipErrorInvalidValue;

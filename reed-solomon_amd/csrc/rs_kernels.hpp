@@ -49,6 +49,23 @@ struct PlanArgs {
     int64_t in_stride, out_stride, idx_stride;
 };
 hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st);
+
+// One GF(2^16) coding matrix built on the device (gf16.cpp:solve_matrix's evaluation) straight into
+// the m = 16 kernels' formats: coefficient tiles (k_apply_m16) and, if rec != null, the packed index
+// records of k_apply_m16_v1 (rt = 64). coef / rec must be zeroed by the caller.
+struct Plan16Args {
+    const uint16_t* src_el;  // [K] source elements Y_q
+    const uint16_t* tgt_el;  // [d] all target elements X_e
+    const int32_t* emit;     // [R] emitted target indices (matrix rows)
+    const uint16_t* logt;    // [65536] discrete log
+    const uint16_t* expt;    // [65536] alpha^i, i < 65535 (entry 65535 = 1)
+    uint32_t* lp;            // [K] scratch
+    uint32_t* ld;            // [R] scratch
+    uint32_t* coef;          // [ntiles][K][rt / 2]
+    uint8_t* rec;            // [ceil(R / 64)][K + 1][256] or null
+    int32_t K, d, R, rt;
+};
+hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st);
 // V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 

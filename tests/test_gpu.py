@@ -313,11 +313,13 @@ def test_decode_batch_device_plans_distinct_patterns(k, r, S, n):
             assert np.array_equal(got[s], want), f"stripe {s}"
 
 
+@pytest.mark.parametrize("plans", [0, 1])
 @pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("S", [2048, 2048 + 264])
-def test_m16_kernels_vs_oracle(S, mode):
+def test_m16_kernels_vs_oracle(S, mode, plans):
     """GF(2^16) code with r > 32 (64-row tiles): the hand-scheduled kernel (m16_mode 0, tail columns
-    by the compiled kernel) and the compiled kernel (2), encode and decode, bit-exact vs the oracle."""
+    by the compiled kernel) and the compiled kernel (2), with plans built on the host (m16_plans 0) or
+    on the device (1), encode and decode, bit-exact vs the oracle."""
     k, r, n = 300, 200, 3
     rng = np.random.default_rng(S + mode)
     host = np.zeros((n, k + r, S), np.uint8)
@@ -325,6 +327,7 @@ def test_m16_kernels_vs_oracle(S, mode):
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r)
     codec.set_option("m16_mode", mode)
+    codec.set_option("m16_plans", plans)  # rebuilds the encode plan
     assert codec.subfield == 16
     codec.encode(dev)
     torch.cuda.synchronize()
