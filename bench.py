@@ -39,14 +39,19 @@ TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")  # scripts/traffic
 
 def measured_traffic(kernel, cfg):
     """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters on this configuration
-    (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches."""
+    (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches: the
+    exact kernel name for JIT kernels (content-addressed), name + source hash for compiled ones."""
     try:
         with open(TRAFFIC_JSON) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    family = lambda name: str(name).split("[")[0]  # specialised kernels carry a matrix hash suffix
-    if family(t.get("bench_kernel")) != family(kernel) or t.get("config") != cfg or t.get("src_hash") != kernel_src_hash(kernel):
+    if t.get("config") != cfg:
+        return None
+    if "[" in str(kernel):  # JIT kernel: its name carries the hash of its generated source
+        if t.get("bench_kernel") != kernel:
+            return None
+    elif t.get("bench_kernel") != kernel or t.get("src_hash") != kernel_src_hash(kernel):
         return None
     return int(t["traffic_bytes"])
 SEED = 0x5EED
