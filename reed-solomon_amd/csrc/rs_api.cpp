@@ -342,6 +342,7 @@ struct rsg_codec {
     // call's launches (which may be on another stream) and is waited for before the next overwrite
     hipEvent_t scratch_ev = nullptr;
     bool scratch_pending = false;
+    hipStream_t scratch_stream = nullptr;
     ~rsg_codec() {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
@@ -488,7 +489,7 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
 
 extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->last_kernel.c_str() : "none"; }
 
-static int scratch_acquire(rsg_codec_t* c);
+static int scratch_acquire(rsg_codec_t* c, hipStream_t st);
 static int scratch_release(rsg_codec_t* c, hipStream_t st);
 
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
@@ -549,7 +550,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     if (p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) {  // split-K scratch for small m = 16 grids
         int64_t need = 0;
         if (m16_kslices(a, int64_t(n_stripes), &need) > 1) {
-            if (int rc = scratch_acquire(c)) return rc;
+            if (int rc = scratch_acquire(c, st)) return rc;
             if (int rc = grow(&c->d_partial, c->partial_cap, size_t(need))) return rc;
             a.scratch = static_cast<uint32_t*>(c->d_partial);
             a.scratch_bytes = int64_t(c->partial_cap);
@@ -638,8 +639,9 @@ extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, u
 }
 
 // rsg_decode_batch scratch: wait until the previous call's launches are done with it / mark this one's
-static int scratch_acquire(rsg_codec_t* c) {
-    if (c->scratch_pending) HIP_TRY(hipEventSynchronize(c->scratch_ev));
+static int scratch_acquire(rsg_codec_t* c, hipStream_t st) {
+    // work queued earlier on the same stream runs first anyway; another stream's is waited for
+    if (c->scratch_pending && c->scratch_stream != st) HIP_TRY(hipEventSynchronize(c->scratch_ev));
     c->scratch_pending = false;
     return 0;
 }
@@ -647,6 +649,7 @@ static int scratch_release(rsg_codec_t* c, hipStream_t st) {
     if (!c->scratch_ev) HIP_TRY(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->scratch_ev, st));
     c->scratch_pending = true;
+    c->scratch_stream = st;
     return 0;
 }
 
@@ -673,7 +676,7 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
         for (size_t i = 0; i < n; ++i) masks.push_back(e[i] ? 1 : 0);
     }
     if (ids.empty()) return 0;
-    int rc = scratch_acquire(c);
+    int rc = scratch_acquire(c, st);
     if (rc) return rc;
     const uint16_t* logt = nullptr;
     const uint8_t* g8 = nullptr;
@@ -775,7 +778,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         first.push_back(ids.size());
         ids.insert(ids.end(), g.second.begin(), g.second.end());
     }
-    if (int rc = scratch_acquire(c)) return rc;
+    if (int rc = scratch_acquire(c, st)) return rc;
     if (ids.size() > c->ids_cap) {
         if (c->d_ids) (void)hipFree(c->d_ids);
         c->d_ids = nullptr;

@@ -465,3 +465,30 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S):
         ref = poisoned[s].copy()
         assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
         assert np.array_equal(out[s], ref)
+
+
+def test_drop_in_m16_large_symbols():
+    """Reference per-call API on a GF(2^16) code with 64 KiB symbols: the call is pipelined in column
+    chunks on one stream and each chunk's small grid runs split-K; encode + restore bit-exact vs the
+    oracle, twice (second call reuses the plans and the split-K scratch)."""
+    k, r, S = 300, 64, 65536
+    rng = np.random.default_rng(64)
+    rs = rs_amd.RS()
+    for rep in range(2):
+        syms = [np.zeros(S, np.uint8) for _ in range(k + r)]
+        for i in range(k):
+            syms[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        assert rs.generate_repair_symbols(syms[:k], syms[k:]) == 0
+        want = np.stack(syms).copy()
+        ref = want.copy()
+        ref[k:] = 0
+        assert oracle_encode(k, r, ref) == 0
+        assert np.array_equal(want, ref)
+        er = np.zeros(k + r, bool)
+        er[rng.choice(k + r, r, replace=False)] = True
+        for i in np.nonzero(er)[0]:
+            syms[i][:] = 0
+        assert rs.restore_symbols(k, r, syms, er, int(er.sum())) == 0
+        got = np.stack(syms)
+        assert np.array_equal(got[:k], want[:k]), f"call {rep}"
+    rs.close()
