@@ -516,11 +516,17 @@ __device__ __forceinline__ void m16_v1_step(uint32_t y, const uint32_t* cp, u32x
 template <int ABL>
 __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[RING_SLOTS * 256];
-    const int64_t bid = blockIdx.x;
-    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    int64_t unit = blockIdx.x;
+    int tile = blockIdx.y;
+    if (a.units) {  // XCD-aware order: workgroup b runs on XCD b % 8
+        const int64_t slot = blockIdx.x >> 3;
+        tile = int(slot % a.tiles);
+        unit = (slot / a.tiles) * 8 + (blockIdx.x & 7);
+        if (unit >= a.units) return;  // padding of the last group of 8 units
+    }
+    const int64_t local = unit / a.nchunks;  // launch-local stripe
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
-    const int tile = blockIdx.y;
+    const int64_t chunk0 = (unit - local * a.nchunks) * 1024;
     const int slice = blockIdx.z;
     // split-K: this workgroup takes inputs [i0, i0 + K) of the full list
     const int i0 = a.kslices > 1 ? int(int64_t(a.K) * slice / a.kslices) : 0;
@@ -574,7 +580,8 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     }
     const int rows = min(64, a.R - tile * 64);
     if (a.kslices > 1) {  // partial products: [slice][stripe][tile * 64 + p][chunk dwords]
-        const int64_t nloc = gridDim.x / a.nchunks, rpad = int64_t(gridDim.y) * 64, cw = a.nchunks * 256;
+        const int64_t nloc = a.units ? a.units / a.nchunks : gridDim.x / a.nchunks;
+        const int64_t rpad = int64_t(a.units ? a.tiles : gridDim.y) * 64, cw = a.nchunks * 256;
         uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 64) * cw + (chunk0 >> 2) + threadIdx.x;
 #pragma unroll
         for (int p = 0; p < 64; ++p)
@@ -745,7 +752,9 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
             V1Args v = v1_args(a, full, nullptr);
             v.kslices = m16_kslices(a, n_stripes, nullptr);
             v.partial = a.scratch;
-            dim3 g(unsigned(n_stripes * full), tiles, unsigned(v.kslices));
+            v.units = n_stripes * full;
+            v.tiles = int(tiles);
+            dim3 g(unsigned((v.units + 7) / 8 * 8 * tiles), 1, unsigned(v.kslices));
             if (a.mode == 0)
                 hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
             else

@@ -29,6 +29,11 @@ struct V1Args {
     // k_xor_slices reduces into the outputs. kslices <= 1: direct stores.
     int32_t kslices;
     uint32_t* partial;
+    // k_apply_m16_v1 block order (XCD-aware): units = n_stripes * nchunks (stripe, chunk) pairs, unit u
+    // on XCD u % 8 with its `tiles` row tiles dispatched back to back there, so they share that XCD's
+    // L2 copy of the unit's inputs. units == 0: grid (units, tiles) in the plain order.
+    int64_t units;
+    int32_t tiles;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.
