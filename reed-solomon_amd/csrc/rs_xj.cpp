@@ -143,6 +143,7 @@ struct XjConfig {
     int ablate = 0;    // timing ablations (wrong results): 1 no finish, 2 no rows, 4 no tables
     int nt = 0;        // cache policy bits on the global loads / stores: 1 = nt loads, 2 = nt stores, 3 = both
     int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
+    int share = 0;     // 1 (two roles): each role builds one group's subset tables, exchanged via LDS
     int lfin = 0;      // finish: 0 = VALU Horner over z (above); 1 = Horner in gamma through a 128 KiB LDS
                        // table T[w] = gamma * w (persistent kernel, one workgroup per CU)
     explicit XjConfig(int R = 0) {
@@ -158,12 +159,14 @@ struct XjConfig {
         env("RS_XJ_LDS", lds);
         env("RS_XJ_NT", nt);
         env("RS_XJ_FIN", lfin);
+        env("RS_XJ_SHARE", share);
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
         if (lds) ring = 2;  // VGPR double buffer behind the LDS ring
         opr = std::max(1, std::min(16, opr));
         if (R > 0) opr = std::min(opr, R);  // small codes: smaller register layout, more waves per SIMD
+        share = (share && !lds && !lfin && R > 0 && (R + opr - 1) / opr == 2) ? 1 : 0;
         ring = std::max(2, std::min(6, ring));
         horner = horner ? 1 : 0;
     }
@@ -177,9 +180,9 @@ struct XjConfig {
     int tmp(int q, int k) const { return ring_base() + opr + 2 * (q % 8) + k; }
     int cst() const { return ring_base() + opr + 16; }
     std::string tag() const {
-        char b[96];
-        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d", opr, ring,
-                      buffer, spread, horner, ablate, lds, nt, lfin);
+        char b[112];
+        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d", opr,
+                      ring, buffer, spread, horner, ablate, lds, nt, lfin, share);
         return b;
     }
 };
@@ -468,17 +471,24 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         // patterns of this role's rows over the pair's two groups
         int pat[16][8][2];
         bool need[2][16] = {};
+        auto pattern = [&](int row, int t, int h) {
+            int e = 0;
+            for (int jj = 0; jj < 4; ++jj) {
+                const int i = 8 * g + 4 * h + jj;
+                if (i < K && ((cb[size_t(row) * K + i] >> t) & 1)) e |= 1 << jj;
+            }
+            return e;
+        };
         for (int q = 0; q < nq; ++q)
             for (int t = 0; t < 8; ++t)
                 for (int h = 0; h < 2; ++h) {
-                    int e = 0;
-                    for (int jj = 0; jj < 4; ++jj) {
-                        const int i = 8 * g + 4 * h + jj;
-                        if (i < K && ((cb[size_t(p0 + q) * K + i] >> t) & 1)) e |= 1 << jj;
-                    }
-                    pat[q][t][h] = e;
-                    need[h][e] = true;
+                    pat[q][t][h] = pattern(p0 + q, t, h);
+                    need[h][pat[q][t][h]] = true;
                 }
+        if (C.share)  // both roles build / receive the entries either of them needs
+            for (int row = 0; row < R; ++row)
+                for (int t = 0; t < 8; ++t)
+                    for (int h = 0; h < 2; ++h) need[h][pattern(row, t, h)] = true;
         auto single = [&](int h, int jj) { return C.ring_base() + 8 * (g % C.ring) + 4 * h + jj; };
         auto reg = [&](int h, int e) {
             if (__builtin_popcount(e) == 1) return single(h, __builtin_ctz(e));
@@ -486,6 +496,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         };
         std::vector<std::string> body;
         for (int h = 0; h < 2; ++h) {
+            if (C.share && h != w) continue;  // the partner role builds the other group
             // popcount 2 and 3 straight from the inputs; 15 from a built triple or pair
             bool built[16] = {};
             for (int e = 3; e < 15; ++e) {
@@ -518,6 +529,20 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                                          single(h, __builtin_ctz(rest)), single(h, 31 - __builtin_clz(rest))));
                 }
             }
+        }
+        if (C.share) {
+            // exchange through LDS slot (g % 2, group, entry) x 64 lanes: write own group's entries,
+            // barrier (the block is the two roles), read the partner's group
+            auto off = [&](int h, int e) { return (((g % 2) * 2 + h) * 16 + e) * 256; };
+            for (int e = 3; e < 16; ++e)
+                if (need[w][e] && __builtin_popcount(e) >= 2)
+                    body.push_back(E.fmt("ds_write_b32 %%[la], v%d offset:%d", reg(w, e), off(w, e)));
+            body.push_back("s_waitcnt lgkmcnt(0)");
+            body.push_back("s_barrier");
+            for (int e = 3; e < 16; ++e)
+                if (need[1 - w][e] && __builtin_popcount(e) >= 2)
+                    body.push_back(E.fmt("ds_read_b32 v%d, %%[la] offset:%d", reg(1 - w, e), off(1 - w, e)));
+            body.push_back("s_waitcnt lgkmcnt(0)");
         }
         if (C.ablate & 4) body.clear();
         for (auto& op : mid) body.push_back(op);  // LDS ring: next pair's reads + refills after the tables
@@ -627,13 +652,14 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
              "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[local] : (uint64_t)local;\n"
              "  const uint32_t col = chunk * 256u + (threadIdx.x & 63u) * 4u;\n";
     } else {
-        o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds[" << std::max(1, roles * C.lds * 512) << "];\n"
+        o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds["
+          << (C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
           << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
              "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
              "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
-          << C.lds * 2048 << "u;\n"
+          << (C.share ? 0 : C.lds * 2048) << "u;\n"
              "  const uint32_t la = lb + (threadIdx.x & 63u) * 4u;\n"
              "  {\n";
     }

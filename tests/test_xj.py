@@ -99,3 +99,30 @@ def test_xj_lds_finish_matches_oracle(k, r, monkeypatch):
     mem.b[:k * S] = want[:k].reshape(-1)
     run_block(src, mem, 0, S, k * S, S)
     assert np.array_equal(mem.b.reshape(k + r, S)[k:], want[k:])
+
+
+@pytest.mark.parametrize("k,r,kind", [(128, 32, "enc"), (128, 32, "bench"), (40, 20, "enc"), (13, 30, "enc")])
+def test_xj_shared_tables_match_oracle(k, r, kind, monkeypatch):
+    """RS_XJ_SHARE=1 (two roles build one group's subset tables each and exchange them through LDS
+    around an s_barrier; the emulator runs the roles in lockstep between barriers)."""
+    monkeypatch.setenv("RS_XJ_SHARE", "1")
+    full = _random_stripe(k, r, 99 + k + r)
+    assert oracle_encode(k, r, full) == 0
+    if kind == "enc":
+        src = xj_source(k, r)
+        assert "share1" in src and "s_barrier" in src
+        mem = Memory((k + r) * S)
+        mem.b[:k * S] = full[:k].reshape(-1)
+        run_block(src, mem, 0, S, k * S, S)
+        assert np.array_equal(mem.b.reshape(k + r, S)[k:], full[k:])
+    else:
+        er = np.zeros(k + r, bool)
+        er[bench_pattern(k, r)] = True
+        rcv = full.copy()
+        rcv[er] = 0
+        mem = Memory((k + r) * S)
+        mem.b[:] = rcv.reshape(-1)
+        src = xj_source(k, r, er)
+        assert "share1" in src
+        run_block(src, mem, 0, S, 0, S)
+        assert np.array_equal(mem.b.reshape(k + r, S)[:k], full[:k])

@@ -79,7 +79,7 @@ class Wave:
                 continue
             op, _, rest = ln.partition(" ")
             a = [x.strip() for x in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
-            if op in ("s_nop", "s_waitcnt", "s_branch", "s_getpc_b64", "s_setpc_b64"):
+            if op in ("s_nop", "s_waitcnt", "s_branch", "s_getpc_b64", "s_setpc_b64", "s_barrier"):
                 continue
             # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
             if op == "s_set_gpr_idx_on":
@@ -194,6 +194,16 @@ class Wave:
                 dst = self.m0 + 4 * np.arange(64)
                 idx = dst[:, None] + np.arange(4)[None, :]
                 self.lds[idx.reshape(-1)] = data.astype("<u4").view(np.uint8)
+            elif op == "ds_write_b32":
+                base, off = a[0], 0
+                if " " in a[1]:
+                    a1, o = a[1].split()
+                    off = int(o.split(":")[1])
+                else:
+                    a1 = a[1]
+                addr = self.val(base).astype(np.int64) + off
+                idx = addr[:, None] + np.arange(4)[None, :]
+                self.lds[idx.reshape(-1)] = np.ascontiguousarray(self.val(a1), dtype="<u4").view(np.uint8)
             elif op == "ds_read_b32":
                 base, off = a[1].split()
                 assert off.startswith("offset:"), ln
@@ -258,7 +268,10 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
     lds = np.zeros(max(1, region * len(roles)) + 64, np.uint8)
     if "ds_read_u16_d16_hi" in src:  # LDS finish: the gamma table at LDS address 0
         lds = gamma_table().copy()
+    if "ds_write_b32" in src:  # shared table exchange between the roles
+        lds = np.zeros(1 << 16, np.uint8)
     col = (chunk * 256 + np.arange(64) * 4).astype(np.uint32)
+    waves, segments = [], []
     for w, lines in enumerate(roles):
         lb = w * region
         ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF,
@@ -266,4 +279,15 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
                    la=(lb + np.arange(64) * 4).astype(np.uint32))
         wave = Wave(mem, ops)
         wave.lds = lds
-        wave.run(lines, finish)
+        waves.append(wave)
+        seg = [[]]  # the block's waves run in lockstep between s_barriers
+        for ln in lines:
+            if ln == "s_barrier":
+                seg.append([])
+            else:
+                seg[-1].append(ln)
+        segments.append(seg)
+    assert len({len(sg) for sg in segments}) == 1, "roles reach different numbers of barriers"
+    for i in range(len(segments[0])):
+        for wave, seg in zip(waves, segments):
+            wave.run(seg[i], finish)
