@@ -1,0 +1,88 @@
+"""Randomised parity fuzz on the GPU against the CPU oracle (TEST INFRASTRUCTURE): random (k, r),
+symbol sizes with and without tail columns, stripe counts and erasure patterns, through every kernel
+path: matrix-specialised XOR kernels (jit=1), generic GF(256) kernels (jit=0), GF(2^16) codes
+(hand-scheduled kernel, split-K on small grids, device-built plans), and rsg_decode_batch with a
+pattern per stripe (device-built plans). Prints one JSON line per case and a summary."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "reed-solomon_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import rs_amd  # noqa: E402
+from _util import oracle_decode, oracle_encode  # noqa: E402
+
+rng = np.random.default_rng(int(sys.argv[1]) if len(sys.argv) > 1 else 2024)
+budget = float(sys.argv[2]) if len(sys.argv) > 2 else 240.0
+t_end = time.time() + budget
+counts = {}
+fails = 0
+
+
+def one(family):
+    if family in ("xj", "generic", "batch"):
+        k = int(rng.integers(1, 200))
+        r = int(rng.integers(1, min(255 - k, 80) + 1))
+    else:  # m16
+        k = int(rng.integers(200, 1500))
+        r = int(rng.integers(max(1, 256 - k), 300))
+    S = int(rng.choice([2048, 4096, 8192, 1024])) + 8 * int(rng.integers(0, 64)) * int(rng.integers(0, 2))
+    if family == "m16":
+        S = min(S, 4096)
+    n = int(rng.integers(1, 5)) if family != "batch" else int(rng.integers(20, 60))
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "batch": dict(batch_plans=1)}[family]
+    codec = rs_amd.Codec(k, r, **kw)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    enc_kernel = codec.last_kernel
+    got = dev.cpu().numpy()
+    want = host.copy()
+    for s in range(n):
+        assert oracle_encode(k, r, want[s]) == 0
+    ok = bool(np.array_equal(got, want))
+    if family == "batch":
+        pats = np.zeros((n, k + r), bool)
+        for s in range(n):
+            pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+        poisoned = got.copy()
+        poisoned[pats] = 0
+        dev.copy_(torch.from_numpy(poisoned))
+        assert codec.decode_batch(dev, pats) == 0
+    else:
+        er = np.zeros(k + r, bool)
+        er[rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+        pats = np.broadcast_to(er, (n, k + r))
+        poisoned = got.copy()
+        poisoned[:, er] = 0
+        dev.copy_(torch.from_numpy(poisoned))
+        codec.decode(dev, er)
+    torch.cuda.synchronize()
+    dec_kernel = codec.last_kernel
+    out = dev.cpu().numpy()
+    for s in range(n):
+        ref = poisoned[s].copy()
+        assert oracle_decode(k, r, ref, pats[s], int(pats[s].sum())) == 0
+        ok = ok and bool(np.array_equal(out[s], ref))
+    codec.close()
+    return dict(family=family, k=k, r=r, S=S, stripes=n, encode=enc_kernel, decode=dec_kernel, ok=ok)
+
+
+families = ["xj", "generic", "m16", "batch"]
+i = 0
+while time.time() < t_end:
+    fam = families[i % len(families)]
+    i += 1
+    res = one(fam)
+    counts[fam] = counts.get(fam, 0) + 1
+    fails += 0 if res["ok"] else 1
+    print(json.dumps(res), flush=True)
+print(json.dumps({"summary": True, "cases": counts, "failures": fails}), flush=True)
+sys.exit(1 if fails else 0)

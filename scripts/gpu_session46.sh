@@ -1,0 +1,7 @@
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 420 python -u scripts/fuzz_parity.py 2024 300 > gpurun_out/fuzz.log 2>&1; rc=$?
+tail -1 gpurun_out/fuzz.log; grep -c '"ok": false' gpurun_out/fuzz.log; grep '"ok": false' gpurun_out/fuzz.log | head -5
+exit $rc
