@@ -126,3 +126,23 @@ def test_xj_shared_tables_match_oracle(k, r, kind, monkeypatch):
         assert "share1" in src
         run_block(src, mem, 0, S, 0, S)
         assert np.array_equal(mem.b.reshape(k + r, S)[:k], full[:k])
+
+
+KNOBS = [{"RS_XJ_OPR": "8"}, {"RS_XJ_OPR": "5"}, {"RS_XJ_RING": "3"}, {"RS_XJ_BUFFER": "1"}, {"RS_XJ_SPREAD": "1"},
+         {"RS_XJ_HORNER": "1"}, {"RS_XJ_LDS": "3"}, {"RS_XJ_NT": "3"}, {"RS_XJ_RING": "4", "RS_XJ_SPREAD": "1"}]
+
+
+@pytest.mark.parametrize("knobs", KNOBS, ids=lambda d: ",".join(f"{k[6:]}={v}" for k, v in d.items()))
+@pytest.mark.parametrize("k,r", [(128, 32), (30, 17)])
+def test_xj_generation_knobs_match_oracle(k, r, knobs, monkeypatch):
+    """Every generation knob of the XOR kernel (outputs per wave, ring depth, buffer addressing, load
+    spreading, Horner element, LDS-DMA ring, cache policy) yields a program that reproduces the
+    oracle's repair symbols in the emulator."""
+    for name, value in knobs.items():
+        monkeypatch.setenv(name, value)
+    want = _random_stripe(k, r, 5 * k + r)
+    assert oracle_encode(k, r, want) == 0
+    mem = Memory((k + r) * S)
+    mem.b[:k * S] = want[:k].reshape(-1)
+    run_block(xj_source(k, r), mem, 0, S, k * S, S)
+    assert np.array_equal(mem.b.reshape(k + r, S)[k:], want[k:])
