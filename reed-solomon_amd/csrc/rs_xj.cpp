@@ -2,17 +2,21 @@
 //
 // Generated kernel `rs_xj` (one per coding matrix and slot lists):
 //   grid (column chunks of 256 B, stripes), block = 64 x roles threads. All waves of a block work on
-//   the same 256-byte column of one stripe; wave w ("role") owns outputs 8w .. 8w+7.
-//   Register contract of a role (fixed, so the generated code can name registers directly):
-//     v[8:71]   accumulators u_{q,t} of output q (0..7), bit-plane t (0..7): v[8 + 8q + t]
-//     v[72:95]  input ring, 3 slots x 8 inputs (one group pair = 8 consecutive inputs)
-//     v[96:106] / v[107:117]  non-trivial subset XORs of the pair's groups A (inputs 0-3) / B (4-7)
-//     v118      this lane's byte offset in the symbol (column)
-//     v[72:103] after the XOR network: finish registers H, T1, T2 (spare) of output q at v[72 + 4q]
-//     s[32:38]  src base, src symbol stride, dst base, dst symbol stride; s[40:55] address pairs;
-//     s[56:59]  call / return address of the shared finish block; s[64:71] output byte offsets
-//   The finish block (Horner in alpha^-1 over the 8 bit-plane accumulators of all 8 outputs) is emitted
-//   once at the kernel entry and entered by s_swappc_b64 from every role.
+//   the same 256-byte column of one stripe; wave w ("role") owns outputs opr*w .. opr*w + opr - 1
+//   (opr = min(16, R) outputs per role by default, XjConfig).
+//   Register contract of a role (XjConfig's map; fixed, so the generated code names registers directly):
+//     v[1 : 8 opr]              accumulators u_{q,t} of output q, bit-plane t: v[1 + 8q + t]
+//     ring_base = 1 + 8 opr     input ring: `ring` slots x 8 inputs (one group pair = 8 consecutive inputs)
+//     tab(h) = ring_base + 8 ring + 11 h    the 11 non-trivial subset XORs of group h (inputs 4h..4h+3)
+//     after the XOR network: fin(q) = ring_base + q holds output q; tmp(q, k) Horner temporaries
+//     s[32:38]  src base, src symbol stride, dst base, dst symbol stride; s[40:55] address pairs /
+//               buffer offsets + V#s; s[56:59] call / return address of the shared finish block;
+//               s62 scratch, s63 saved m0; the column offset is the compiler's %[col] VGPR
+//   The finish block (Horner in alpha^-1 over the 16 z-coordinates, chains interleaved 8 at a time) is
+//   emitted once at the kernel entry and entered by s_swappc_b64 from every role.
+//   Experimental forms (knobs in XjConfig, measured in DESIGN.md section 5): LDS-DMA input ring,
+//   buffer addressing, spread loads, Horner in alpha, LDS-table finish (persistent grid), LDS table
+//   sharing between roles.
 #include "rs_xj.hpp"
 
 #include <algorithm>

@@ -10,8 +10,9 @@
 // accumulator. All register indices are fixed by the matrix, so the kernel is generated per coding
 // matrix (hiprtc) and cached in memory and on disk, like rs_jit.hpp.
 //
-// Work per 256-byte column of a stripe at k=128, r=32: 4096 XOR3 (rows) + 4 x 352 table XORs +
-// 32 x ~88 finish ops, against ~18000 for the per-input multiple/nibble-table kernels.
+// Work per 256-byte column of a stripe at k=128, r=32 (two roles of 16 outputs): 4096 XOR3 (rows) +
+// 2 x 352 table XORs + 32 x ~88 finish ops ~= 7500 VALU, against ~18000 for the per-input
+// multiple / nibble-table kernels.
 #pragma once
 #include <hip/hip_runtime.h>
 
