@@ -927,9 +927,14 @@ struct Impl {
     size_t cap = 0;
     std::unique_ptr<HostPool> pool;  // gather / scatter workers
     hipEvent_t ev[kMaxChunks] = {};
+    int32_t* h_rows = nullptr;  // pinned / device row list of the decode's packed copy-back
+    int32_t* d_rows = nullptr;
+    size_t rows_cap = 0;
     ~Impl() {
         (void)hipSetDevice(device);
         codecs.clear();
+        if (h_rows) (void)hipHostFree(h_rows);
+        if (d_rows) (void)hipFree(d_rows);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (h_buf) (void)hipHostFree(h_buf);
@@ -1084,16 +1089,34 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    const size_t P = pad16(S), W = chunk_width(S), nch = (S + W - 1) / W;
-    if (im.reserve(n * P)) return 1;
-    uint8_t *h = im.h_buf, *d = im.d_buf;
-    // erased slots are neither gathered nor read by the decoder; only rows lost[0] .. lost.back() come back
+    const size_t P = pad16(S), W = chunk_width(S), nch = (S + W - 1) / W, nl = lost.size();
+    // erased slots are neither gathered nor read by the decoder. Only restored rows come back: the span
+    // lost[0] .. lost.back() when it is (nearly) contiguous, else the rows packed on the device behind
+    // the stripe (k_gather_rows) and copied as one block
     const size_t lo = size_t(lost.front()), rows = size_t(lost.back()) - lo + 1;
+    const bool packed = rows > nl + nl / 4;
+    if (im.reserve((n + (packed ? nl : 0)) * P)) return 1;
+    uint8_t *h = im.h_buf, *d = im.d_buf;
+    if (packed) {
+        if (nl > im.rows_cap) {
+            if (im.h_rows) (void)hipHostFree(im.h_rows);
+            if (im.d_rows) (void)hipFree(im.d_rows);
+            im.h_rows = nullptr;
+            im.d_rows = nullptr;
+            im.rows_cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&im.h_rows), nl * 4, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&im.d_rows), nl * 4));
+            im.rows_cap = nl;
+        }
+        std::memcpy(im.h_rows, lost.data(), nl * 4);  // the previous call has finished with it (synchronous)
+        HIP_TRY(hipMemcpyAsync(im.d_rows, im.h_rows, nl * 4, hipMemcpyHostToDevice, im.stream));
+    }
+    uint8_t *hp = h + n * P, *dp = d + n * P;  // packed restored rows (row j = slot lost[j])
     auto scatter = [&](size_t ch) {
         const size_t off = ch * W, w = std::min(W, S - off);
-        im.pool->run(int(lost.size()), [&](int j) {
+        im.pool->run(int(nl), [&](int j) {
             const size_t i = size_t(lost[size_t(j)]);
-            std::memcpy(rcv->symbols[i]->data + off, h + i * P + off, w);
+            std::memcpy(rcv->symbols[i]->data + off, (packed ? hp + size_t(j) * P : h + i * P) + off, w);
         });
     };
     for (size_t ch = 0; ch < nch; ++ch) {
@@ -1105,7 +1128,14 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
         HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, n, hipMemcpyHostToDevice, im.stream));
         rc = rsg_decode(c, d + off, n * P, P, 1, w, is_erased, t, im.stream);
         if (rc) return rc;
-        HIP_TRY(hipMemcpy2DAsync(h + lo * P + off, P, d + lo * P + off, P, w, rows, hipMemcpyDeviceToHost, im.stream));
+        if (packed) {
+            HIP_TRY(launch_gather_rows(dp + off, int64_t(P), d + off, int64_t(P), im.d_rows, int64_t(nl), int64_t(w),
+                                       im.stream));
+            HIP_TRY(hipMemcpy2DAsync(hp + off, P, dp + off, P, w, nl, hipMemcpyDeviceToHost, im.stream));
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(h + lo * P + off, P, d + lo * P + off, P, w, rows, hipMemcpyDeviceToHost,
+                                     im.stream));
+        }
         HIP_TRY(hipEventRecord(im.ev[ch], im.stream));
         if (ch) {
             HIP_TRY(hipEventSynchronize(im.ev[ch - 1]));

@@ -752,9 +752,13 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
             V1Args v = v1_args(a, full, nullptr);
             v.kslices = m16_kslices(a, n_stripes, nullptr);
             v.partial = a.scratch;
-            v.units = n_stripes * full;
+            // XCD-aware order only with units to spread over all 8 XCDs (a single stripe's tiles and
+            // slices would otherwise all land on one XCD)
+            const int64_t units = n_stripes * full;
+            v.units = (v.kslices == 1 && units >= 64) ? units : 0;
             v.tiles = int(tiles);
-            dim3 g(unsigned((v.units + 7) / 8 * 8 * tiles), 1, unsigned(v.kslices));
+            dim3 g = v.units ? dim3(unsigned((units + 7) / 8 * 8 * tiles), 1, 1)
+                             : dim3(unsigned(units), tiles, unsigned(v.kslices));
             if (a.mode == 0)
                 hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
             else
@@ -1015,6 +1019,25 @@ hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st) {
     const int64_t nsum = int64_t(a.K) + a.R, nfill = int64_t(a.R) * a.K;
     if (nsum > 0) hipLaunchKernelGGL(k_plan16_sums, dim3(unsigned((nsum + 255) / 256)), dim3(256), 0, st, a);
     if (nfill > 0) hipLaunchKernelGGL(k_plan16_fill, dim3(unsigned((nfill + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// dst row j = src row rows[j] (16-byte units; the per-call decode packs the restored rows for one D2H)
+__global__ void __launch_bounds__(256) k_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
+                                                     const int32_t* rows, int64_t units) {
+    const int64_t u = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (u >= units) return;
+    const int64_t j = blockIdx.y;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<u32x4*>(dst + j * dpitch)[u] = reinterpret_cast<const u32x4*>(src + int64_t(rows[j]) * spitch)[u];
+}
+
+hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                              int64_t nrows, int64_t width, hipStream_t st) {
+    const int64_t units = (width + 15) / 16;
+    if (nrows <= 0 || units <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_rows, dim3(unsigned((units + 255) / 256), unsigned(nrows)), dim3(256), 0, st, dst,
+                       dpitch, src, spitch, rows, units);
     return hipGetLastError();
 }
 

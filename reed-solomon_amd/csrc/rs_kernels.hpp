@@ -69,6 +69,10 @@ hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st);
 // V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 
+// dst row j = src row rows[j] for j < nrows, `width` bytes each (16-byte aligned rows, padded pitch)
+hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                              int64_t nrows, int64_t width, hipStream_t st);
+
 int apply_tile_rows(int m, int R);
 // V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff);
