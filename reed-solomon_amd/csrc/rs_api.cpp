@@ -343,9 +343,17 @@ struct rsg_codec {
     hipEvent_t scratch_ev = nullptr;
     bool scratch_pending = false;
     hipStream_t scratch_stream = nullptr;
+    // rsg_encode_host / rsg_decode_host: two streams, each with its own device batch buffer
+    hipStream_t hs[2] = {nullptr, nullptr};
+    uint8_t* hbuf[2] = {nullptr, nullptr};
+    size_t hbuf_cap = 0;
     ~rsg_codec() {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
+        for (int i = 0; i < 2; ++i) {
+            if (hs[i]) (void)hipStreamDestroy(hs[i]);
+            if (hbuf[i]) (void)hipFree(hbuf[i]);
+        }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
                         d_partial})
             if (p) (void)hipFree(p);
@@ -744,6 +752,107 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
     }
     c->last_kernel = "apply_m8_v1_ps";
     return scratch_release(c, st);
+}
+
+// ---------------------------------------------------------------- host-memory batches (PCIe)
+// Stripes in host memory: batches of stripes alternate over two streams, each H2D -> kernel -> D2H,
+// so one batch's kernel overlaps the other's copies and H2D overlaps D2H. Pinned host memory
+// (hipHostMalloc / hipHostRegister) runs the copies at PCIe rate; pageable memory works, slower.
+static constexpr size_t kHostBatchBytes = size_t(256) << 20;  // device buffer per stream
+
+static int host_pipe_reserve(rsg_codec_t* c, size_t bytes) {
+    HIP_TRY(hipSetDevice(c->device));
+    for (int i = 0; i < 2; ++i)
+        if (!c->hs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking));
+    if (bytes > c->hbuf_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (c->hbuf[i]) (void)hipFree(c->hbuf[i]);
+            c->hbuf[i] = nullptr;
+        }
+        c->hbuf_cap = 0;
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->hbuf[i]), bytes));
+        c->hbuf_cap = bytes;
+    }
+    return 0;
+}
+
+extern "C" int rsg_encode_host(rsg_codec_t* c, const void* h_info, uint64_t info_stripe_stride,
+                               uint64_t info_symbol_stride, void* h_rep, uint64_t rep_stripe_stride,
+                               uint64_t rep_symbol_stride, uint64_t n_stripes, uint64_t symbol_size) {
+    if (!c || (n_stripes && (!h_info || !h_rep))) return RS_ERR_INVALID;
+    const uint64_t S = symbol_size, k = c->k, r = c->r;
+    if (S & 1) return RS_ERR_INVALID;
+    if (!n_stripes || !S || !r) return 0;
+    const uint64_t P = (S + 15) & ~uint64_t(15), per = (k + r) * P;
+    const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kHostBatchBytes / per));
+    if (int rc = host_pipe_reserve(c, size_t(B * per))) return rc;
+    const bool reg_in = info_stripe_stride == k * info_symbol_stride, reg_out = rep_stripe_stride == r * rep_symbol_stride;
+    const uint8_t* hi = static_cast<const uint8_t*>(h_info);
+    uint8_t* ho = static_cast<uint8_t*>(h_rep);
+    for (uint64_t s0 = 0, it = 0; s0 < n_stripes; s0 += B, ++it) {
+        const uint64_t nb = std::min(B, n_stripes - s0);
+        hipStream_t st = c->hs[it & 1];
+        uint8_t* d_info = c->hbuf[it & 1];  // [nb][k][P] then [nb][r][P]
+        uint8_t* d_rep = d_info + nb * k * P;
+        if (reg_in)
+            HIP_TRY(hipMemcpy2DAsync(d_info, P, hi + s0 * info_stripe_stride, info_symbol_stride, S, nb * k,
+                                     hipMemcpyHostToDevice, st));
+        else
+            for (uint64_t b = 0; b < nb; ++b)
+                HIP_TRY(hipMemcpy2DAsync(d_info + b * k * P, P, hi + (s0 + b) * info_stripe_stride, info_symbol_stride,
+                                         S, k, hipMemcpyHostToDevice, st));
+        if (int rc = rsg_encode(c, d_info, k * P, P, d_rep, r * P, P, nb, S, st)) return rc;
+        if (reg_out)
+            HIP_TRY(hipMemcpy2DAsync(ho + s0 * rep_stripe_stride, rep_symbol_stride, d_rep, P, S, nb * r,
+                                     hipMemcpyDeviceToHost, st));
+        else
+            for (uint64_t b = 0; b < nb; ++b)
+                HIP_TRY(hipMemcpy2DAsync(ho + (s0 + b) * rep_stripe_stride, rep_symbol_stride, d_rep + b * r * P, P, S,
+                                         r, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(c->hs[0]));
+    HIP_TRY(hipStreamSynchronize(c->hs[1]));
+    return 0;
+}
+
+extern "C" int rsg_decode_host(rsg_codec_t* c, void* h_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
+                               uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, uint16_t t) {
+    if (!c || !is_erased || (n_stripes && !h_rcv)) return RS_ERR_INVALID;
+    if (t > c->r) return RS_ERR_CANNOT_RESTORE;
+    const uint64_t S = symbol_size, n = uint64_t(c->k) + c->r;
+    if (S & 1) return RS_ERR_INVALID;
+    std::vector<int> lost;  // restored (erased information) slots
+    uint16_t cnt = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (is_erased[i]) {
+            ++cnt;
+            if (i < c->k) lost.push_back(int(i));
+        }
+    if (cnt != t) return RS_ERR_INVALID;
+    if (!n_stripes || !S || lost.empty()) return 0;
+    const uint64_t P = (S + 15) & ~uint64_t(15), per = n * P;
+    const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kHostBatchBytes / per));
+    if (int rc = host_pipe_reserve(c, size_t(B * per))) return rc;
+    const bool reg = stripe_stride == n * symbol_stride;
+    uint8_t* h = static_cast<uint8_t*>(h_rcv);
+    for (uint64_t s0 = 0, it = 0; s0 < n_stripes; s0 += B, ++it) {
+        const uint64_t nb = std::min(B, n_stripes - s0);
+        hipStream_t st = c->hs[it & 1];
+        uint8_t* d = c->hbuf[it & 1];  // [nb][k + r][P]
+        if (reg)
+            HIP_TRY(hipMemcpy2DAsync(d, P, h + s0 * stripe_stride, symbol_stride, S, nb * n, hipMemcpyHostToDevice, st));
+        else
+            for (uint64_t b = 0; b < nb; ++b)
+                HIP_TRY(hipMemcpy2DAsync(d + b * n * P, P, h + (s0 + b) * stripe_stride, symbol_stride, S, n,
+                                         hipMemcpyHostToDevice, st));
+        if (int rc = rsg_decode(c, d, n * P, P, nb, S, is_erased, t, st)) return rc;
+        for (int i : lost)  // restored slot i of every stripe of the batch: one strided copy
+            HIP_TRY(hipMemcpy2DAsync(h + s0 * stripe_stride + uint64_t(i) * symbol_stride, stripe_stride,
+                                     d + uint64_t(i) * P, n * P, S, nb, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(c->hs[0]));
+    HIP_TRY(hipStreamSynchronize(c->hs[1]));
+    return 0;
 }
 
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,

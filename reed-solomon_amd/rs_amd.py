@@ -78,6 +78,8 @@ _sig("rsg_last_kernel", ctypes.c_char_p, P)
 _sig("rsg_encode", ctypes.c_int, P, P, u64, u64, P, u64, u64, u64, u64, P)
 _sig("rsg_decode", ctypes.c_int, P, P, u64, u64, u64, u64, P, u16, P)
 _sig("rsg_decode_batch", ctypes.c_int, P, P, u64, u64, u64, u64, P, P)
+_sig("rsg_encode_host", ctypes.c_int, P, P, u64, u64, P, u64, u64, u64, u64)
+_sig("rsg_decode_host", ctypes.c_int, P, P, u64, u64, u64, u64, P, u16)
 _sig("rsg_fill_info", ctypes.c_int, P, u64, u64, u64, u16, u64, u64, u64, P)
 _sig("rsg_fingerprint", ctypes.c_int, P, u64, u64, u64, u32, u32, u64, P, P)
 _sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
@@ -283,6 +285,27 @@ class Codec:
                                    _stream_ptr(stream))
         if check and rc:
             raise RSError(rc, "rsg_decode_batch")
+        return rc
+
+    def encode_host(self, stripes, check=True):
+        """Stripes in HOST memory: a [n, k + r, S] uint8 array (numpy or a CPU tensor, pinned for PCIe
+        rate); writes the repair symbols in place (rsg_encode_host, pipelined, synchronous)."""
+        n, nsym, S = stripes.shape
+        assert nsym == self.k + self.r
+        ptr = stripes.data_ptr() if hasattr(stripes, "data_ptr") else stripes.ctypes.data
+        rc = _lib.rsg_encode_host(self._h, P(ptr), nsym * S, S, P(ptr + self.k * S), nsym * S, S, n, S)
+        if check and rc:
+            raise RSError(rc, "rsg_encode_host")
+        return rc
+
+    def decode_host(self, stripes, is_erased, check=True):
+        """Restores erased information symbols of host-memory stripes in place (rsg_decode_host)."""
+        n, nsym, S = stripes.shape
+        er = np.ascontiguousarray(is_erased, dtype=np.bool_)
+        ptr = stripes.data_ptr() if hasattr(stripes, "data_ptr") else stripes.ctypes.data
+        rc = _lib.rsg_decode_host(self._h, P(ptr), nsym * S, S, n, S, _np_ptr(er), int(er.sum()))
+        if check and rc:
+            raise RSError(rc, "rsg_decode_host")
         return rc
 
     def encode_raw(self, d_info, info_stripe, info_sym, d_rep, rep_stripe, rep_sym, n, S, stream):

@@ -38,6 +38,12 @@ def body(kind):
             "mov": f"v_mov_b32 v{d}, v{a}",
             "xor_sdwa": f"v_xor_b32_sdwa v{d}, v{a}, v{b} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD",
             "idx_noswitch": f"v_xor_b32 v{d}, v40, v{d}",
+            # accumulate patterns of the XOR kernel's rows: destination also a source
+            "b3_rmw0": f"v_bitop3_b32 v{d}, v{d}, v{a}, v{b} bitop3:0x96",
+            "b3_rmw2": f"v_bitop3_b32 v{d}, v{a}, v{b}, v{d} bitop3:0x96",
+            "b3_new": f"v_bitop3_b32 v{d}, v{c}, v{a}, v{b} bitop3:0x96",
+            "xor_rmw": f"v_xor_b32 v{d}, v{a}, v{d}",
+            "xor_c0": f"v_xor_b32 v{d}, v40, v{b}",
         }
         if kind.startswith("dep"):  # d interleaved self-dependent chains
             dd = int(kind[3:-1])
@@ -58,7 +64,7 @@ def body(kind):
             raise ValueError(kind)
     return L
 
-KINDS = ["dep1x", "dep2x", "dep3x", "dep4x", "dep6x", "dep8x", "dep1a", "dep2a", "dep4a", "xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
+KINDS = ["b3_rmw0", "b3_rmw2", "b3_new", "xor_rmw", "xor_c0", "idx_noswitch", "xor", "bitop3_v"] if "--rmw" in sys.argv else ["dep1x", "dep2x", "dep3x", "dep4x", "dep6x", "dep8x", "dep1a", "dep2a", "dep4a", "xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
          "lshl_add", "lshl_or", "and_or", "or3", "bfi", "bfe", "perm_v", "perm_s", "alignbit", "pk_mul", "pk_mul_v",
          "mul_u24", "bitop3_s", "bitop3_v", "cndmask", "mov", "xor_sdwa", "idx_noswitch", "idx_sw2",
          "idx_sw4", "nop_sw2", "sadd_2"]
@@ -107,4 +113,4 @@ out.append(r'''int main() {
         }
     return 0;
 }''')
-open(sys.argv[1] if len(sys.argv) > 1 else "issue_bench.hip", "w").write("\n".join(out) + "\n")
+open(sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "issue_bench.hip", "w").write("\n".join(out) + "\n")

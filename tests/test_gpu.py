@@ -492,3 +492,32 @@ def test_drop_in_m16_large_symbols():
         got = np.stack(syms)
         assert np.array_equal(got[:k], want[:k]), f"call {rep}"
     rs.close()
+
+
+
+@pytest.mark.parametrize("k,r,S,n,pinned", [(128, 32, 65536, 30, True), (10, 4, 4096 + 24, 300, False),
+                                            (300, 70, 2048 + 10, 5, True)])
+def test_host_memory_batches(k, r, S, n, pinned):
+    """rsg_encode_host / rsg_decode_host on stripes in host memory (pinned and pageable; C3 shape in
+    two device batches; GF(2^16) code; tail columns): bit-exact vs the oracle."""
+    rng = np.random.default_rng(k + r + n)
+    host = torch.zeros((n, k + r, S), dtype=torch.uint8)
+    if pinned:
+        host = host.pin_memory()
+    host[:, :k] = torch.from_numpy(rng.integers(0, 256, (n, k, S), dtype=np.uint8))
+    codec = rs_amd.Codec(k, r)
+    codec.encode_host(host)
+    got = host.numpy().copy()
+    for s in range(0, n, max(1, n // 4)):
+        want = got[s].copy()
+        want[k:] = 0
+        assert oracle_encode(k, r, want) == 0
+        assert np.array_equal(got[s], want), f"encode stripe {s}"
+    er = np.zeros(k + r, bool)
+    er[1 + rng.choice(k + r - 1, r - 1, replace=False)] = True
+    er[0] = True  # r erasures, information slot 0 among them
+    host[:, torch.from_numpy(er)] = 0
+    codec.decode_host(host, er)
+    out = host.numpy()
+    assert np.array_equal(out[:, :k], got[:, :k])
+    assert not out[:, k:][:, er[k:]].any()  # erased repair slots are not written
