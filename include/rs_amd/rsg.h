@@ -77,7 +77,8 @@ int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64
  * HOST memory, pipelined over two streams (H2D -> kernel -> D2H per batch of up to 256 MiB, batches
  * overlapped). Synchronous: results are in host memory on return. Pinned memory (hipHostMalloc /
  * hipHostRegister) runs at PCIe rate; pageable memory works, slower. Any even symbol_size and byte
- * strides. rsg_decode_host copies whole stripes in and only the restored information symbols out. */
+ * strides. rsg_decode_host copies only surviving symbols in and only the restored information symbols
+ * out. */
 int rsg_encode_host(rsg_codec_t* c, const void* h_info, uint64_t info_stripe_stride, uint64_t info_symbol_stride,
                     void* h_rep, uint64_t rep_stripe_stride, uint64_t rep_symbol_stride, uint64_t n_stripes,
                     uint64_t symbol_size);

@@ -833,18 +833,35 @@ extern "C" int rsg_decode_host(rsg_codec_t* c, void* h_rcv, uint64_t stripe_stri
     const uint64_t P = (S + 15) & ~uint64_t(15), per = n * P;
     const uint64_t B = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kHostBatchBytes / per));
     if (int rc = host_pipe_reserve(c, size_t(B * per))) return rc;
-    const bool reg = stripe_stride == n * symbol_stride;
+    // surviving slots in runs of consecutive slots: with rows packed in host and device memory
+    // (symbol_stride == S == P) a run of every stripe of a batch is one strided copy, erased slots are
+    // never transferred (the decoder does not read them)
+    std::vector<std::pair<uint64_t, uint64_t>> runs;  // [first slot, count)
+    for (uint64_t i = 0; i < n;) {
+        if (is_erased[i]) {
+            ++i;
+            continue;
+        }
+        uint64_t j = i;
+        while (j < n && !is_erased[j]) ++j;
+        runs.emplace_back(i, j - i);
+        i = j;
+    }
+    const bool packed_rows = symbol_stride == S && S == P;
     uint8_t* h = static_cast<uint8_t*>(h_rcv);
     for (uint64_t s0 = 0, it = 0; s0 < n_stripes; s0 += B, ++it) {
         const uint64_t nb = std::min(B, n_stripes - s0);
         hipStream_t st = c->hs[it & 1];
         uint8_t* d = c->hbuf[it & 1];  // [nb][k + r][P]
-        if (reg)
-            HIP_TRY(hipMemcpy2DAsync(d, P, h + s0 * stripe_stride, symbol_stride, S, nb * n, hipMemcpyHostToDevice, st));
+        if (packed_rows)
+            for (const auto& run : runs)
+                HIP_TRY(hipMemcpy2DAsync(d + run.first * P, n * P, h + s0 * stripe_stride + run.first * S, stripe_stride,
+                                         run.second * S, nb, hipMemcpyHostToDevice, st));
         else
-            for (uint64_t b = 0; b < nb; ++b)
-                HIP_TRY(hipMemcpy2DAsync(d + b * n * P, P, h + (s0 + b) * stripe_stride, symbol_stride, S, n,
-                                         hipMemcpyHostToDevice, st));
+            for (const auto& run : runs)  // per slot: the slot of every stripe of the batch
+                for (uint64_t i = run.first; i < run.first + run.second; ++i)
+                    HIP_TRY(hipMemcpy2DAsync(d + i * P, n * P, h + s0 * stripe_stride + i * symbol_stride,
+                                             stripe_stride, S, nb, hipMemcpyHostToDevice, st));
         if (int rc = rsg_decode(c, d, n * P, P, nb, S, is_erased, t, st)) return rc;
         for (int i : lost)  // restored slot i of every stripe of the batch: one strided copy
             HIP_TRY(hipMemcpy2DAsync(h + s0 * stripe_stride + uint64_t(i) * symbol_stride, stripe_stride,

@@ -137,5 +137,5 @@ assert torch.equal(h_all[:, :k], h_info)
 out["host_api_encode_GBps"] = round(n_b * (k + r) * S / t_enc / 1e9, 2)
 out["host_api_decode_GBps"] = round(n_b * (k + t) * S / t_dec / 1e9, 2)
 out["host_api"] = (f"rsg_encode_host / rsg_decode_host, {n_b} pinned stripes: encode copies k symbols in and r "
-                   f"out, decode copies the whole stripe in and only the t restored symbols out")
+                   f"out, decode copies the surviving symbols in and only the t restored symbols out")
 print(json.dumps(out))
