@@ -148,6 +148,7 @@ struct XjConfig {
     int nt = 0;        // cache policy bits on the global loads / stores: 1 = nt loads, 2 = nt stores, 3 = both
     int lds = 0;       // > 0: per-wave LDS-DMA prefetch ring of `lds` group pairs (2 KiB each); 0: direct loads
     int share = 0;     // 1 (two roles): each role builds one group's subset tables, exchanged via LDS
+    int kreg = 1;      // finish step constants: 1 = in VGPRs (4-byte VOP2 forms), 0 = literals
     int lfin = 0;      // finish: 0 = VALU Horner over z (above); 1 = Horner in gamma through a 128 KiB LDS
                        // table T[w] = gamma * w (persistent kernel, one workgroup per CU)
     explicit XjConfig(int R = 0) {
@@ -164,6 +165,7 @@ struct XjConfig {
         env("RS_XJ_NT", nt);
         env("RS_XJ_FIN", lfin);
         env("RS_XJ_SHARE", share);
+        env("RS_XJ_KREG", kreg);
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
@@ -182,11 +184,11 @@ struct XjConfig {
     // after the XOR network: result of output q, and per-chain temporaries (chains run in batches of 8)
     int fin(int q) const { return ring_base() + q; }
     int tmp(int q, int k) const { return ring_base() + opr + 2 * (q % 8) + k; }
-    int cst() const { return ring_base() + opr + 16; }
+    int cst() const { return ring_base() + opr + 16; }  // cst .. cst + 2 <= max_vgpr: opr <= 8 ring + 3
     std::string tag() const {
-        char b[112];
-        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d", opr,
-                      ring, buffer, spread, horner, ablate, lds, nt, lfin, share);
+        char b[128];
+        std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
+                      opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
         return b;
     }
 };
@@ -230,7 +232,13 @@ std::vector<std::string> finish_block(const XjConfig& C) {
     std::vector<std::string> L;
     L.push_back("s_branch L_xj_fin_end");
     L.push_back("L_xj_fin:");
-    if (C.horner) L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0x2d002d");
+    if (C.horner) {
+        L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0x2d002d");
+    } else if (C.kreg) {  // step constants in VGPRs: 4-byte VOP2 forms issue faster than literal ones (bank_bench)
+        L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0xfffeffff");
+        L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 1) + ", 0x10001");
+        L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 2) + ", 0x8016");
+    }
     for (int q0 = 0; q0 < C.opr; q0 += 8) {
         const int nc = std::min(8, C.opr - q0);
         std::vector<std::vector<std::string>> chains(static_cast<size_t>(nc));
@@ -277,10 +285,17 @@ std::vector<std::string> finish_block(const XjConfig& C) {
                     add("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x78", H, T1, T2, C.cst());  // T1 ^ (T2 & C)
                     fold(H, v, 0);
                 } else {
-                    add("v_and_b32 v%d, 0xfffeffff, v%d", T1, cur);
-                    add("v_lshrrev_b32 v%d, 1, v%d", T1, T1);
-                    add("v_and_b32 v%d, 0x10001, v%d", T2, cur);
-                    add("v_mul_u32_u24 v%d, 0x8016, v%d", T2, T2);
+                    if (C.kreg) {
+                        add("v_and_b32 v%d, v%d, v%d", T1, C.cst(), cur);
+                        add("v_lshrrev_b32 v%d, 1, v%d", T1, T1);
+                        add("v_and_b32 v%d, v%d, v%d", T2, C.cst() + 1, cur);
+                        add("v_mul_u32_u24 v%d, v%d, v%d", T2, C.cst() + 2, T2);
+                    } else {
+                        add("v_and_b32 v%d, 0xfffeffff, v%d", T1, cur);
+                        add("v_lshrrev_b32 v%d, 1, v%d", T1, T1);
+                        add("v_and_b32 v%d, 0x10001, v%d", T2, cur);
+                        add("v_mul_u32_u24 v%d, 0x8016, v%d", T2, T2);
+                    }
                     if (v.empty()) {
                         add("v_xor_b32 v%d, v%d, v%d", H, T1, T2);
                     } else {
