@@ -333,6 +333,13 @@ struct rsg_codec {
     // rsg_decode_batch with device-built per-stripe plans (k_plan_m8): 0 = host plans per distinct
     // pattern, 1 = device plans, 2 = device plans when more than kHostPlanGroups patterns (default)
     int batch_plans = 2;
+    // device-plan decodes of m <= 8 codes: 1 = syndrome route (fixed r x (k + r) syndrome matrix on the
+    // XOR kernel, then a per-stripe t_info x t solve), 0 = per-stripe survivor matrices (k_plan_m8)
+    int syn_route = 1;
+    std::unique_ptr<DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
+    bool syn_failed = false;
+    void* d_syn = nullptr;  // [chunk][r][S] syndromes
+    size_t syn_cap = 0;
     uint16_t* d_elem = nullptr;  // [k + r] slot elements alpha^position
     void *d_masks = nullptr, *d_kr = nullptr, *d_pin = nullptr, *d_pout = nullptr, *d_pidx = nullptr;
     size_t masks_cap = 0, kr_cap = 0, pin_cap = 0, pout_cap = 0, pidx_cap = 0;
@@ -355,7 +362,7 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial})
+                        d_partial, d_syn})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -487,6 +494,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "syn_route")) {
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->syn_route = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "batch_plans")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
         c->batch_plans = int(value);
@@ -502,7 +514,7 @@ static int scratch_release(rsg_codec_t* c, hipStream_t st);
 
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
-                    const int32_t* d_ids = nullptr) {
+                    const int32_t* d_ids = nullptr, bool dst_local = false) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
     const int64_t align = p.m == 8 ? 8 : 4;
     if ((S & 1) || (uintptr_t(src) % align) || (uintptr_t(dst) % align) || (src_stripe % align) ||
@@ -510,7 +522,9 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
     ++p.uses;
-    const bool policy = p.m == 8 && p.d_idx && (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || p.uses >= c->dec_jit_uses)));
+    const bool policy = p.m == 8 && p.d_idx &&
+                        (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || &p == c->syn.get() ||
+                                                          p.uses >= c->dec_jit_uses)));
     // bit-plane XOR kernel: slot * stride must fit the kernel's 32-bit scalar offsets
     int64_t max_in = 0, max_out = 0;
     for (int32_t v : p.in_slots) max_in = std::max<int64_t>(max_in, v);
@@ -525,6 +539,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
             p.xj.reset();
         }
     }
+    if (dst_local && !(xj_ok && p.xj)) return RS_ERR_INVALID;  // only the XOR kernel indexes dst locally
     const bool jit_ok = policy && !(xj_ok && p.xj) && !p.jit_failed && jit_supported(8, p.K, p.R);
     if (jit_ok && !p.jit) {
         const Gamma8& g = gamma8();
@@ -574,6 +589,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         x.src_sym = int32_t(src_sym);
         x.dst_sym = int32_t(dst_sym);
         x.ids = d_ids;
+        x.dst_local = dst_local ? 1u : 0u;
         c->last_kernel = p.xj->name;
         // 256-byte column chunks up to the last full 2 KiB boundary; the rest by the generic tail kernel
         int rc = xj_launch(*p.xj, x, int64_t(n_stripes), (a.nbytes / 2048) * (2048 / kXjChunk), st);
@@ -665,6 +681,36 @@ static int scratch_release(rsg_codec_t* c, hipStream_t st) {
 // host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
 constexpr size_t kHostPlanGroups = 16;
 
+// Syndrome route eligibility: the r x (k + r) syndrome matrix H[j][i] = X_i^j runs on its bit-plane XOR
+// kernel (built once per codec), which covers whole 2 KiB column blocks only.
+static bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
+    const int n = int(c->k) + c->r;
+    if (!c->syn_route || c->syn_failed || !c->xj || c->jit == 0 || c->m > 8 || S % 2048 || !xj_supported(8, n, c->r) ||
+        int64_t(n) * symbol_stride >= (int64_t(1) << 31) || int64_t(c->r) * int64_t(S) >= (int64_t(1) << 31))
+        return false;
+    if (!c->syn) {
+        const Field& F = field();
+        std::vector<uint16_t> H(size_t(c->r) * n);
+        for (int j = 0; j < c->r; ++j)
+            for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(c->positions[i]) * j) % kN];
+        std::vector<int32_t> in(n), out(c->r);
+        for (int i = 0; i < n; ++i) in[size_t(i)] = i;
+        for (int j = 0; j < c->r; ++j) out[size_t(j)] = j;
+        std::unique_ptr<DevPlan> p;
+        if (build_plan(c->device, 8, std::move(H), n, c->r, std::move(in), std::move(out), p) || !p) {
+            c->syn_failed = true;
+            return false;
+        }
+        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj) || !p->xj) {
+            std::fprintf(stderr, "librs_amd: syndrome XOR kernel unavailable; per-stripe survivor plans\n");
+            c->syn_failed = true;
+            return false;
+        }
+        c->syn = std::move(p);
+    }
+    return true;
+}
+
 // rsg_decode_batch for m <= 8 codes with device-built plans: k_plan_m8 turns each selected stripe's
 // erasure mask into its decode matrix (nibble records of the V = 1 kernel), then one V = 1 launch (+
 // the tail kernel) applies every stripe's own plan. Stripes without erased information slots are
@@ -714,6 +760,64 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
     HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (syn_prepare(c, S, symbol_stride)) {
+        // syndrome route: zero erased information slots + build the t_info x t solves (k_plan_syn_m8),
+        // the r syndromes of every selected stripe into scratch (XOR kernel, dst indexed by the chunk-
+        // local stripe), then the per-stripe solves from the syndromes into the erased information slots
+        const uint16_t* expt = nullptr;
+        if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
+        const int64_t per = int64_t(c->r) * int64_t(S);
+        const int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t(1) << 30) / per));
+        if ((rc = grow(&c->d_syn, c->syn_cap, size_t(sch * per)))) return rc;
+        for (int64_t c0 = 0; c0 < nsel; c0 += sch) {
+            const int64_t cn = std::min(sch, nsel - c0);
+            SynPlanArgs pa{};
+            pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+            pa.elem = c->d_elem;
+            pa.logt = logt;
+            pa.expt = expt;
+            pa.g8 = g8;
+            pa.k = c->k;
+            pa.r = c->r;
+            pa.n = int32_t(n);
+            pa.kr = static_cast<int32_t*>(c->d_kr);
+            pa.pin = static_cast<int32_t*>(c->d_pin);
+            pa.pout = static_cast<int32_t*>(c->d_pout);
+            pa.pidx = static_cast<uint32_t*>(c->d_pidx);
+            pa.in_stride = in_stride;
+            pa.out_stride = out_stride;
+            pa.idx_stride = idx_stride;
+            pa.base = base;
+            pa.stripe_stride = stripe_stride;
+            pa.symbol_stride = symbol_stride;
+            pa.S = int64_t(S);
+            pa.ids = c->d_ids + c0;
+            HIP_TRY(launch_plan_syn_m8(pa, cn, st));
+            uint8_t* syn = static_cast<uint8_t*>(c->d_syn);
+            if ((rc = run_plan(c, *c->syn, base, stripe_stride, symbol_stride, syn, per, int64_t(S), uint64_t(cn), S,
+                               st, c->d_ids + c0, true)))
+                return rc;
+            V1Args v{};
+            v.src = syn;
+            v.src_stripe = 0;  // slots are local * r + j
+            v.src_sym = int64_t(S);
+            v.in_idx = pa.pin;
+            v.dst = base;
+            v.dst_stripe = stripe_stride;
+            v.dst_sym = symbol_stride;
+            v.out_idx = pa.pout;
+            v.ltab = c->d_ltab;
+            v.idx = pa.pidx;
+            v.ids = c->d_ids + c0;
+            v.ps_kr = pa.kr;
+            v.ps_in = in_stride;
+            v.ps_out = out_stride;
+            v.ps_idx = idx_stride;
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+        }
+        c->last_kernel = "syn_xj+apply_m8_v1_ps";
+        return scratch_release(c, st);
+    }
     for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {
         const int64_t cn = std::min(chunk, nsel - c0);
         PlanArgs pa{};

@@ -924,6 +924,98 @@ __global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
     }
 }
 
+// Syndrome-route plans (SynPlanArgs). With E the erased slots (t <= r) and P(x) = prod_{e in E}(x + X_e),
+// the reference's evaluator / Forney steps (reed_solomon.c:186-336) solve the t x t Vandermonde system
+// sum_{e in E} X_e^j d_e = S_j, j < t, over the syndromes of fft_transform_cycl (fft.c:39-100, erased
+// slots read as zero). Its inverse is W[p][j] = q_{p,j} / Q_p(X_p), q_p the coefficients of
+// Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Garbage in
+// erased repair slots only shifts their own (unused) unknowns; erased information slots are zeroed here.
+__global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
+    __shared__ uint16_t ee[256], pe[256];
+    __shared__ int32_t ps[256];
+    __shared__ uint16_t cf[2][257];
+    __shared__ int cnt[4][2];
+    constexpr uint32_t N = 65535u;
+    const int64_t s = blockIdx.x;
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const bool valid = j < a.n;
+    const bool er = valid && a.masks[s * a.n + j] != 0;
+    const uint64_t be = __ballot(er), bp = __ballot(er && j < a.k);
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    if (lane == 0) {
+        cnt[w][0] = __popcll(be);
+        cnt[w][1] = __popcll(bp);
+    }
+    __syncthreads();
+    int oe = 0, op = 0, t = 0, R = 0;
+    for (int v = 0; v < 4; ++v) {
+        if (v < w) oe += cnt[v][0], op += cnt[v][1];
+        t += cnt[v][0], R += cnt[v][1];
+    }
+    if (er) {
+        const uint16_t xj = a.elem[j];
+        ee[oe + __popcll(be & below)] = xj;
+        if (j < a.k) {
+            const int i = op + __popcll(bp & below);
+            pe[i] = xj;
+            ps[i] = j;
+        }
+    }
+    auto gmul = [&](uint32_t x, uint32_t y) -> uint32_t {
+        return (x && y) ? a.expt[(uint32_t(a.logt[x]) + a.logt[y]) % N] : 0u;
+    };
+    // P(x) = prod (x + X_e), coefficients cf[.][0..t]
+    if (j <= 256) cf[0][j] = j == 0 ? 1 : 0;
+    if (j == 0) cf[0][256] = 0;
+    __syncthreads();
+    int cur = 0;
+    for (int e = 0; e < t; ++e) {
+        const uint32_t xe = ee[e];
+        if (j <= e + 1) cf[cur ^ 1][j] = uint16_t((j ? cf[cur][j - 1] : 0u) ^ (j <= e ? gmul(xe, cf[cur][j]) : 0u));
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (j == 0) {
+        a.kr[2 * s] = t;
+        a.kr[2 * s + 1] = R;
+    }
+    int32_t* pin = a.pin + s * a.in_stride;
+    for (int q = j; q < a.in_stride; q += 256) pin[q] = q < t ? int32_t(s * a.r + q) : 0;
+    int32_t* pout = a.pout + s * a.out_stride;
+    for (int p = j; p < a.out_stride; p += 256) pout[p] = p < R ? ps[p] : 0;
+    // row j of the records: synthetic division of P by (x + X_p), q_{t-1} = 1, q_{i-1} = c_i + X_p q_i
+    uint32_t* rec = a.pidx + s * a.idx_stride;
+    const int ntiles = (R + 31) / 32;
+    if (j < ntiles * 32) {
+        const int tile = j >> 5, jj = j & 31;
+        uint32_t* r0 = rec + size_t(tile) * t * 64;
+        if (j < R) {
+            const uint32_t xp = pe[j];
+            uint32_t ld = 0;  // log prod_{e != p} (X_p + X_e)
+            for (int e = 0; e < t; ++e)
+                if (ee[e] != xp) ld += a.logt[xp ^ ee[e]];
+            ld %= N;
+            uint32_t q = 1;
+            for (int i = t - 1; i >= 0; --i) {
+                uint32_t b = 0;
+                if (q) b = a.g8[((uint32_t(a.logt[q]) + N - ld) % N) / 257u];
+                r0[size_t(i) * 64 + jj] = b & 15u;
+                r0[size_t(i) * 64 + 32 + jj] = b >> 4;
+                if (i > 0) q = cf[cur][i] ^ gmul(xp, q);
+            }
+        } else {
+            for (int i = 0; i < t; ++i) r0[size_t(i) * 64 + jj] = r0[size_t(i) * 64 + 32 + jj] = 0u;
+        }
+    }
+    // zero the erased information slots of this stripe (8-byte stores; S, bases and strides are 8-aligned)
+    uint8_t* sb = a.base + int64_t(a.ids[s]) * a.stripe_stride;
+    const int64_t words = a.S / 8;
+    for (int p = 0; p < R; ++p) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(sb + int64_t(ps[p]) * a.symbol_stride);
+        for (int64_t x = j; x < words; x += 256) d[x] = 0;
+    }
+}
+
 // Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
 // coefficients from the nibble records, multiplication by masked gamma-multiples.
 __global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0, int64_t nbytes) {
@@ -1045,6 +1137,12 @@ hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
     if (n_sel <= 0) return hipSuccess;
     if (a.n > 256) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_plan_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_plan_syn_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

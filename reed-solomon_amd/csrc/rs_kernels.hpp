@@ -50,6 +50,28 @@ struct PlanArgs {
 };
 hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st);
 
+// Syndrome route of rsg_decode_batch (m <= 8): per selected stripe, the t_info x t matrix W that maps
+// the first t syndromes S_j = sum_i X_i^j rcv_i to the erased information symbols (V = 1 nibble
+// records; inputs are syndrome slots local * r + j of the syndrome scratch), and zeroes the stripe's
+// erased information slots (the syndrome pass reads every slot).
+struct SynPlanArgs {
+    const uint8_t* masks;  // [n_sel][n] 1 = erased
+    const uint16_t* elem;  // [n] X_j = alpha^position of slot j
+    const uint16_t* logt;  // [65536] discrete log
+    const uint16_t* expt;  // [65536] alpha^e, e < 65536
+    const uint8_t* g8;     // [255] gamma-basis byte of alpha^(257 e)
+    int32_t k, r, n;
+    int32_t* kr;           // [n_sel][2] inputs t, erased information slots R
+    int32_t* pin;          // [n_sel][in_stride] syndrome slots
+    int32_t* pout;         // [n_sel][out_stride] erased information slots
+    uint32_t* pidx;        // [n_sel][idx_stride] V = 1 nibble records
+    int64_t in_stride, out_stride, idx_stride;
+    uint8_t* base;         // stripes (erased information slots are zeroed)
+    int64_t stripe_stride, symbol_stride, S;
+    const int32_t* ids;    // [n_sel] stripe indices
+};
+hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st);
+
 // One GF(2^16) coding matrix built on the device (gf16.cpp:solve_matrix's evaluation) straight into
 // the m = 16 kernels' formats: coefficient tiles (k_apply_m16) and, if rec != null, the packed index
 // records of k_apply_m16_v1 (rt = 64). coef / rec must be zeroed by the caller.

@@ -650,7 +650,8 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
          "typedef unsigned short uint16_t; typedef long long int64_t; typedef unsigned long long uint64_t;\n"
          "typedef unsigned int xj_u4 __attribute__((ext_vector_type(4)));\n"
          "struct XJArgs { const uint8_t* src; int64_t src_stripe; uint8_t* dst; int64_t dst_stripe;"
-         " int32_t src_sym, dst_sym; const int32_t* ids; const uint16_t* tab; uint32_t nchunks, ncols; };\n"
+         " int32_t src_sym, dst_sym; const int32_t* ids; const uint16_t* tab; uint32_t nchunks, ncols,"
+         " dst_local; };\n"
       << "// K=" << K << " R=" << R << " roles=" << roles << " pairs=" << pairs << " " << C.tag() << "\n"
       << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles * pairs << ") rs_xj(XJArgs a) {\n";
     if (C.lfin) {
@@ -669,12 +670,14 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
           << pairs << "u) {\n"
              "  const uint32_t local = c / a.nchunks, chunk = c - local * a.nchunks;\n"
              "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[local] : (uint64_t)local;\n"
+             "  const uint64_t dstripe = a.dst_local ? (uint64_t)local : stripe;\n"
              "  const uint32_t col = chunk * 256u + (threadIdx.x & 63u) * 4u;\n";
     } else {
         o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds["
           << (C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
           << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
+             "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n"
              "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
              "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
@@ -683,7 +686,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
              "  {\n";
     }
     o << "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
-         "  const uint64_t db = (uint64_t)a.dst + stripe * (uint64_t)a.dst_stripe;\n"
+         "  const uint64_t db = (uint64_t)a.dst + dstripe * (uint64_t)a.dst_stripe;\n"
          "  const uint32_t sl = (uint32_t)sb, sh = (uint32_t)(sb >> 32), dl = (uint32_t)db, dh = (uint32_t)(db >> 32);\n"
          "  switch (role) {\n";
     std::string clob;
@@ -792,6 +795,7 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
             XJArgs a = a0;
             if (a.ids) {
                 a.ids += s0;
+                if (a.dst_local) a.dst += s0 * a.dst_stripe;
             } else {
                 a.src += s0 * a.src_stripe;
                 a.dst += s0 * a.dst_stripe;
@@ -826,6 +830,7 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
         XJArgs a = a0;
         if (a.ids) {
             a.ids += s0;
+            if (a.dst_local) a.dst += s0 * a.dst_stripe;
         } else {
             a.src += s0 * a.src_stripe;
             a.dst += s0 * a.dst_stripe;

@@ -35,6 +35,7 @@ struct XJArgs {
     const int32_t* ids;        // optional [n_stripes] stripe indices; null = 0..n-1
     const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch)
     uint32_t nchunks, ncols;   // persistent form: chunks per stripe, chunks in the launch (set by xj_launch)
+    uint32_t dst_local;        // 1: dst indexed by the launch-local stripe (ids only select the source)
 };
 
 struct XjKernel {

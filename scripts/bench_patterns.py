@@ -58,7 +58,11 @@ def run(codec, label, reps):
                       "GBps": round(alg / ms / 1e6, 1), "restored": ok, "kernel": codec.last_kernel}), flush=True)
 
 
-run(rs_amd.Codec(k, r, batch_plans=1), "device_plans", 5)
+syn = rs_amd.Codec(k, r, batch_plans=1)
+run(syn, "device_plans_syndrome", 5)
+sur = rs_amd.Codec(k, r, batch_plans=1)
+sur.set_option("syn_route", 0)
+run(sur, "device_plans_survivor", 5)
 run(rs_amd.Codec(k, r, batch_plans=0), "host_plans", 2)
 # the same bytes with one shared pattern (t = r information erasures): generic and specialised kernels
 one = np.zeros(k + r, bool)

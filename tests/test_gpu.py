@@ -313,6 +313,48 @@ def test_decode_batch_device_plans_distinct_patterns(k, r, S, n):
             assert np.array_equal(got[s], want), f"stripe {s}"
 
 
+@pytest.mark.parametrize("route", [0, 1])
+@pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
+                                     (128, 32, 32768, 1030)])
+def test_decode_batch_syndrome_route(k, r, S, n, route):
+    """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
+    the XOR kernel, then each stripe's t_info x t solve) and the survivor-matrix route (0). Erased slots
+    hold garbage, not zeros: information slots come back bit-exact vs the oracle (which reads erased
+    slots as zero), erased repair slots are left as they were. n = 1030 at 32 KiB spans two chunks of
+    the syndrome scratch."""
+    rng = np.random.default_rng(k + 3 * n + route)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xD5)
+    codec = rs_amd.Codec(k, r, batch_plans=1)
+    codec.set_option("syn_route", route)
+    codec.encode(dev)
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    pats[0, :] = False
+    pats[0, :r] = True  # r information erasures
+    pats[1, :] = False
+    pats[1, k:] = True  # repair slots only: nothing to restore
+    full = dev.clone()
+    mask = torch.from_numpy(pats).cuda()
+    garbage = torch.randint(0, 256, (int(pats.sum()), S), dtype=torch.uint8, device="cuda")
+    dev[mask] = garbage
+    poisoned = dev.clone()
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert codec.last_kernel == ("syn_xj+apply_m8_v1_ps" if route else "apply_m8_v1_ps")
+    assert torch.equal(dev[:, :k], full[:, :k])
+    rep_er = mask.clone()
+    rep_er[:, :k] = False
+    assert torch.equal(dev[rep_er], poisoned[rep_er])  # erased repair slots not written
+    assert torch.equal(dev[:, k:][~mask[:, k:]], full[:, k:][~mask[:, k:]])
+    for s in list(range(0, n, max(1, n // 6))) + [n - 1]:
+        want = poisoned[s].cpu().numpy()
+        want[pats[s]] = 0
+        assert oracle_decode(k, r, want, pats[s], int(pats[s].sum())) == 0
+        assert np.array_equal(dev[s, :k].cpu().numpy(), want[:k]), f"stripe {s}"
+
+
 @pytest.mark.parametrize("plans", [0, 1])
 @pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("S", [2048, 2048 + 264])
