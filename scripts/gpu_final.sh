@@ -14,5 +14,5 @@ bash scripts/gpu_traffic.sh rs_xj "$K" || exit 1
 cp gpurun_out/traffic.json profiles/traffic.json
 timeout -k 10 600 python bench.py > gpurun_out/final_bench.log 2>&1 || { tail -5 gpurun_out/final_bench.log; exit 1; }
 tail -1 gpurun_out/final_bench.log
-timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d gpurun_out/final_prof -o run -- python3 bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/final_prof.log 2>&1 || exit 1
+timeout -s KILL 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final_prof -o run -- python3 bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/final_prof.log 2>&1 || exit 1
 tail -1 gpurun_out/final_prof.log
