@@ -345,6 +345,14 @@ struct rsg_codec {
     size_t masks_cap = 0, kr_cap = 0, pin_cap = 0, pout_cap = 0, pidx_cap = 0;
     void* d_partial = nullptr;  // split-K partial products of small m = 16 launches
     size_t partial_cap = 0;
+    // rsg_decode_batch for GF(2^16) codes with many patterns: one reusable device plan, rebuilt on the
+    // stream for each pattern (batch_plan_m16); its lists go through two pinned staging buffers
+    std::unique_ptr<DevPlan> bp16;
+    void* d_bp16 = nullptr;      // [y: n u16][x: r u16][emit: r i32][lp: n u32][ld: r u32]
+    void* d_bp16_rec = nullptr;  // index records (the plan's d_idx when the pattern uses them)
+    uint8_t* h_bp16[2] = {nullptr, nullptr};
+    hipEvent_t bp16_ev[2] = {nullptr, nullptr};
+    bool bp16_rec_pending[2] = {false, false};
     // the scratch above is reused by every rsg_decode_batch call: the event marks the end of the last
     // call's launches (which may be on another stream) and is waited for before the next overwrite
     hipEvent_t scratch_ev = nullptr;
@@ -357,12 +365,17 @@ struct rsg_codec {
     ~rsg_codec() {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
+        if (bp16) bp16->d_idx = nullptr;  // d_bp16_rec, freed below
+        for (int i = 0; i < 2; ++i) {
+            if (bp16_ev[i]) (void)hipEventDestroy(bp16_ev[i]);
+            if (h_bp16[i]) (void)hipHostFree(h_bp16[i]);
+        }
         for (int i = 0; i < 2; ++i) {
             if (hs[i]) (void)hipStreamDestroy(hs[i]);
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn})
+                        d_partial, d_syn, d_bp16, d_bp16_rec})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -976,6 +989,99 @@ extern "C" int rsg_decode_host(rsg_codec_t* c, void* h_rcv, uint64_t stripe_stri
     return 0;
 }
 
+// rsg_decode_batch, GF(2^16) codes past kHostPlanGroups patterns: the codec's one batch plan is rebuilt
+// on the stream for every pattern by k_plan16_sums / k_plan16_fill -- the same evaluation and formats as
+// build_plan_m16_device, so results are identical -- instead of a cached plan per pattern (allocations,
+// synchronous uploads and, past 16 patterns, an eviction that frees device memory). Launches on one
+// stream are ordered, so the plan of the next pattern is written after the previous apply has read it;
+// only the host staging needs a ring (two pinned buffers, each guarded by the event after its copies).
+static size_t al16(size_t v) { return (v + 15) & ~size_t(15); }
+
+static int batch_plan_m16(rsg_codec_t* c, const bool* er, int slot, hipStream_t st, DevPlan** out) {
+    const Field& F = field();
+    const size_t n = size_t(c->k) + c->r, r = c->r;
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(c->positions, c->k, c->r, er, targets, emit, sources, in, outs);
+    const int K = int(sources.size()), R = int(emit.size()), d = int(targets.size());
+    if (R == 0 || size_t(K) > n || size_t(d) > r) return RS_ERR_INVALID;
+    const size_t o_x = al16(n * 2), o_emit = o_x + al16(r * 2), o_lp = o_emit + al16(r * 4), o_ld = o_lp + al16(n * 4);
+    const size_t dev_bytes = o_ld + al16(r * 4);
+    const size_t o_in = o_lp, o_out = o_in + al16((n + 16) * 4), host_bytes = o_out + al16((r + 64) * 4);
+    const size_t rec_cap = ((r + 63) / 64) * (n + 1) * 256;
+    if (!c->bp16) {
+        auto p = std::make_unique<DevPlan>();
+        p->device = c->device;
+        p->m = 16;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_coef), (r + 64) * n * 2));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_in), (n + 16) * 4));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_out), (r + 64) * 4));
+        if (!c->d_bp16) HIP_TRY(hipMalloc(&c->d_bp16, dev_bytes));
+        if (!c->d_bp16_rec && rec_cap <= (size_t(256) << 20)) HIP_TRY(hipMalloc(&c->d_bp16_rec, rec_cap));
+        for (int i = 0; i < 2; ++i) {
+            if (!c->h_bp16[i])
+                HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_bp16[i]), host_bytes, hipHostMallocDefault));
+            if (!c->bp16_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->bp16_ev[i], hipEventDisableTiming));
+        }
+        c->bp16 = std::move(p);
+    }
+    DevPlan& p = *c->bp16;
+    p.K = K;
+    p.R = R;
+    p.rt = apply_tile_rows(16, R);
+    p.ntiles = (R + p.rt - 1) / p.rt;
+    const size_t coef_bytes = size_t(p.ntiles) * size_t(K) * size_t(p.rt / 2) * 4;
+    const size_t rec_bytes = size_t(p.ntiles) * size_t(K + 1) * 256;
+    const bool records = p.rt == 64 && c->d_bp16_rec && rec_bytes <= (size_t(256) << 20);
+    p.d_idx = records ? static_cast<uint32_t*>(c->d_bp16_rec) : nullptr;
+    p.in_slots = in;
+    p.out_slots = outs;
+    p.out_slots.resize(std::max(size_t(p.ntiles) * p.rt, size_t((R + 31) / 32) * 32), 0);
+    p.uses = 0;
+    // stage the lists (the copies that last used this buffer are complete once its event is)
+    if (c->bp16_rec_pending[slot]) HIP_TRY(hipEventSynchronize(c->bp16_ev[slot]));
+    uint8_t* h = c->h_bp16[slot];
+    uint16_t* hy = reinterpret_cast<uint16_t*>(h);
+    uint16_t* hx = reinterpret_cast<uint16_t*>(h + o_x);
+    int32_t* he = reinterpret_cast<int32_t*>(h + o_emit);
+    int32_t* hin = reinterpret_cast<int32_t*>(h + o_in);
+    int32_t* hout = reinterpret_cast<int32_t*>(h + o_out);
+    for (int q = 0; q < K; ++q) hy[q] = F.exp[sources[size_t(q)]];
+    for (int e = 0; e < d; ++e) hx[e] = F.exp[targets[size_t(e)]];
+    for (int j = 0; j < R; ++j) he[j] = emit[size_t(j)];
+    for (int q = 0; q < K + 16; ++q) hin[q] = q < K ? in[size_t(q)] : 0;
+    for (size_t j = 0; j < p.out_slots.size(); ++j) hout[j] = p.out_slots[j];
+    HIP_TRY(hipMemcpyAsync(c->d_bp16, h, o_lp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p.d_in, hin, size_t(K + 16) * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p.d_out, hout, p.out_slots.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(c->bp16_ev[slot], st));
+    c->bp16_rec_pending[slot] = true;
+    HIP_TRY(hipMemsetAsync(p.d_coef, 0, coef_bytes, st));
+    if (records) HIP_TRY(hipMemsetAsync(p.d_idx, 0, rec_bytes, st));
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
+    uint8_t* dt = static_cast<uint8_t*>(c->d_bp16);
+    Plan16Args a{};
+    a.src_el = reinterpret_cast<const uint16_t*>(dt);
+    a.tgt_el = reinterpret_cast<const uint16_t*>(dt + o_x);
+    a.emit = reinterpret_cast<const int32_t*>(dt + o_emit);
+    a.logt = logt;
+    a.expt = expt;
+    a.lp = reinterpret_cast<uint32_t*>(dt + o_lp);
+    a.ld = reinterpret_cast<uint32_t*>(dt + o_ld);
+    a.coef = p.d_coef;
+    a.rec = records ? reinterpret_cast<uint8_t*>(p.d_idx) : nullptr;
+    a.K = K;
+    a.d = d;
+    a.R = R;
+    a.rt = p.rt;
+    HIP_TRY(launch_plan_m16(a, st));
+    *out = &p;
+    return 0;
+}
+
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
@@ -1020,13 +1126,16 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
     uint8_t* base = static_cast<uint8_t*>(d_rcv);
+    // GF(2^16) codes with many patterns: one plan rebuilt on the stream per pattern (batch_plan_m16)
+    const bool stream_plans = c->m > 8 && c->m16_plans != 0 &&
+                              (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups));
     size_t gi = 0;
     for (auto& g : groups) {
         std::unique_ptr<bool[]> er(new bool[n]);
         uint16_t t = 0;
         for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.first[i] != 0));
         DevPlan* p = nullptr;
-        int rc = decode_plan(c, er.get(), t, &p);
+        int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p);
         if (rc) return rc;
         rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
                       int64_t(symbol_stride), g.second.size(), symbol_size, st, c->d_ids + first[gi]);

@@ -1072,28 +1072,37 @@ __global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0
 }
 
 // ------------------------------------------------------------ GF(2^16) plans on the device
+// lp[q] = sum_e log(Y_q + X_e), ld[p] = sum_{e != p} log(X_p + X_e) (solve_matrix's log-sums): 16
+// lanes per item, each summing every 16th target, then a shuffle reduction (sums < 2^32 for d <= 65535)
 __global__ void __launch_bounds__(256) k_plan16_sums(Plan16Args a) {
-    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) >> 4;
+    const int part = int(threadIdx.x & 15);
     constexpr uint32_t N = 65535u;
-    if (i < a.K) {  // lp[q] = sum_e log(Y_q + X_e)
+    uint32_t acc = 0;
+    if (i < a.K) {
         const uint16_t y = a.src_el[i];
-        uint32_t acc = 0;
-        for (int e = 0; e < a.d; ++e) acc += a.logt[y ^ a.tgt_el[e]];
-        a.lp[i] = acc % N;
-    } else if (i < int64_t(a.K) + a.R) {  // ld[p] = sum_{e != p} log(X_p + X_e)
-        const int p = int(i - a.K), self = a.emit[p];
+        for (int e = part; e < a.d; e += 16) acc += a.logt[y ^ a.tgt_el[e]];
+    } else if (i < int64_t(a.K) + a.R) {
+        const int self = a.emit[i - a.K];
         const uint16_t x = a.tgt_el[self];
-        uint32_t acc = 0;
-        for (int e = 0; e < a.d; ++e)
+        for (int e = part; e < a.d; e += 16)
             if (e != self) acc += a.logt[x ^ a.tgt_el[e]];
-        a.ld[p] = acc % N;
+    }
+    for (int o = 8; o; o >>= 1) acc += __shfl_xor(acc, o, 16);
+    if (part == 0) {
+        if (i < a.K)
+            a.lp[i] = acc % N;
+        else if (i < int64_t(a.K) + a.R)
+            a.ld[i - a.K] = acc % N;
     }
 }
 
+// Coefficient (row, i) = alpha^(lp[i] - ld[row] - log(X_row + Y_i)), written into the coefficient tiles
+// and, for 64-row tiles, the packed index records. Grid (row blocks, sources): consecutive lanes take
+// consecutive rows of one source, so tile writes are contiguous and record bytes share one record.
 __global__ void __launch_bounds__(256) k_plan16_fill(Plan16Args a) {
-    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;  // row * K + i
-    if (e >= int64_t(a.R) * a.K) return;
-    const int row = int(e / a.K), i = int(e - int64_t(row) * a.K);
+    const int row = int(blockIdx.x) * 256 + int(threadIdx.x), i = int(blockIdx.y);
+    if (row >= a.R) return;
     constexpr uint32_t N = 65535u;
     const uint32_t L = (a.lp[i] + 2 * N - a.ld[row] - a.logt[a.tgt_el[a.emit[row]] ^ a.src_el[i]]) % N;
     const uint32_t c = a.expt[L];
@@ -1108,9 +1117,11 @@ __global__ void __launch_bounds__(256) k_plan16_fill(Plan16Args a) {
 }
 
 hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st) {
-    const int64_t nsum = int64_t(a.K) + a.R, nfill = int64_t(a.R) * a.K;
+    const int64_t nsum = (int64_t(a.K) + a.R) * 16;
+    if (a.K > 65535) return hipErrorInvalidValue;  // grid y of the fill (K <= k + r <= 65535)
     if (nsum > 0) hipLaunchKernelGGL(k_plan16_sums, dim3(unsigned((nsum + 255) / 256)), dim3(256), 0, st, a);
-    if (nfill > 0) hipLaunchKernelGGL(k_plan16_fill, dim3(unsigned((nfill + 255) / 256)), dim3(256), 0, st, a);
+    if (a.R > 0 && a.K > 0)
+        hipLaunchKernelGGL(k_plan16_fill, dim3(unsigned((a.R + 255) / 256), unsigned(a.K)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

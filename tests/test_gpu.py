@@ -313,6 +313,48 @@ def test_decode_batch_device_plans_distinct_patterns(k, r, S, n):
             assert np.array_equal(got[s], want), f"stripe {s}"
 
 
+@pytest.mark.parametrize("k,r,S,n", [(300, 200, 1024 + 8, 40), (4096, 1024, 1024, 24)])
+def test_decode_batch_m16_stream_plans(k, r, S, n):
+    """GF(2^16) codes with more than 16 distinct patterns in one rsg_decode_batch: the codec's batch plan
+    is rebuilt on the stream for every pattern (k_plan16_*). Information symbols come back on every
+    stripe (64-row asm tiles and the compiled kernel for R <= 32, split-K single-stripe launches,
+    repair-only stripes skipped); stripes bit-exact vs the oracle where it is quick, and the whole
+    batch byte-identical to the cached per-pattern plans (batch_plans=0)."""
+    rng = np.random.default_rng(k + n)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xD5)
+    codec = rs_amd.Codec(k, r)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        if s % 7 == 6:
+            pats[s, k + rng.choice(r, 3, replace=False)] = True  # repair-only: nothing to restore
+        else:
+            pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    pats[0, :] = False
+    pats[0, :r] = True  # r information erasures (largest plan)
+    pats[1, :] = False
+    pats[1, rng.choice(k, 20, replace=False)] = True  # R <= 32 (compiled kernel tiles)
+    poisoned = full.copy()
+    poisoned[pats] = 0
+    dev.copy_(torch.from_numpy(poisoned))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    for s in range(n):
+        assert np.array_equal(got[s, :k], full[s, :k]), f"stripe {s}"
+    for s in range(n) if k + r <= 1024 else []:
+        want = poisoned[s].copy()
+        assert oracle_decode(k, r, want, pats[s], int(pats[s].sum())) == 0
+        assert np.array_equal(got[s], want), f"stripe {s}"
+    dev.copy_(torch.from_numpy(poisoned))
+    assert rs_amd.Codec(k, r, batch_plans=0).decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), got)
+
+
 @pytest.mark.parametrize("route", [0, 1])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030)])
