@@ -139,16 +139,44 @@ struct DevPlan {
     std::unique_ptr<XjKernel> xj;    // bit-plane XOR kernel (rs_xj.hpp), if built
     bool xj_failed = false;
     int64_t uses = 0;                // launches of this plan (JIT policy)
+    void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
     ~DevPlan() {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(device);
-        (void)hipFree(d_in);
-        (void)hipFree(d_out);
-        (void)hipFree(d_coef);
-        (void)hipFree(d_idx);
+        if (blob) {
+            (void)hipFree(blob);
+        } else {
+            (void)hipFree(d_in);
+            (void)hipFree(d_out);
+            (void)hipFree(d_coef);
+            (void)hipFree(d_idx);
+        }
         (void)hipSetDevice(cur);
     }
+};
+
+// A plan's device arrays in one allocation, filled by one copy (a new decode pattern then costs one
+// hipMalloc + one upload instead of four of each, and one hipFree when the cache evicts it).
+struct PlanBlob {
+    std::vector<uint8_t> host;  // the uploaded prefix: every part added with a source
+    size_t total = 0;           // prefix + device-only parts (src = null, added after the prefix)
+    size_t add(const void* src, size_t bytes) {  // offset of a 256-byte aligned part
+        const size_t o = (total + 255) & ~size_t(255);
+        total = o + std::max<size_t>(bytes, 16);
+        if (src) {
+            host.resize(total, 0);
+            if (bytes) std::memcpy(host.data() + o, src, bytes);
+        }
+        return o;
+    }
+    int upload(DevPlan& p) {
+        HIP_TRY(hipMalloc(&p.blob, total));
+        HIP_TRY(hipMemcpy(p.blob, host.data(), host.size(), hipMemcpyHostToDevice));
+        return 0;
+    }
+    template <class T>
+    static T* at(DevPlan& p, size_t o) { return reinterpret_cast<T*>(static_cast<uint8_t*>(p.blob) + o); }
 };
 
 int upload(void** dst, const void* src, size_t bytes) {
@@ -192,6 +220,8 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     }
     out_slots.resize(std::max(size_t(p->ntiles) * rt, size_t((R + 31) / 32) * 32), 0);  // padded rows: never stored
     int rc;
+    PlanBlob blob;
+    size_t o_idx = SIZE_MAX;
     if (p->m == 8) {
         // gpr-index kernels (k_apply_m8_idx / _lds / _v1), 32-row tiles whatever p->rt is: record per
         // (tile, input) = 64 dwords, [j] = low, [32 + j] = high nibble of output j's coefficient
@@ -205,7 +235,7 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
                     idx[(size_t(t) * K + i) * 64 + j] = c & 15;
                     idx[(size_t(t) * K + i) * 64 + 32 + j] = c >> 4;
                 }
-        if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
+        o_idx = blob.add(idx.data(), idx.size() * 4);
     } else if (rt == 64 && size_t(p->ntiles) * (K + 1) * 256 <= (size_t(256) << 20)) {
         // k_apply_m16_v1: per (tile, input) 256 byte-sized table indices packed in 64 dwords (16 per
         // nibble plane n; output j's index 16n + nibble n in byte (j % 8) / 2 of the plane's dword
@@ -224,12 +254,17 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
                         rec[4 * dw + by] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
                     }
             }
-        if ((rc = upload(reinterpret_cast<void**>(&p->d_idx), idx.data(), idx.size() * 4))) return rc;
+        o_idx = blob.add(idx.data(), idx.size() * 4);
     }
     in_slots.resize(in_slots.size() + 16, 0);  // kernels read slot indices in vectors past the end
-    if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
-    if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
-    if ((rc = upload(reinterpret_cast<void**>(&p->d_coef), coef.data(), coef.size() * 4))) return rc;
+    const size_t o_in = blob.add(in_slots.data(), in_slots.size() * 4);
+    const size_t o_out = blob.add(out_slots.data(), out_slots.size() * 4);
+    const size_t o_coef = blob.add(coef.data(), coef.size() * 4);
+    if ((rc = blob.upload(*p))) return rc;
+    if (o_idx != SIZE_MAX) p->d_idx = PlanBlob::at<uint32_t>(*p, o_idx);
+    p->d_in = PlanBlob::at<int32_t>(*p, o_in);
+    p->d_out = PlanBlob::at<int32_t>(*p, o_out);
+    p->d_coef = PlanBlob::at<uint32_t>(*p, o_coef);
     p->matrix = std::move(M);
     in_slots.resize(size_t(K));
     p->in_slots = std::move(in_slots);
@@ -266,33 +301,37 @@ int build_plan_m16_device(int device, const std::vector<uint16_t>& targets, cons
     std::vector<uint16_t> y(static_cast<size_t>(K)), x(static_cast<size_t>(d));
     for (int q = 0; q < K; ++q) y[size_t(q)] = F.exp[sources[size_t(q)]];
     for (int e = 0; e < d; ++e) x[size_t(e)] = F.exp[targets[size_t(e)]];
-    void *d_y = nullptr, *d_x = nullptr, *d_emit = nullptr, *d_lp = nullptr, *d_ld = nullptr;
-    struct Tmp {  // temporaries of the build, freed on every return
-        void** v[5];
-        ~Tmp() {
-            for (void** q : v)
-                if (*q) (void)hipFree(*q);
-        }
-    } tmp{{&d_y, &d_x, &d_emit, &d_lp, &d_ld}};
-    if ((rc = upload(&d_y, y.data(), y.size() * 2)) || (rc = upload(&d_x, x.data(), x.size() * 2)) ||
-        (rc = upload(&d_emit, emit.data(), emit.size() * 4)))
-        return rc;
-    HIP_TRY(hipMalloc(&d_lp, std::max<size_t>(size_t(K) * 4, 16)));
-    HIP_TRY(hipMalloc(&d_ld, std::max<size_t>(size_t(R) * 4, 16)));
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_coef), std::max<size_t>(coef_bytes, 16)));
-    HIP_TRY(hipMemsetAsync(p->d_coef, 0, coef_bytes, nullptr));
-    if (records) {
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_idx), rec_bytes));
-        HIP_TRY(hipMemsetAsync(p->d_idx, 0, rec_bytes, nullptr));
-    }
+    // plan arrays in one allocation: [in][out] uploaded, then [coef][records] zeroed and filled on the
+    // device; the build's temporaries [y][x][emit][lp][ld] in a second one, freed on return
+    out_slots.resize(std::max(size_t(p->ntiles) * p->rt, size_t((R + 31) / 32) * 32), 0);
+    in_slots.resize(in_slots.size() + 16, 0);
+    PlanBlob blob;
+    const size_t o_in = blob.add(in_slots.data(), in_slots.size() * 4);
+    const size_t o_out = blob.add(out_slots.data(), out_slots.size() * 4);
+    const size_t up = blob.host.size();
+    const size_t o_coef = blob.add(nullptr, coef_bytes);
+    const size_t o_idx = records ? blob.add(nullptr, rec_bytes) : SIZE_MAX;
+    if ((rc = blob.upload(*p))) return rc;
+    HIP_TRY(hipMemsetAsync(PlanBlob::at<uint8_t>(*p, up), 0, blob.total - up, nullptr));
+    p->d_in = PlanBlob::at<int32_t>(*p, o_in);
+    p->d_out = PlanBlob::at<int32_t>(*p, o_out);
+    p->d_coef = PlanBlob::at<uint32_t>(*p, o_coef);
+    if (records) p->d_idx = PlanBlob::at<uint32_t>(*p, o_idx);
+    PlanBlob tb;
+    const size_t o_y = tb.add(y.data(), y.size() * 2), o_x = tb.add(x.data(), x.size() * 2);
+    const size_t o_emit = tb.add(emit.data(), emit.size() * 4);
+    const size_t o_lp = tb.add(nullptr, size_t(K) * 4), o_ld = tb.add(nullptr, size_t(R) * 4);
+    DevPlan tmp;  // owns the temporaries' allocation
+    tmp.device = device;
+    if ((rc = tb.upload(tmp))) return rc;
     Plan16Args a{};
-    a.src_el = static_cast<const uint16_t*>(d_y);
-    a.tgt_el = static_cast<const uint16_t*>(d_x);
-    a.emit = static_cast<const int32_t*>(d_emit);
+    a.src_el = PlanBlob::at<const uint16_t>(tmp, o_y);
+    a.tgt_el = PlanBlob::at<const uint16_t>(tmp, o_x);
+    a.emit = PlanBlob::at<const int32_t>(tmp, o_emit);
     a.logt = logt;
     a.expt = expt;
-    a.lp = static_cast<uint32_t*>(d_lp);
-    a.ld = static_cast<uint32_t*>(d_ld);
+    a.lp = PlanBlob::at<uint32_t>(tmp, o_lp);
+    a.ld = PlanBlob::at<uint32_t>(tmp, o_ld);
     a.coef = p->d_coef;
     a.rec = records ? reinterpret_cast<uint8_t*>(p->d_idx) : nullptr;
     a.K = K;
@@ -301,10 +340,6 @@ int build_plan_m16_device(int device, const std::vector<uint16_t>& targets, cons
     a.rt = p->rt;
     HIP_TRY(launch_plan_m16(a, nullptr));
     HIP_TRY(hipStreamSynchronize(nullptr));
-    out_slots.resize(std::max(size_t(p->ntiles) * p->rt, size_t((R + 31) / 32) * 32), 0);
-    in_slots.resize(in_slots.size() + 16, 0);
-    if ((rc = upload(reinterpret_cast<void**>(&p->d_in), in_slots.data(), in_slots.size() * 4))) return rc;
-    if ((rc = upload(reinterpret_cast<void**>(&p->d_out), out_slots.data(), out_slots.size() * 4))) return rc;
     in_slots.resize(size_t(K));
     p->in_slots = std::move(in_slots);
     p->out_slots = std::move(out_slots);
@@ -525,6 +560,8 @@ extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->las
 static int scratch_acquire(rsg_codec_t* c, hipStream_t st);
 static int scratch_release(rsg_codec_t* c, hipStream_t st);
 
+constexpr uint64_t kJitMinBytes = uint64_t(1) << 20;
+
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
                     const int32_t* d_ids = nullptr, bool dst_local = false) {
@@ -534,7 +571,9 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
         (src_sym % align) || (dst_stripe % align) || (dst_sym % align))
         return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
-    ++p.uses;
+    // a decode plan is specialised (hiprtc) after dec_jit_uses launches that each move at least
+    // kJitMinBytes: a compile costs far more than tiny launches (one C1 / C2 stripe per call) can recover
+    if (uint64_t(p.K + p.R) * S * n_stripes >= kJitMinBytes) ++p.uses;
     const bool policy = p.m == 8 && p.d_idx &&
                         (c->jit == 1 || (c->jit == 2 && (&p == c->enc.get() || &p == c->syn.get() ||
                                                           p.uses >= c->dec_jit_uses)));
