@@ -39,7 +39,7 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * indexing; 1 = masked multiples; 10-19 timing ablations), "jit" (matrix-specialised kernels
  * compiled with hiprtc and cached on disk: 0 = off, 1 = every eligible matrix, 2 = the encode matrix
  * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
- * before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
+ * of at least 1 MiB before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
  * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
  * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default), "syn_route"
  * (device-plan decodes of m <= 8 codes with symbol sizes a multiple of 2 KiB: 1 = syndromes of every slot on
