@@ -2,7 +2,8 @@
 symbol sizes with and without tail columns, stripe counts and erasure patterns, through every kernel
 path: matrix-specialised XOR kernels (jit=1), generic GF(256) kernels (jit=0), GF(2^16) codes
 (hand-scheduled kernel, split-K on small grids, device-built plans), and rsg_decode_batch with a
-pattern per stripe (device-built plans). Prints one JSON line per case and a summary."""
+pattern per stripe (device-built plans; for GF(2^16) codes, "batch16", one plan rebuilt on the stream
+per pattern). Prints one JSON line per case and a summary."""
 import json
 import os
 import sys
@@ -28,17 +29,21 @@ def one(family):
     if family in ("xj", "generic", "batch"):
         k = int(rng.integers(1, 200))
         r = int(rng.integers(1, min(255 - k, 80) + 1))
-    else:  # m16
+    elif family == "m16":
         k = int(rng.integers(200, 1500))
         r = int(rng.integers(max(1, 256 - k), 300))
+    else:  # batch16: GF(2^16) codes, small enough for the oracle to check every stripe quickly
+        k = int(rng.integers(150, 500))
+        r = int(rng.integers(max(1, 256 - k), 160))
     S = int(rng.choice([2048, 4096, 8192, 1024])) + 8 * int(rng.integers(0, 64)) * int(rng.integers(0, 2))
-    if family == "m16":
-        S = min(S, 4096)
-    n = int(rng.integers(1, 5)) if family != "batch" else int(rng.integers(20, 60))
+    if family in ("m16", "batch16"):
+        S = min(S, 4096 if family == "m16" else 2048)
+    n = int(rng.integers(1, 5)) if family not in ("batch", "batch16") else int(rng.integers(20, 60))
     host = np.zeros((n, k + r, S), np.uint8)
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
-    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "batch": dict(batch_plans=1)}[family]
+    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "batch": dict(batch_plans=1),
+          "batch16": dict(batch_plans=1)}[family]
     codec = rs_amd.Codec(k, r, **kw)
     codec.encode(dev)
     torch.cuda.synchronize()
@@ -48,7 +53,7 @@ def one(family):
     for s in range(n):
         assert oracle_encode(k, r, want[s]) == 0
     ok = bool(np.array_equal(got, want))
-    if family == "batch":
+    if family in ("batch", "batch16"):
         pats = np.zeros((n, k + r), bool)
         for s in range(n):
             pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
@@ -75,7 +80,7 @@ def one(family):
     return dict(family=family, k=k, r=r, S=S, stripes=n, encode=enc_kernel, decode=dec_kernel, ok=ok)
 
 
-families = ["xj", "generic", "m16", "batch"]
+families = ["xj", "generic", "m16", "batch", "batch16"]
 i = 0
 while time.time() < t_end:
     fam = families[i % len(families)]
