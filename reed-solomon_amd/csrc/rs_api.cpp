@@ -1338,8 +1338,9 @@ struct Impl {
             rsg_codec* c = nullptr;
             int rc = rsg_codec_create(device, k, r, &c);
             if (rc) return rc;
-            // one call launches up to kMaxChunks decodes: specialise a pattern from its third call on
-            c->dec_jit_uses = 2 * kMaxChunks + 1;
+            // a decode call launches once until its plan is specialised (rs_restore_symbols):
+            // specialise a pattern from its third call on
+            c->dec_jit_uses = 3;
             it = codecs.emplace(key, std::unique_ptr<rsg_codec>(c)).first;
         }
         *out = it->second.get();
@@ -1467,7 +1468,13 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    const size_t P = pad16(S), W = chunk_width(S), nch = (S + W - 1) / W, nl = lost.size();
+    // A plan not yet specialised runs the generic kernel, whose few workgroups per column chunk leave the
+    // chip mostly idle (one C3 stripe: 16 per 16 KiB chunk, 87 us a launch): one launch over the whole
+    // symbol then beats the copy / kernel pipeline over kMaxChunks column chunks.
+    DevPlan* dplan = nullptr;
+    if ((rc = decode_plan(c, is_erased, t, &dplan))) return rc;
+    const size_t P = pad16(S), W = (dplan->xj || dplan->jit) ? chunk_width(S) : S, nch = (S + W - 1) / W,
+                 nl = lost.size();
     // erased slots are neither gathered nor read by the decoder. Only restored rows come back: the span
     // lost[0] .. lost.back() when it is (nearly) contiguous, else the rows packed on the device behind
     // the stripe (k_gather_rows) and copied as one block
