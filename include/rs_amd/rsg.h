@@ -41,7 +41,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
  * of at least 1 MiB before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
  * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
- * 1 = device-built per-stripe plans, 2 = device plans above 16 distinct patterns, the default), "syn_route"
+ * 1 = device-built plans -- per stripe for m <= 8, rebuilt on the stream per pattern for GF(2^16) codes --,
+ * 2 = device plans above 16 distinct patterns, the default), "syn_route"
  * (device-plan decodes of m <= 8 codes with symbol sizes a multiple of 2 KiB: 1 = syndromes of every slot on
  * the bit-plane XOR kernel, then a per-stripe t_info x t solve, the default; 0 = per-stripe survivor
  * matrices), "m16_mode"
