@@ -785,10 +785,16 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
 int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes) {
     // split K when the grid would leave most CUs idle (one workgroup walks all K inputs serially):
     // aim for >= 512 workgroups, slices of >= 64 inputs, at most 32 slices, within the scratch
+    // (RS_AMD_KSLICES overrides the slice cap for experiments; target = 16 workgroups per slice cap)
+    static const int64_t cap = [] {
+        const char* e = std::getenv("RS_AMD_KSLICES");
+        const long v = e ? std::atol(e) : 32;
+        return int64_t(v >= 2 && v <= 256 ? v : 32);
+    }();
     const int64_t full = a.nbytes / 1024, tiles = (a.R + 63) / 64;
     const int64_t blocks = n_stripes * full * tiles;
     if (blocks <= 0 || blocks >= 256) return 1;
-    int64_t s = std::min<int64_t>({(512 + blocks - 1) / blocks, int64_t(a.K) / 64, 32});
+    int64_t s = std::min<int64_t>({(16 * cap + blocks - 1) / blocks, int64_t(a.K) / 64, cap});
     const int64_t per = n_stripes * tiles * 64 * full * 1024;  // partial bytes per slice
     if (!scratch_bytes) s = std::min<int64_t>(s, per > 0 ? a.scratch_bytes / per : 0);
     if (s < 2) return 1;
