@@ -7,57 +7,57 @@ every stripe (read k, write r symbols) + decode every stripe with t = r erased i
 (read the k survivors, write the t restored symbols), in place through the C ABI.
 Byte accounting: encode (k + r) * S, decode (k + t) * S per stripe.
 
-Multi-GPU: one process per GPU (torchrun), stripes partitioned, no data-path collective; the timed
-region is bracketed by barriers and the max time over ranks is reported (weak scaling).
+Multi-GPU: one process per GPU, stripes partitioned, no data-path collective; the timed region is
+bracketed by barriers and the max time over ranks is reported (weak scaling). `--gpus N` without a
+torchrun environment spawns the N rank processes itself (before anything touches a GPU) and relays
+rank 0's line; under torchrun, --gpus must equal WORLD_SIZE.
 
 Also reported: the dominant kernel's roofline fraction (HIP-event timing of each launch on the
 stream it runs on), and the CPU baseline -- the reference src/rs built from source
-(oracle/_ref/librs_ref.so) or, if absent, the clean-room oracle -- timed on this host's cores on a
-bounded sample of the same workload.
+(oracle/_ref/librs_ref.so) on a pthread pool of this host's cores (oracle/cpu_baseline.c), or, if
+that build is absent, the clean-room port, labelled as such -- on a bounded sample of the workload.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
-import threading
 import time
 
 import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "reed-solomon_amd"))
-import rs_amd  # noqa: E402  (raises if librs_amd.so is missing: no fallback)
-import rs_dist  # noqa: E402
-from srchash import kernel_src_hash  # noqa: E402
-
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")  # scripts/traffic.py output
+SEED = 0x5EED
+METRIC = "encode+decode GB/s (device-resident) at k/r/symbol_len; % HBM roofline"  # BASELINE.json
 
 
 def measured_traffic(kernel, cfg):
     """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters on this configuration
     (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches: the
-    exact kernel name for JIT kernels (content-addressed), name + source hash for compiled ones."""
+    exact kernel name for JIT kernels (content-addressed), name + source hash for compiled ones.
+    traffic.json holds one record per (kernel, config)."""
+    from srchash import kernel_src_hash
     try:
         with open(TRAFFIC_JSON) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("config") != cfg:
-        return None
-    if "[" in str(kernel):  # JIT kernel: its name carries the hash of its generated source
-        if t.get("bench_kernel") != kernel:
-            return None
-    elif t.get("bench_kernel") != kernel or t.get("src_hash") != kernel_src_hash(kernel):
-        return None
-    return int(t["traffic_bytes"])
-SEED = 0x5EED
+    for rec in t.get("records", [t]):
+        if rec.get("config") != cfg or rec.get("bench_kernel") != kernel:
+            continue
+        if "[" not in str(kernel) and rec.get("src_hash") != kernel_src_hash(kernel):
+            continue
+        return int(rec["traffic_bytes"])
+    return None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -66,128 +66,144 @@ def parse():
     ap.add_argument("--r", type=int, default=32)
     ap.add_argument("--symbol", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c", "m16p"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c"],
                     help="auto = library default policy (matrix-specialised kernels, generic fallback)")
     ap.add_argument("--cpu-stripes", type=int, default=128, help="CPU-baseline sample (stripes, resident)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (passes repeat)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-only", action="store_true", help="skip verification/CPU legs (profilers)")
     ap.add_argument("--scatter", type=int, default=0, metavar="STRIPES",
                     help="N>1: also time an RCCL scatter of STRIPES stripes per rank from rank 0 (and the gather of "
                          "their repair symbols back), outside the timed region; reported as 'scatter'")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks run the launch / barrier / max-over-ranks protocol with no coding work "
+                         "(tests the multi-rank harness on CPU); the line says dry_run")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------ rank launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`--gpus N` outside torchrun: start N rank processes (this script, RANK/LOCAL_RANK/WORLD_SIZE set,
+    rendezvous on 127.0.0.1) and wait for them. This process never touches a GPU (the device count
+    below does not initialise one on this image); rank 0 prints the JSON line. A failing rank stops
+    the others. Returns the exit code."""
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            print(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for rank in range(n):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for i in sorted(live):
+            c = procs[i].poll()
+            if c is None:
+                continue
+            live.discard(i)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for j in live:
+                    procs[j].terminate()
+        time.sleep(0.05)
+    return rc
 
 
 # ------------------------------------------------------------------------------ CPU baseline
-class _Sym(ctypes.Structure):
-    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8))]
-
-
-class _Seq(ctypes.Structure):
-    _fields_ = [("length", ctypes.c_size_t), ("symbol_size", ctypes.c_size_t),
-                ("symbols", ctypes.POINTER(ctypes.POINTER(_Sym)))]
-
-
-def _seq(buf, first, count, S):
-    syms = (_Sym * count)()
-    ptrs = (ctypes.POINTER(_Sym) * count)()
-    for i in range(count):
-        syms[i].data = buf[first + i].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
-        ptrs[i] = ctypes.pointer(syms[i])
-    return _Seq(count, S, ptrs), (syms, ptrs)
+def cpu_cores():
+    """(cores this process may run on, cgroup CPU quota in cores or None)."""
+    avail = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota> <period>" or "max <period>"
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f1, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f2:
+                q, p = int(f1.read()), int(f2.read())
+                if q > 0:
+                    quota = max(1, q // p)
+        except (OSError, ValueError):
+            pass
+    return avail, quota
 
 
 def cpu_baseline(args, erased, gpu_sample):
-    """Times encode + decode of `cpu_stripes` stripes on `cpu_threads` host threads.
-    Returns (baseline dict, parity ok)."""
+    """Times encode + decode of `cpu_stripes` resident stripes with the reference CPU path on a pthread
+    pool (oracle/cpu_baseline.c: one context per thread, views built before the clock). Returns
+    (baseline dict, parity ok)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from _util import gen_info
     k, r, S = args.k, args.r, args.symbol
     t = int(erased.sum())
     n = args.cpu_stripes
     ref_so = os.path.join(REPO, "oracle", "_ref", "librs_ref.so")
+    port_so = os.path.join(REPO, "oracle", "librs_oracle.so")
+    drv_so = os.path.join(REPO, "oracle", "libcpu_baseline.so")
     kind = "reference" if os.path.exists(ref_so) else "port"
+    drv = ctypes.CDLL(drv_so)
+    drv.cpub_run.restype = ctypes.c_int
+    drv.cpub_run.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    avail, quota = cpu_cores()
+    threads = args.cpu_threads or (min(avail, quota) if quota else avail)
+    threads = max(1, min(threads, n))
     stripes = np.zeros((n, k + r, S), np.uint8)
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from _util import gen_info, oracle
     for s in range(n):
         stripes[s, :k] = gen_info(SEED, s, k * S).reshape(k, S)
+    er = np.ascontiguousarray(erased, np.bool_)
 
-    if kind == "reference":
-        lib = ctypes.CDLL(ref_so)
-        lib.rs_create.restype = ctypes.c_void_p
-        lib.rs_destroy.argtypes = [ctypes.c_void_p]
-        lib.rs_generate_repair_symbols.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Seq), ctypes.POINTER(_Seq)]
-        lib.rs_restore_symbols.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint16, ctypes.POINTER(_Seq),
-                                           ctypes.c_void_p, ctypes.c_uint16]
-        er = np.ascontiguousarray(erased, np.bool_)
+    def run(op, passes, nt, cnt):
+        sec = ctypes.c_double()
+        rc = drv.cpub_run((ref_so if kind == "reference" else port_so).encode(), 0 if kind == "reference" else 1,
+                          k, r, S, stripes.ctypes.data, cnt, er.ctypes.data, t, op, passes, nt, ctypes.byref(sec))
+        if rc:
+            raise RuntimeError(f"cpu baseline ({kind}) failed with {rc}")
+        return sec.value
 
-        def work(lo, hi, dec, errs):
-            rs = lib.rs_create()
-            for s in range(lo, hi):
-                buf = stripes[s]
-                if not dec:
-                    inf, keep1 = _seq(buf, 0, k, S)
-                    rep, keep2 = _seq(buf, k, r, S)
-                    errs.append(lib.rs_generate_repair_symbols(rs, ctypes.byref(inf), ctypes.byref(rep)))
-                else:
-                    rcv, keep = _seq(buf, 0, k + r, S)
-                    errs.append(lib.rs_restore_symbols(rs, k, r, ctypes.byref(rcv), er.ctypes.data, t))
-            lib.rs_destroy(rs)
-
-        def run(dec, nt=None, cnt=n):
-            nt = min(args.cpu_threads if nt is None else nt, cnt)
-            errs, ths = [], []
-            for i in range(nt):
-                th = threading.Thread(target=work, args=(cnt * i // nt, cnt * (i + 1) // nt, dec, errs))
-                ths.append(th)
-            t0 = time.perf_counter()
-            for th in ths:
-                th.start()
-            for th in ths:
-                th.join()
-            dt = time.perf_counter() - t0
-            assert not any(errs), errs
-            return dt
-    else:
-        o = oracle()
-        er = np.ascontiguousarray(erased, np.bool_)
-
-        def run(dec, nt=None, cnt=n):
-            nt = args.cpu_threads if nt is None else nt
-            t0 = time.perf_counter()
-            if dec:
-                rc = o.orc_decode_many(k, r, S, stripes.ctypes.data, cnt, er.ctypes.data, t, nt)
-            else:
-                rc = o.orc_encode_many(k, r, S, stripes.ctypes.data, cnt, nt)
-            assert rc == 0
-            return time.perf_counter() - t0
-
-    # bounded sample: passes over the resident stripes repeat until the time budget is spent
-    t_enc, p_enc = run(False), 1
+    # bounded sample: passes over the resident stripes, sized from the first pass to the time budget
+    t_enc, p_enc = run(0, 1, threads, n), 1
     parity = all(np.array_equal(stripes[s], gpu_sample[s]) for s in range(min(len(gpu_sample), n)))
-    while t_enc < args.cpu_seconds / 2:
-        t_enc += run(False)
-        p_enc += 1
+    more = int(max(0.0, args.cpu_seconds / 2 - t_enc) / max(t_enc, 1e-9))
+    if more:
+        t_enc += run(0, more, threads, n)
+        p_enc += more
     info = stripes[:, :k].copy()
-    t_dec, p_dec = 0.0, 0
-    while p_dec == 0 or t_dec < args.cpu_seconds / 2:
-        stripes[:, erased] = 0  # the reference requires erased slots to be zero (untimed)
-        t_dec += run(True)
-        p_dec += 1
+    t_dec, p_dec = run(1, 1, threads, n), 1
+    more = int(max(0.0, args.cpu_seconds / 2 - t_dec) / max(t_dec, 1e-9))
+    if more:
+        t_dec += run(1, more, threads, n)
+        p_dec += more
     parity = parity and np.array_equal(stripes[:, :k], info)
-    bytes_total = n * ((k + r) * p_enc + (k + t) * p_dec) * S
-    gbs = bytes_total / (t_enc + t_dec) / 1e9
-    threads = min(args.cpu_threads, n)
-    # single core, same code, a few stripes (SURVEY.md 8d: all-core and single-core rates)
+    gbs = n * ((k + r) * p_enc + (k + t) * p_dec) * S / (t_enc + t_dec) / 1e9
+    # single core, same driver, a few stripes (SURVEY.md 8d: all-core and single-core rates)
     c1 = min(n, 4)
-    t1e, t1d = run(False, 1, c1), 0.0
-    stripes[:c1, erased] = 0
-    t1d = run(True, 1, c1)
-    gbs1 = c1 * ((k + r) + (k + t)) * S / (t1e + t1d) / 1e9
-    return dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind, single_core=round(gbs1, 4),
-                sample=f"{n} resident stripes of k={k} r={r} S={S}: {p_enc} encode + {p_dec} decode (t={t}) "
-                       f"passes, {threads} threads, {t_enc + t_dec:.1f} s; single_core: {c1} stripes, "
-                       f"1 thread, {t1e + t1d:.1f} s"), parity
+    t1 = run(0, 1, 1, c1) + run(1, 1, 1, c1)
+    gbs1 = c1 * ((k + r) + (k + t)) * S / t1 / 1e9
+    label = kind if kind == "reference" else "port (oracle/_ref/librs_ref.so absent: clean-room restatement timed)"
+    return dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind, cores_available=avail, cpu_quota=quota,
+                single_core=round(gbs1, 4),
+                sample=f"{label}: {n} resident stripes of k={k} r={r} S={S}, {p_enc} encode + {p_dec} decode (t={t}) "
+                       f"passes on {threads} pthreads ({avail} cores available, quota {quota}), "
+                       f"{t_enc + t_dec:.1f} s; single_core: {c1} stripes, 1 thread, {t1:.2f} s"), parity
 
 
 # ------------------------------------------------------------------- stripes from one rank
@@ -196,6 +212,8 @@ def scatter_leg(args, rank, world, dev):
     symbols to their owners (rs_dist.scatter_stripes, one P2P group, one xGMI link per peer) and the
     gather of the repair symbols back. Timed on its own (barrier-bracketed, max over ranks); never
     part of `value`."""
+    import torch
+    import rs_dist
     k, r, S, m = args.k, args.r, args.symbol, args.scatter
     src = torch.empty((world * m if rank == 0 else 1, k, S), dtype=torch.uint8, device=dev)
     if rank == 0:
@@ -217,10 +235,85 @@ def scatter_leg(args, rank, world, dev):
             "gather_ms": round(t_ga.max_elapsed * 1e3, 3), "check": "ok" if ok else "MISMATCH"}
 
 
+def per_rank_times(enc_ms, dec_ms, dev):
+    """[{rank, encode_ms, decode_ms}] of every rank (all_gather; one entry without a process group)."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([enc_ms, dec_ms], dtype=torch.float64, device=dev)
+    if not (dist.is_available() and dist.is_initialized()):
+        parts = [mine]
+    else:
+        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, mine)
+    return [{"rank": i, "encode_ms": round(float(p[0]), 3), "decode_ms": round(float(p[1]), 3)}
+            for i, p in enumerate(parts)]
+
+
+def base_line(args, world, n, k, r, S, t, elapsed):
+    total_bytes = n * ((k + r) * S + (k + t) * S) * world * args.steps
+    return {
+        "metric": METRIC,
+        "value": round(total_bytes / elapsed / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16 (GF(2^16) words)",
+        "data": "synthetic (counter-based splitmix64 stripes generated in HBM)",
+        "config": {"workload": f"k={k} r={r} symbol={S}B stripes/gpu={n} decode t={t} (info erasures "
+                               f"at i*{max(k // max(r, 1), 1)})", "stripes_total": n * world,
+                   "parallelism": f"stripes x{world}"},
+    }
+
+
+# ------------------------------------------------------------------------------ dry run (CPU)
+def dry_run_main(args, rank, world):
+    """The multi-rank protocol without a GPU: gloo process group, the same barrier-bracketed timed
+    region and max-over-ranks reduction, per-rank times gathered, no coding work (step = a no-op)."""
+    import torch
+    import torch.distributed as dist
+    import rs_dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, k, r, S = args.stripes, args.k, args.r, args.symbol
+    with rs_dist.TimedRegion(None) as region:
+        for _ in range(args.steps):
+            time.sleep(0.001 * (1 + rank))
+    line = base_line(args, world, n, k, r, S, r, region.max_elapsed)
+    line["dry_run"] = True
+    line["value"] = None  # no coding work ran: there is no throughput to report
+    line["data"] = "dry run: no GPU work, harness protocol only"
+    line["rccl_world"] = dist.get_world_size() if dist.is_initialized() else 1
+    line["per_rank"] = per_rank_times(region.elapsed * 1e3, 0.0, "cpu")
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))  # parent: no GPU touched, children do the work
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} does not match WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    import rs_dist
     rank, world, local = rs_dist.env()
+    if args.dry_run:
+        return dry_run_main(args, rank, world)
+
+    import torch
+    if world > torch.cuda.device_count():
+        print(f"bench.py: WORLD_SIZE {world} exceeds the {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+        sys.exit(2)
+    import rs_amd  # raises if librs_amd.so is missing: no fallback
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -230,11 +323,12 @@ def main():
     k, r, S, n = args.k, args.r, args.symbol, args.stripes
     erased = rs_amd.bench_pattern(k, r)
     t = int(erased.sum())
-    opts = {"auto": {}, "jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(jit=0, m8_mode=18), "idx": dict(jit=0, m8_mode=2),
-            "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1), "m16c": {}, "m16p": {}}[args.kernel]
+    opts = {"auto": {}, "jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(jit=0, m8_mode=18),
+            "idx": dict(jit=0, m8_mode=2), "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1),
+            "m16c": {}}[args.kernel]
     codec = rs_amd.Codec(k, r, device=local, **opts)
-    if args.kernel in ("m16c", "m16p"):  # GF(2^16) codes: compiled kernel / asm timing ablation (wrong results)
-        codec.set_option("m16_mode", 2 if args.kernel == "m16c" else 1)
+    if args.kernel == "m16c":  # GF(2^16) codes: the compiled kernel
+        codec.set_option("m16_mode", 2)
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     stripe0, _ = rs_dist.weak_shard(n, rank)  # this rank's global stripe ids: [stripe0, stripe0 + n)
@@ -268,8 +362,7 @@ def main():
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     enc_bytes = n * (k + r) * S
     dec_bytes = n * (k + t) * S
-    total_bytes = (enc_bytes + dec_bytes) * world * args.steps
-    value = total_bytes / elapsed / 1e9
+    per_rank = per_rank_times(enc_ms, dec_ms, dev)
 
     # verification: restored information == generated information (fingerprints), sampled repair
     parity = "skipped"
@@ -301,30 +394,17 @@ def main():
     dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, kern_enc) if enc_ms >= dec_ms else (dec_ms, dec_bytes, kern_dec)
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
     traffic = measured_traffic(dom_name, f"k{k}_r{r}_S{S}_n{n}_t{t}")
-    line = {
-        "metric": "encode+decode GB/s (device-resident) at k/r/symbol_len; % HBM roofline",  # BASELINE.json
-        "value": round(value, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u16 (GF(2^16) words)",
-        "data": "synthetic (counter-based splitmix64 stripes generated in HBM)",
-        "config": {"workload": f"k={k} r={r} symbol={S}B stripes/gpu={n} decode t={t} (info erasures "
-                               f"at i*{k // r})", "stripes_total": n * world, "parallelism": f"stripes x{world}",
-                   "kernel": {"encode": kern_enc, "decode": kern_dec}},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes},
-        "encode_ms": round(enc_ms, 3),
-        "decode_ms": round(dec_ms, 3),
-        "cpu_baseline": cpu,
-        "parity": parity,
-    }
+    line = base_line(args, world, n, k, r, S, t, elapsed)
+    line["config"]["kernel"] = {"encode": kern_enc, "decode": kern_dec}
+    line["rccl_world"] = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes}
+    line["encode_ms"] = round(enc_ms, 3)
+    line["decode_ms"] = round(dec_ms, 3)
+    line["per_rank"] = per_rank
+    line["cpu_baseline"] = cpu
+    line["parity"] = parity
     if scatter is not None:
         line["scatter"] = scatter
     if rank == 0:

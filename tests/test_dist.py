@@ -140,3 +140,29 @@ def test_scatter_gather_from_rank0_gloo():
         assert oracle_encode(K, R, buf) == 0
         want.append(buf[K:])
     assert res[0][2] == np.stack(want).tobytes()
+
+
+def _bench_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return __import__("json").loads(lines[0])
+
+
+def test_bench_launcher_spawns_ranks_dry_run():
+    """`bench.py --gpus 2` outside torchrun starts two rank processes itself (gloo dry run here): the
+    line reports both ranks, the whole-job stripe count and per-rank times; a --gpus / WORLD_SIZE
+    mismatch is fatal."""
+    import subprocess
+    bench = os.path.join(HERE, "..", "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run", "--steps", "2", "--stripes", "64"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr
+    line = _bench_line(p.stdout)
+    assert line["n_gpus"] == 2 and line["rccl_world"] == 2
+    assert line["config"]["stripes_total"] == 2 * 64
+    assert [e["rank"] for e in line["per_rank"]] == [0, 1]
+    assert line["dry_run"] is True and line["value"] is None
+    bad = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run"], capture_output=True, text=True,
+                         timeout=120, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert bad.returncode == 2 and "does not match" in bad.stderr
