@@ -32,7 +32,11 @@ extern "C" {
 
 using namespace rsamd;
 
-#define RSG_VERSION "rs_amd 0.1 (gfx950)"
+#ifdef RS_AMD_DIAG
+#define RSG_VERSION "rs_amd 0.2 (gfx950, DIAGNOSTIC build: timing ablations enabled)"
+#else
+#define RSG_VERSION "rs_amd 0.2 (gfx950)"
+#endif
 
 static int hip_fail(hipError_t e, const char* what) {
     std::fprintf(stderr, "librs_amd: %s failed: %s\n", what, hipGetErrorString(e));
@@ -500,14 +504,19 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value < 0 || (value > 4 && value < 10) || value > 20) return RS_ERR_INVALID;
+        if (value < 0 || (value > 4 && value < 10) || value > 19) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 10-13, 15, 16, 19: timing ablations with wrong results; 17: s_memtime stamps
+        if ((value >= 10 && value <= 13) || (value >= 15 && value <= 17) || value == 19) return RS_ERR_INVALID;
+#endif
         c->m8_mode = int(value);
         return 0;
     }
+#ifdef RS_AMD_DIAG
     if (!std::strcmp(name, "stamp_buffer")) {  // device pointer, [blocks * 4][4] uint64 (mode 17)
         c->stamps = reinterpret_cast<uint64_t*>(static_cast<uintptr_t>(value));
         return 0;
     }
+#endif
     if (!std::strcmp(name, "xj")) {
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->xj = int(value);
@@ -525,6 +534,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     if (!std::strcmp(name, "m16_mode")) {
         if (value < 0 || value > 2) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 1: timing ablation with wrong results, diagnostic build only
+        if (value == 1) return RS_ERR_INVALID;
+#endif
         c->m16_mode = int(value);
         return 0;
     }

@@ -694,10 +694,12 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
             if (full > 0) {
                 const V1Args v = v1_args(a, full, nullptr);
                 dim3 g(unsigned(n_stripes * full), grid.y);
-                if (a.mode == 18)
-                    hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
-                else
+#ifdef RS_AMD_DIAG
+                if (a.mode == 19)
                     hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
+                else
+#endif
+                    hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
             }
             launch_m8_tail(a, n_stripes, grid.y, st);
         } else if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15) || a.mode == 17) {
@@ -706,16 +708,18 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
             if (f.nchunks > 0) {
                 dim3 g(unsigned(n_stripes * f.nchunks), grid.y);
                 switch (a.mode) {
+                case 14: hipLaunchKernelGGL((k_apply_m8_lds<5>), g, dim3(256), 0, st, f, a.in_idx); break;
+#ifdef RS_AMD_DIAG  // timing ablations (wrong results) and stamps: diagnostic build only (make diag)
                 case 10: hipLaunchKernelGGL((k_apply_m8_lds<1>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 11: hipLaunchKernelGGL((k_apply_m8_lds<2>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 12: hipLaunchKernelGGL((k_apply_m8_lds<3>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 13: hipLaunchKernelGGL((k_apply_m8_lds<4>), g, dim3(256), 0, st, f, a.in_idx); break;
-                case 14: hipLaunchKernelGGL((k_apply_m8_lds<5>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 15: hipLaunchKernelGGL((k_apply_m8_lds<6>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 17:  // production kernel with s_memtime phase counters (needs a.stamps)
                     if (!a.stamps) return hipErrorInvalidValue;
                     hipLaunchKernelGGL((k_apply_m8_lds<0, true>), g, dim3(256), 0, st, f, a.in_idx);
                     break;
+#endif
                 default: hipLaunchKernelGGL((k_apply_m8_lds<0>), g, dim3(256), 0, st, f, a.in_idx); break;
                 }
             }
@@ -728,8 +732,10 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
             }
         } else if (a.mode == 4) {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 8>), grid, dim3(256), 0, st, a, a.in_idx);
-        } else if (a.mode == 16) {  // loads only, register ring 4
+#ifdef RS_AMD_DIAG
+        } else if (a.mode == 16) {  // loads only, register ring 4 (timing ablation, wrong results)
             hipLaunchKernelGGL((k_apply_m8_idx<4, 4>), grid, dim3(256), 0, st, a, a.in_idx);
+#endif
         } else {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), grid, dim3(256), 0, st, a, a.in_idx);
         }
@@ -759,10 +765,12 @@ static hipError_t launch_m16(const ApplyArgs& a, int64_t n_stripes, hipStream_t 
             v.tiles = int(tiles);
             dim3 g = v.units ? dim3(unsigned((units + 7) / 8 * 8 * tiles), 1, 1)
                              : dim3(unsigned(units), tiles, unsigned(v.kslices));
-            if (a.mode == 0)
-                hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
-            else
+#ifdef RS_AMD_DIAG
+            if (a.mode == 1)  // fixed-register timing ablation (wrong results)
                 hipLaunchKernelGGL((k_apply_m16_v1<1>), g, dim3(256), 0, st, v);
+            else
+#endif
+                hipLaunchKernelGGL((k_apply_m16_v1<0>), g, dim3(256), 0, st, v);
             if (v.kslices > 1) {
                 const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
                 hipLaunchKernelGGL(k_xor_slices, dim3(unsigned((rows + 255) / 256), unsigned(n_stripes)), dim3(256), 0,

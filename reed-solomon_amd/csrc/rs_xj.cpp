@@ -160,7 +160,9 @@ struct XjConfig {
         env("RS_XJ_BUFFER", buffer);
         env("RS_XJ_SPREAD", spread);
         env("RS_XJ_HORNER", horner);
+#ifdef RS_AMD_DIAG  // timing ablations produce wrong results: diagnostic build only
         env("RS_XJ_ABLATE", ablate);
+#endif
         env("RS_XJ_LDS", lds);
         env("RS_XJ_NT", nt);
         env("RS_XJ_FIN", lfin);
@@ -785,7 +787,11 @@ XjDevState* xj_dev_state(int device) {
 
 int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nchunks, hipStream_t st) {
     if (n_stripes <= 0 || nchunks <= 0) return 0;
+#ifdef RS_AMD_DIAG  // every stripe reads and writes stripe 0 (wrong results): diagnostic build only
     static const bool alias = std::getenv("RS_XJ_ALIAS") && std::atoi(std::getenv("RS_XJ_ALIAS"));
+#else
+    constexpr bool alias = false;
+#endif
     if (k.pairs > 0) {  // persistent form: one workgroup per CU loops over all (stripe, chunk) columns
         XjDevState* d = xj_dev_state(k.device);
         if (!d) return 3;

@@ -17,7 +17,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librs_amd.so")
+# RS_AMD_LIB selects another build of the library (the diagnostic librs_amd_diag.so of the sweep
+# scripts); the default is the product build
+LIB_PATH = os.environ.get("RS_AMD_LIB") or os.path.join(HERE, "librs_amd.so")
 
 RS_OK = 0
 RS_ERR_ALLOC = 1

@@ -4,6 +4,8 @@ import os, sys, json
 import numpy as np
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd"))
+# ablation modes exist only in the diagnostic build (make -C reed-solomon_amd diag)
+os.environ.setdefault("RS_AMD_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "reed-solomon_amd", "librs_amd_diag.so"))
 import rs_amd
 k, r, S, n = 128, 32, 65536, int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")

@@ -2,6 +2,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
+export RS_AMD_LIB=$GRAFT_REPO_ROOT/reed-solomon_amd/librs_amd_diag.so  # RS_XJ_ALIAS: diagnostic build only
 D=gpurun_out/clock
 mkdir -p $D
 for v in 0 1; do

@@ -605,3 +605,42 @@ def test_host_memory_batches(k, r, S, n, pinned):
     out = host.numpy()
     assert np.array_equal(out[:, :k], got[:, :k])
     assert not out[:, k:][:, er[k:]].any()  # erased repair slots are not written
+
+
+def test_release_build_ignores_diagnostic_knobs():
+    """The product library rejects the ablation options (RS_ERR_INVALID) and ignores the ablation
+    environment variables: with RS_XJ_ABLATE / RS_XJ_ALIAS set, a fresh process still encodes and
+    decodes bit-exactly through the XOR kernel."""
+    codec = rs_amd.Codec(128, 32)
+    for name, value in [("m8_mode", v) for v in (10, 11, 12, 13, 15, 16, 17, 19)] + [("m16_mode", 1), ("stamp_buffer", 1)]:
+        with pytest.raises(rs_amd.RSError):
+            codec.set_option(name, value)
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import numpy as np, torch, rs_amd, sys
+sys.path.insert(0, sys.argv[1])
+from _util import gen_info, oracle_encode, oracle_decode
+k, r, S, n = 128, 32, 4096, 3
+host = np.zeros((n, k + r, S), np.uint8)
+for s in range(n): host[s, :k] = gen_info(7, s, k * S).reshape(k, S)
+dev = torch.from_numpy(host).cuda()
+c = rs_amd.Codec(k, r)
+c.encode(dev); torch.cuda.synchronize()
+assert c.last_kernel.startswith("rs_xj"), c.last_kernel
+got = dev.cpu().numpy()
+for s in range(n):
+    want = host[s].copy(); assert oracle_encode(k, r, want) == 0
+    assert np.array_equal(got[s], want), s
+er = rs_amd.bench_pattern(k, r)
+for _ in range(2):
+    dev[:, torch.from_numpy(er)] = 0xA5
+    c.decode(dev, er); torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy()[:, :k], got[:, :k])
+print("ok", c.last_kernel)
+"""
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, RS_XJ_ABLATE="1", RS_XJ_ALIAS="1", PYTHONPATH=os.path.dirname(rs_amd.__file__))
+    p = subprocess.run([sys.executable, "-c", code, here], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and p.stdout.startswith("ok rs_xj"), p.stdout + p.stderr

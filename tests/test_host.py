@@ -183,3 +183,14 @@ def test_invalid_arguments():
     with pytest.raises(rs_amd.RSError) as e:
         rs_amd.coding_matrix(4, 2, er)
     assert e.value.rc == rs_amd.RS_ERR_CANNOT_RESTORE
+
+
+def test_release_build_has_no_ablation_kernels():
+    """Timing ablations (wrong results by construction) live only in the diagnostic build
+    (make diag -> librs_amd_diag.so); the product library must not contain them."""
+    import subprocess
+    out = subprocess.run(["nm", "-C", rs_amd.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    for bad in ("k_apply_m8_lds<1", "k_apply_m8_lds<2", "k_apply_m8_lds<3", "k_apply_m8_lds<4", "k_apply_m8_lds<6",
+                "k_apply_m8_lds<0, true>", "k_apply_m8_v1<1>", "k_apply_m16_v1<1>", "k_apply_m8_idx<4, 4>"):
+        assert bad not in out, bad
+    assert "DIAGNOSTIC" not in rs_amd.version()
