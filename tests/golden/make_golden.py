@@ -66,6 +66,13 @@ def cases():
     add("c5_enc", "encode", 4096, 1024, 64, 1)
     add("c5_dec_bench", "decode", 4096, 1024, 64, 1, 1024, bench_pattern(4096, 1024))
     add("c5_dec_rand", "decode", 4096, 1024, 64, 1, 700, rand_pattern(4096, 1024, 700, 3))
+    # C5 at full 1 KiB column chunks: the hand-scheduled GF(2^16) kernel (64-byte symbols above only
+    # reach the compiled tail kernel); sha256 of the outputs
+    add("c5_enc_1k", "encode", 4096, 1024, 1024, 2)
+    add("c5_dec_bench_1k", "decode", 4096, 1024, 1024, 1, 1024, bench_pattern(4096, 1024))
+    add("c5_dec_rand_2k", "decode", 4096, 1024, 2048, 1, 1024, rand_pattern(4096, 1024, 1024, 9))
+    add("c5_dec_t32_1k", "decode", 4096, 1024, 1024, 1, 32, rand_pattern(4096, 1024, 32, 10, info_only=True))
+    add("c5_dec_noncw_1k", "decode_noncw", 4096, 1024, 1024, 1, 300, rand_pattern(4096, 1024, 300, 11))
     # example.c shape: 10-byte symbols (5 words, not a multiple of 16 B)
     add("ex_enc", "encode", 100, 10, 10, 1)
     add("ex_dec", "decode", 100, 10, 10, 1, 10, rand_pattern(100, 10, 10, 4))
