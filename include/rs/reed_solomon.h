@@ -46,7 +46,9 @@ void rs_destroy(RS_t* rs);
 int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf_symbols, symbol_seq_t* rep_symbols);
 /* reference :74 -- erased slots must be zero on entry; restores erased information symbols in place
  * (erased repair slots are left untouched, as in the reference). 0, 1, RS_ERR_CANNOT_RESTORE (t > r),
- * RS_ERR_INVALID, RS_ERR_DEVICE. */
+ * RS_ERR_INVALID, RS_ERR_DEVICE. Bit-identical to the reference under its zeroed-erased-slots
+ * contract; erased slots are not read, so non-zero garbage there still yields the true symbols here,
+ * where the reference would return c XOR garbage-dependent values. */
 int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv_symbols, const bool* is_erased,
                        uint16_t t);
 

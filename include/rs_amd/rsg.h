@@ -6,7 +6,10 @@
  * `symbol_size` bytes, addressed as  base + stripe * stripe_stride + symbol * symbol_stride.
  * It is what the reference's rs_generate_repair_symbols (src/rs/reed_solomon.c:338-441) and
  * rs_restore_symbols (src/rs/reed_solomon.c:443-559) become when the buffers are device-resident;
- * results are bit-identical, stripe by stripe.
+ * results are bit-identical, stripe by stripe, under the reference's contract that erased slots hold
+ * zeros on entry (reed_solomon.h:64). Erased slots are never read here, so with garbage in them this
+ * library still restores the true symbols, where the reference (whose syndromes read every slot,
+ * fft.c:68-75) would not: parity for non-zeroed erased slots is by design, not with the reference.
  *
  * Plain C ABI: device pointers, sizes, `stream` is a hipStream_t (NULL = default stream).
  * Calls only enqueue work; synchronise the stream before reading results.

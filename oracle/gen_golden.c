@@ -8,7 +8,11 @@
  *
  * Usage: gen_golden <case-spec-file> <out-dir>
  * Each spec line:  name op k r S n_stripes seed t erased_csv
- *   op = encode | encode_iota | decode | decode_noncw | gmatrix | dmatrix
+ *   op = encode | encode_iota | decode | decode_noncw | gmatrix | dmatrix   (codec, reed_solomon.h)
+ *      | gf_add | gf_mul | gf_madd        a = stripe-0 bytes, b = stripe-1 bytes, coef = t; out: a
+ *      | fft_t | fft_tc | fft_p | fft_pc  f = k symbols (stripe 0), r outputs; fft_t / fft_tc positions,
+ *        fft_p components = pos_gen(seed, i); fft_pc cosets "leader:size,..." in the erased_csv field;
+ *        out: the r outputs (fft_tc / fft_pc print their return code)
  * For every case it writes <out-dir>/<name>.bin (raw outputs) and prints "name rc" to stdout.
  * Inputs come from the portable counter-based generator below (mirrored in tests/ and on device).
  */
@@ -18,6 +22,8 @@
 #include <string.h>
 
 #include <memory/seq.h>
+#include <rs/fft.h>
+#include <rs/gf65536.h>
 #include <rs/reed_solomon.h>
 
 static uint64_t mix64(uint64_t z) {
@@ -44,6 +50,62 @@ static void dump(FILE* f, const symbol_seq_t* seq, size_t first, size_t cnt) {
     for (size_t i = 0; i < cnt; ++i) fwrite(seq->symbols[first + i]->data, 1, seq->symbol_size, f);
 }
 
+/* i-th position / component of the fft cases: mix64(seed ^ (i + 1) * G) % N (tests/_util.py:pos_gen) */
+static uint16_t pos_gen(uint64_t seed, uint64_t i) { return (uint16_t)(mix64(seed ^ ((i + 1) * 0x9E3779B97F4A7C15ULL)) % 65535u); }
+
+/* the symbol-wide ops and the transforms (reference include/rs/gf65536.h:146-167, include/rs/fft.h) */
+static int run_extra(RS_t* rs, const char* op, unsigned k, unsigned r, unsigned S, unsigned long long seed, unsigned t,
+                     const char* ecsv, FILE* out, int* handled) {
+    *handled = 1;
+    if (!strncmp(op, "gf_", 3)) {
+        uint8_t* a = malloc(S + 1);
+        uint8_t* b = malloc(S + 1);
+        for (unsigned i = 0; i < S; ++i) a[i] = gen_byte(seed, 0, i), b[i] = gen_byte(seed, 1, i);
+        if (!strcmp(op, "gf_add")) gf_add(a, b, S);
+        else if (!strcmp(op, "gf_mul")) gf_mul(rs->gf, a, (element_t)t, S);
+        else gf_madd(rs->gf, a, (element_t)t, b, S);
+        fwrite(a, 1, S, out);
+        free(a);
+        free(b);
+        return 0;
+    }
+    if (strncmp(op, "fft_", 4)) {
+        *handled = 0;
+        return 0;
+    }
+    symbol_seq_t* f = seq_create(k, S);
+    symbol_seq_t* res = seq_create(r, S);
+    fill(f, 0, k, seed, 0);
+    for (unsigned j = 0; j < r; ++j) memset(res->symbols[j]->data, 0xA5, S); /* outputs are overwritten */
+    uint16_t* pos = calloc(k + r + 1, sizeof(uint16_t));
+    int rc = 0;
+    if (!strcmp(op, "fft_t") || !strcmp(op, "fft_tc")) {
+        for (unsigned i = 0; i < k; ++i) pos[i] = pos_gen(seed, i);
+        if (!strcmp(op, "fft_t")) fft_transform(rs->gf, f, pos, res);
+        else rc = fft_transform_cycl(rs->gf, f, pos, res);
+    } else if (!strcmp(op, "fft_p")) {
+        for (unsigned j = 0; j < r; ++j) pos[j] = pos_gen(seed, j);
+        fft_partial_transform(rs->gf, f, pos, res);
+    } else { /* fft_pc */
+        coset_t cs[4200];
+        uint16_t cnt = 0;
+        const char* p = ecsv;
+        while (*p && cnt < 4200) {
+            char* q;
+            cs[cnt].leader = (uint16_t)strtoul(p, &q, 10);
+            cs[cnt].size = (uint8_t)strtoul(q + 1, &q, 10);
+            ++cnt;
+            p = *q == ',' ? q + 1 : q;
+        }
+        rc = fft_partial_transform_cycl(rs->gf, f, cs, cnt, res);
+    }
+    dump(out, res, 0, r);
+    free(pos);
+    seq_destroy(f);
+    seq_destroy(res);
+    return rc;
+}
+
 int main(int argc, char** argv) {
     if (argc != 3) {
         fprintf(stderr, "usage: %s spec outdir\n", argv[0]);
@@ -62,7 +124,7 @@ int main(int argc, char** argv) {
         int got = sscanf(line, "%255s %31s %u %u %u %u %llu %u %59999s", name, op, &k, &r, &S, &n, &seed, &t, ecsv);
         if (got < 8) continue;
         bool* er = calloc(k + r + 1, 1);
-        if (got == 9 && strcmp(ecsv, "-") != 0) {
+        if (got == 9 && strcmp(ecsv, "-") != 0 && strncmp(op, "fft_", 4) != 0) {
             char* p = ecsv;
             while (*p) {
                 er[strtoul(p, &p, 10)] = true;
@@ -72,7 +134,14 @@ int main(int argc, char** argv) {
         char path[1024];
         snprintf(path, sizeof path, "%s/%s.bin", argv[2], name);
         FILE* out = fopen(path, "wb");
-        int rc = 0;
+        int rc = 0, handled = 0;
+        rc = run_extra(rs, op, k, r, S, seed, t, ecsv, out, &handled);
+        if (handled) {
+            fclose(out);
+            printf("%s %d\n", name, rc);
+            free(er);
+            continue;
+        }
         for (unsigned s = 0; s < n; ++s) {
             symbol_seq_t* all = seq_create(k + r, S);
             symbol_seq_t inf = {k, S, all->symbols}, rep = {r, S, all->symbols + k};

@@ -25,6 +25,7 @@
 extern "C" {
 #include <memory/seq.h>
 #include <rs/cyclotomic_coset.h>
+#include <rs/fft.h>
 #include <rs/gf65536.h>
 #include <rs/reed_solomon.h>
 #include <rs_amd/rsg.h>
@@ -1480,12 +1481,15 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    // A plan not yet specialised runs the generic kernel, whose few workgroups per column chunk leave the
-    // chip mostly idle (one C3 stripe: 16 per 16 KiB chunk, 87 us a launch): one launch over the whole
-    // symbol then beats the copy / kernel pipeline over kMaxChunks column chunks.
+    // A GF(256) plan that will be specialised at a later call runs the generic kernel until then, whose
+    // few workgroups per column chunk leave the chip mostly idle (one C3 stripe: 16 per 16 KiB chunk, 87 us
+    // a launch): one launch over the whole symbol then beats the copy / kernel pipeline over kMaxChunks
+    // column chunks. Plans that are never specialised (GF(2^16) codes, jit = 0, a failed compile) keep
+    // the chunked pipeline.
     DevPlan* dplan = nullptr;
     if ((rc = decode_plan(c, is_erased, t, &dplan))) return rc;
-    const size_t P = pad16(S), W = (dplan->xj || dplan->jit) ? chunk_width(S) : S, nch = (S + W - 1) / W,
+    const bool pending = c->m <= 8 && c->jit != 0 && !dplan->xj && !dplan->jit && !dplan->xj_failed && !dplan->jit_failed;
+    const size_t P = pad16(S), W = pending ? S : chunk_width(S), nch = (S + W - 1) / W,
                  nl = lost.size();
     // erased slots are neither gathered nor read by the decoder. Only restored rows come back: the span
     // lost[0] .. lost.back() when it is (nearly) contiguous, else the rows packed on the device behind
@@ -1631,6 +1635,7 @@ extern "C" void seq_printf(const symbol_seq_t* q) {
 }
 
 // ============================================================================ rs/gf65536.h, rs/cyclotomic_coset.h
+// normal bases of GF(2), GF(4), GF(16), GF(256), GF(2^16): facts restated from reference gf65536.c:21-57
 static const uint16_t kNormalBases[GF_NORMAL_BASES_ELEMENTS] = {
     1,                                                           // GF(2)
     44234, 44235,                                                // GF(4)
@@ -1638,35 +1643,17 @@ static const uint16_t kNormalBases[GF_NORMAL_BASES_ELEMENTS] = {
     16402, 53598, 44348, 63986, 22060, 64366, 6088, 32521,       // GF(256)
     2048, 2880, 7129, 30616, 2643, 6897, 29685, 7378, 30100, 2743, 20193, 36223, 24055, 41458, 41014, 61451};
 
-extern "C" GF_t* gf_create(void) {
-    GF_t* gf = static_cast<GF_t*>(std::malloc(sizeof(GF_t)));
-    if (!gf) return nullptr;
-    const Field& F = field();
-    for (uint32_t i = 0; i < (kN << 1) - 1; ++i) gf->pow_table[i] = F.exp[i];
-    std::memcpy(gf->log_table, F.log, sizeof(gf->log_table));
-    std::memcpy(gf->normal_bases, kNormalBases, sizeof(kNormalBases));
-    return gf;
-}
-
-extern "C" void gf_destroy(GF_t* gf) { std::free(gf); }
-
 static int m_index(uint8_t m) { return m == 1 ? 0 : m == 2 ? 1 : m == 4 ? 3 : m == 8 ? 7 : 15; }
 
-extern "C" element_t gf_get_normal_basis_element(GF_t* gf, uint8_t m, uint8_t i) {
-    return gf ? gf->normal_bases[m_index(m) + i] : kNormalBases[m_index(m) + i];
-}
-
-extern "C" uint16_t gf_get_normal_repr(GF_t* gf, uint8_t m, uint16_t d) {
-    (void)gf;
-    // coordinates of alpha^d in the normal basis of GF(2^m) (0 when alpha^d is not in GF(2^m)),
-    // as reference gf65536.c:90-108 tabulates them
+// normal_repr[li][d]: bits of alpha^d in the normal basis of GF(2^m), m = 1 << li (0 when alpha^d is
+// not in GF(2^m)), as reference gf65536.c:90-108 tabulates them
+static const std::vector<uint16_t>* normal_repr_tables() {
     static std::once_flag once;
-    static std::vector<uint16_t> tab[5];
+    static std::vector<uint16_t> tab[CC_COSET_SIZES_CNT];
     std::call_once(once, [] {
         const Field& F = field();
-        const uint8_t ms[5] = {1, 2, 4, 8, 16};
-        for (int li = 0; li < 5; ++li) {
-            const uint8_t mm = ms[li];
+        for (int li = 0; li < CC_COSET_SIZES_CNT; ++li) {
+            const uint8_t mm = uint8_t(1u << li);
             tab[li].assign(kN, 0);
             for (uint32_t bits = 1; bits < (1u << mm); ++bits) {
                 uint16_t e = 0;
@@ -1676,8 +1663,35 @@ extern "C" uint16_t gf_get_normal_repr(GF_t* gf, uint8_t m, uint16_t d) {
             }
         }
     });
+    return tab;
+}
+
+extern "C" GF_t* gf_create(void) {
+    GF_t* gf = static_cast<GF_t*>(std::calloc(1, sizeof(GF_t)));
+    if (!gf) return nullptr;
+    const Field& F = field();
+    for (uint32_t i = 0; i < (kN << 1) - 1; ++i) gf->pow_table[i] = F.exp[i];
+    std::memcpy(gf->log_table, F.log, sizeof(gf->log_table));
+    std::memcpy(gf->normal_bases, kNormalBases, sizeof(kNormalBases));
+    const std::vector<uint16_t>* tab = normal_repr_tables();
+    for (int li = 0; li < CC_COSET_SIZES_CNT; ++li) {
+        uint16_t* dst = gf->_normal_repr_by_subfield_memory + size_t(li) * N;
+        std::memcpy(dst, tab[li].data(), size_t(N) * sizeof(uint16_t));
+        gf->normal_repr_by_subfield[1u << li] = dst;  // other entries stay NULL, as the reference's
+    }
+    return gf;
+}
+
+extern "C" void gf_destroy(GF_t* gf) { std::free(gf); }
+
+extern "C" element_t gf_get_normal_basis_element(GF_t* gf, uint8_t m, uint8_t i) {
+    return gf ? gf->normal_bases[m_index(m) + i] : kNormalBases[m_index(m) + i];
+}
+
+extern "C" uint16_t gf_get_normal_repr(GF_t* gf, uint8_t m, uint16_t d) {
+    if (gf && m <= CC_MAX_COSET_SIZE && gf->normal_repr_by_subfield[m]) return gf->normal_repr_by_subfield[m][d];
     const int li = m == 1 ? 0 : m == 2 ? 1 : m == 4 ? 2 : m == 8 ? 3 : 4;
-    return tab[li][d % kN];
+    return normal_repr_tables()[li][d % kN];
 }
 
 extern "C" element_t gf_mul_ee(GF_t* gf, element_t a, element_t b) {
@@ -1739,4 +1753,214 @@ extern "C" void cc_cosets_to_positions(const coset_t* cs, uint16_t cosets_cnt, u
             e = NEXT_COSET_ELEMENT(e);
         } while (e != cs[c].leader && w < positions_cnt);
     }
+}
+
+// ============================================================================ context-free host ops
+// gf_add / gf_mul / gf_madd and the fft_* transforms take host symbols and no codec. They run on the
+// GPU through one process-wide engine: the current device at first use, one non-blocking stream,
+// pinned + device staging that only grows, and an m = 16 codec shell whose matrix kernels, options
+// and split-K scratch the transforms use. Calls are serialised by the engine's mutex.
+namespace {
+
+struct HostOps {
+    std::mutex mu;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    std::unique_ptr<rsg_codec> codec;
+    int init() {
+        if (device >= 0) return 0;
+        int ndev = 0, dev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+            std::fprintf(stderr, "librs_amd: no usable HIP device for the symbol operations (no CPU fallback)\n");
+            return RS_ERR_DEVICE;
+        }
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipSetDevice(dev));
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        auto c = std::make_unique<rsg_codec>();
+        c->device = dev;
+        c->m = 16;
+        if (int rc = device_tables(dev, &c->d_ltab)) return rc;
+        codec = std::move(c);
+        device = dev;
+        return 0;
+    }
+    int reserve(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        h = nullptr;
+        d = nullptr;
+        cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+        cap = bytes;
+        return 0;
+    }
+};
+
+HostOps& hostops() {
+    static HostOps* ops = new HostOps();  // never destroyed: outlives the HIP runtime's teardown
+    return *ops;
+}
+
+// a ^= b (op 0), a = coef * a (1), a ^= coef * b (2) over symbol_size / 2 words, on the GPU
+int symbol_op(int op, void* a, element_t coef, const void* b, size_t symbol_size) {
+    const size_t nw = symbol_size / 2, bytes = nw * 2, P = pad16(bytes);
+    if (!nw) return 0;
+    HostOps& o = hostops();
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (int rc = o.init()) return rc;
+    HIP_TRY(hipSetDevice(o.device));
+    if (int rc = o.reserve(2 * P)) return rc;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if (int rc = plan_tables(o.device, &logt, &g8, &expt)) return rc;
+    std::memcpy(o.h, a, bytes);
+    if (op != 1) std::memcpy(o.h + P, b, bytes);
+    HIP_TRY(hipMemcpyAsync(o.d, o.h, op != 1 ? P + bytes : bytes, hipMemcpyHostToDevice, o.stream));
+    const uint32_t lc = op == 0 ? 0u : field().log[coef];
+    HIP_TRY(launch_symbol_op(reinterpret_cast<uint16_t*>(o.d), reinterpret_cast<const uint16_t*>(o.d + P), op, lc,
+                             int64_t(nw), logt, expt, o.stream));
+    HIP_TRY(hipMemcpyAsync(o.h, o.d, bytes, hipMemcpyDeviceToHost, o.stream));
+    HIP_TRY(hipStreamSynchronize(o.stream));
+    std::memcpy(a, o.h, bytes);
+    return 0;
+}
+
+[[noreturn]] void symbol_op_failed(const char* what, int rc) {
+    // void entry points cannot report an error; a wrong symbol must never be returned silently
+    std::fprintf(stderr, "librs_amd: %s failed (code %d); aborting\n", what, rc);
+    std::abort();
+}
+
+// res[j] = sum_i M[j][i] f[i] for the transforms: f and res gathered / scattered through pinned
+// staging, the matrix applied by the engine's GF(2^16) kernels (host-built plan). Odd symbol sizes
+// follow the reference under NDEBUG: words cover symbol_size / 2, the outputs' last byte is zero
+// (fft.c memsets every output before accumulating into it).
+int transform_apply(std::vector<uint16_t> M, const symbol_seq_t* f, symbol_seq_t* res) {
+    if (!f || !res || f->symbol_size != res->symbol_size) return RS_ERR_INVALID;
+    const size_t S = f->symbol_size, Se = S & ~size_t(1), K = f->length, R = res->length;
+    if (R == 0) return 0;
+    if (K == 0 || Se == 0) {
+        for (size_t j = 0; j < R; ++j) std::memset(res->symbols[j]->data, 0, S);
+        return 0;
+    }
+    if (K > kN || R > kN) return RS_ERR_INVALID;
+    HostOps& o = hostops();
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (int rc = o.init()) return rc;
+    HIP_TRY(hipSetDevice(o.device));
+    const size_t P = pad16(Se);
+    if (int rc = o.reserve((K + R) * P)) return rc;
+    for (size_t i = 0; i < K; ++i) std::memcpy(o.h + i * P, f->symbols[i]->data, Se);
+    HIP_TRY(hipMemcpyAsync(o.d, o.h, K * P, hipMemcpyHostToDevice, o.stream));
+    std::vector<int32_t> in(K), out(R);
+    for (size_t i = 0; i < K; ++i) in[i] = int32_t(i);
+    for (size_t j = 0; j < R; ++j) out[j] = int32_t(j);
+    std::unique_ptr<DevPlan> plan;
+    if (int rc = build_plan(o.device, 16, std::move(M), int(K), int(R), std::move(in), std::move(out), plan)) return rc;
+    uint8_t* dres = o.d + K * P;
+    if (int rc = run_plan(o.codec.get(), *plan, o.d, 0, int64_t(P), dres, 0, int64_t(P), 1, Se, o.stream)) return rc;
+    HIP_TRY(hipMemcpyAsync(o.h + K * P, dres, R * P, hipMemcpyDeviceToHost, o.stream));
+    HIP_TRY(hipStreamSynchronize(o.stream));  // also: the plan's last launch is done before it is freed
+    for (size_t j = 0; j < R; ++j) {
+        std::memcpy(res->symbols[j]->data, o.h + (K + j) * P, Se);
+        if (S != Se) res->symbols[j]->data[Se] = 0;
+    }
+    return 0;
+}
+
+// alpha^e for the reference's int products (a * b) % N, computed exactly (parity where they do not
+// overflow an int)
+inline element_t pow_mod(uint64_t a, uint64_t b) { return field().exp[(a * b) % kN]; }
+
+}  // namespace
+
+extern "C" void gf_add(void* a, const void* b, size_t symbol_size) {
+    if (int rc = symbol_op(0, a, 0, b, symbol_size)) symbol_op_failed("gf_add", rc);
+}
+
+extern "C" void gf_mul(GF_t* gf, void* a, element_t coef, size_t symbol_size) {
+    (void)gf;
+    if (coef == 0) {  // reference gf65536.c:175-181
+        std::memset(a, 0, symbol_size);
+        return;
+    }
+    if (coef == 1) return;
+    if (int rc = symbol_op(1, a, coef, nullptr, symbol_size)) symbol_op_failed("gf_mul", rc);
+}
+
+extern "C" void gf_madd(GF_t* gf, void* a, element_t coef, const void* b, size_t symbol_size) {
+    (void)gf;
+    if (coef == 0) return;  // reference gf65536.c:199-205
+    if (int rc = symbol_op(coef == 1 ? 0 : 2, a, coef, b, symbol_size)) symbol_op_failed("gf_madd", rc);
+}
+
+// DFT matrix of fft_transform / fft_transform_cycl: M[j][i] = alpha^(positions[i] * j)
+static std::vector<uint16_t> dft_matrix(const symbol_seq_t* f, const uint16_t* positions, const symbol_seq_t* res) {
+    const size_t K = f->length, R = res->length;
+    std::vector<uint16_t> M(R * K);
+    for (size_t j = 0; j < R; ++j)
+        for (size_t i = 0; i < K; ++i) M[j * K + i] = pow_mod(positions[i], j);
+    return M;
+}
+
+extern "C" void fft_transform(GF_t* gf, const symbol_seq_t* f, const uint16_t* positions, symbol_seq_t* res) {
+    (void)gf;
+    if (!f || !res || (!positions && f->length)) symbol_op_failed("fft_transform (bad arguments)", RS_ERR_INVALID);
+    if (int rc = transform_apply(dft_matrix(f, positions, res), f, res)) symbol_op_failed("fft_transform", rc);
+}
+
+extern "C" int fft_transform_cycl(GF_t* gf, const symbol_seq_t* f, const uint16_t* positions, symbol_seq_t* res) {
+    (void)gf;
+    if (!f || !res || (!positions && f->length)) return RS_ERR_INVALID;
+    return transform_apply(dft_matrix(f, positions, res), f, res);
+}
+
+extern "C" void fft_partial_transform(GF_t* gf, const symbol_seq_t* f, const uint16_t* components,
+                                      symbol_seq_t* res) {
+    (void)gf;
+    if (!f || !res || (!components && res->length))
+        symbol_op_failed("fft_partial_transform (bad arguments)", RS_ERR_INVALID);
+    const size_t K = f->length, R = res->length;
+    std::vector<uint16_t> M(R * K);
+    for (size_t r = 0; r < R; ++r) {
+        const uint64_t j = (kN - components[r]) % kN;  // reference fft.c:115
+        for (size_t i = 0; i < K; ++i) M[r * K + i] = pow_mod(i, j);
+    }
+    if (int rc = transform_apply(std::move(M), f, res)) symbol_op_failed("fft_partial_transform", rc);
+}
+
+extern "C" int fft_partial_transform_cycl(GF_t* gf, const symbol_seq_t* f, const coset_t* cosets, uint16_t cosets_cnt,
+                                          symbol_seq_t* res) {
+    if (!f || !res || (!cosets && cosets_cnt)) return RS_ERR_INVALID;
+    const size_t K = f->length, R = res->length;
+    size_t total = 0;
+    for (uint16_t c = 0; c < cosets_cnt; ++c) {
+        const uint8_t m = cosets[c].size;
+        if (m != 1 && m != 2 && m != 4 && m != 8 && m != 16) return RS_ERR_INVALID;
+        total += m;
+    }
+    if (total != R) return RS_ERR_INVALID;  // the reference asserts idx == res->length (fft.c:172)
+    // the reference's evaluation entry by entry (fft.c:142-169): res[idx] of coset (L, m), element j,
+    // = sum_i f[i] * sum_t bit_t(repr_m((s * i) % N)) * nb^(m)_((j + t) % m), s = N - L
+    std::vector<uint16_t> M(R * K);
+    size_t idx = 0;
+    for (uint16_t c = 0; c < cosets_cnt; ++c) {
+        const uint8_t m = cosets[c].size;
+        const uint16_t s = uint16_t(N - cosets[c].leader);
+        for (uint8_t j = 0; j < m; ++j, ++idx)
+            for (size_t i = 0; i < K; ++i) {
+                const uint16_t repr = gf_get_normal_repr(gf, m, uint16_t((uint64_t(s) * i) % kN));
+                uint16_t v = 0;
+                for (uint8_t t = 0; t < m; ++t)
+                    if (repr & (1u << t)) v ^= kNormalBases[m_index(m) + (j + t) % m];
+                M[idx * K + i] = v;
+            }
+    }
+    return transform_apply(std::move(M), f, res);
 }

@@ -650,6 +650,30 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
     if ((threadIdx.x & 63) == 0) atomicXor(out + s, (unsigned long long)h);
 }
 
+// ---------------------------------------------------- symbol-wide ops (gf_add / gf_mul / gf_madd)
+// One word (LE u16) per lane, reference src/rs/gf65536.c:155-219: add a ^= b; mul a = c * a; madd
+// a ^= c * b, products through the log / exp tables with zero words skipped (lc = log c, c != 0, 1).
+__global__ void __launch_bounds__(256) k_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw,
+                                                   const uint16_t* __restrict__ logt, const uint16_t* __restrict__ expt) {
+    for (int64_t w = int64_t(blockIdx.x) * 256 + threadIdx.x; w < nw; w += int64_t(gridDim.x) * 256) {
+        const uint32_t x = op == 1 ? a[w] : b[w];
+        uint32_t v = x;
+        if (op != 0 && x) {
+            const uint32_t e = logt[x] + lc;
+            v = expt[e >= 65535u ? e - 65535u : e];
+        }
+        a[w] = op == 1 ? uint16_t(v) : uint16_t(a[w] ^ v);
+    }
+}
+
+hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw, const uint16_t* logt,
+                            const uint16_t* expt, hipStream_t st) {
+    if (nw <= 0) return hipSuccess;
+    const unsigned grid = unsigned(std::min<int64_t>((nw + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_symbol_op, dim3(grid), dim3(256), 0, st, a, b, op, lc, nw, logt, expt);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------ launchers
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
     V1Args v{};

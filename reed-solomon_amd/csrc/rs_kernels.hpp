@@ -95,6 +95,11 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
 hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
                               int64_t nrows, int64_t width, hipStream_t st);
 
+// symbol-wide word ops over nw words: op 0 a ^= b, 1 a = c * a, 2 a ^= c * b (lc = log c; logt / expt:
+// discrete log and alpha^i tables, i < 65535)
+hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw, const uint16_t* logt,
+                            const uint16_t* expt, hipStream_t st);
+
 int apply_tile_rows(int m, int R);
 // V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff);

@@ -94,6 +94,13 @@ _sig("gf_mul_ee", u16, P, u16, u16)
 _sig("gf_div_ee", u16, P, u16, u16)
 _sig("gf_get_normal_repr", u16, P, u8, u16)
 _sig("gf_get_normal_basis_element", u16, P, u8, u8)
+_sig("gf_add", None, P, P, ctypes.c_size_t)
+_sig("gf_mul", None, P, P, u16, ctypes.c_size_t)
+_sig("gf_madd", None, P, P, u16, P, ctypes.c_size_t)
+_sig("fft_transform", None, P, ctypes.POINTER(SymbolSeqT), P, ctypes.POINTER(SymbolSeqT))
+_sig("fft_transform_cycl", ctypes.c_int, P, ctypes.POINTER(SymbolSeqT), P, ctypes.POINTER(SymbolSeqT))
+_sig("fft_partial_transform", None, P, ctypes.POINTER(SymbolSeqT), P, ctypes.POINTER(SymbolSeqT))
+_sig("fft_partial_transform_cycl", ctypes.c_int, P, ctypes.POINTER(SymbolSeqT), P, u16, ctypes.POINTER(SymbolSeqT))
 _sig("cc_create", P)
 _sig("cc_destroy", None, P)
 _sig("cc_get_coset_size", u8, u16)
@@ -200,6 +207,48 @@ class RS:
         return _lib.rs_restore_symbols(self._h, k, r, ctypes.byref(a.seq), _np_ptr(er), t)
 
 
+# ------------------------------------------------------------------------------ symbol ops, transforms
+class CosetT(ctypes.Structure):  # include/rs/cyclotomic_coset.h coset_t
+    _fields_ = [("leader", ctypes.c_uint16), ("size", ctypes.c_uint8)]
+
+
+def _u8(a):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous, "symbols must be C-contiguous uint8 arrays"
+    return a
+
+
+def symbol_add(a, b):
+    """a ^= b in place (gf_add, reference include/rs/gf65536.h:146); numpy uint8 arrays of equal size."""
+    _lib.gf_add(_np_ptr(_u8(a)), _np_ptr(_u8(b)), a.size)
+
+
+def symbol_mul(a, coef, gf=None):
+    """a = coef * a in place (gf_mul, reference :156)."""
+    _lib.gf_mul(gf, _np_ptr(_u8(a)), coef, a.size)
+
+
+def symbol_madd(a, coef, b, gf=None):
+    """a ^= coef * b in place (gf_madd, reference :167)."""
+    _lib.gf_madd(gf, _np_ptr(_u8(a)), coef, _np_ptr(_u8(b)), a.size)
+
+
+def fft(kind, f, res, arg, gf=None):
+    """Reference rs/fft.h transforms on lists of host symbols (numpy uint8). kind: "transform" /
+    "transform_cycl" (arg = positions, uint16), "partial" (arg = components, uint16),
+    "partial_cycl" (arg = [(leader, size), ...]). Writes res in place; returns the C rc (0 for the void
+    entry points)."""
+    S = (f[0] if len(f) else res[0]).size
+    a, b = _SeqBuf([_u8(x) for x in f], S), _SeqBuf([_u8(x) for x in res], S)
+    if kind == "partial_cycl":
+        cs = (CosetT * max(len(arg), 1))(*[CosetT(int(l), int(m)) for l, m in arg])
+        return _lib.fft_partial_transform_cycl(gf, ctypes.byref(a.seq), cs, len(arg), ctypes.byref(b.seq))
+    v = np.ascontiguousarray(arg, dtype=np.uint16)
+    fn = {"transform": _lib.fft_transform, "transform_cycl": _lib.fft_transform_cycl,
+          "partial": _lib.fft_partial_transform}[kind]
+    rc = fn(gf, ctypes.byref(a.seq), _np_ptr(v), ctypes.byref(b.seq))
+    return 0 if rc is None else rc
+
+
 # ------------------------------------------------------------------------------ device engine
 def _stream_ptr(stream):
     if stream is None:
@@ -289,12 +338,23 @@ class Codec:
             raise RSError(rc, "rsg_decode_batch")
         return rc
 
+    @staticmethod
+    def _host_ptr(stripes):
+        """Address of a C-contiguous uint8 host array (numpy or CPU tensor): the host batch calls derive
+        their byte strides from the shape alone."""
+        if hasattr(stripes, "data_ptr"):
+            import torch
+            assert stripes.dtype == torch.uint8 and stripes.is_contiguous() and not stripes.is_cuda
+            return stripes.data_ptr()
+        assert stripes.dtype == np.uint8 and stripes.flags.c_contiguous
+        return stripes.ctypes.data
+
     def encode_host(self, stripes, check=True):
         """Stripes in HOST memory: a [n, k + r, S] uint8 array (numpy or a CPU tensor, pinned for PCIe
         rate); writes the repair symbols in place (rsg_encode_host, pipelined, synchronous)."""
         n, nsym, S = stripes.shape
         assert nsym == self.k + self.r
-        ptr = stripes.data_ptr() if hasattr(stripes, "data_ptr") else stripes.ctypes.data
+        ptr = self._host_ptr(stripes)
         rc = _lib.rsg_encode_host(self._h, P(ptr), nsym * S, S, P(ptr + self.k * S), nsym * S, S, n, S)
         if check and rc:
             raise RSError(rc, "rsg_encode_host")
@@ -304,7 +364,8 @@ class Codec:
         """Restores erased information symbols of host-memory stripes in place (rsg_decode_host)."""
         n, nsym, S = stripes.shape
         er = np.ascontiguousarray(is_erased, dtype=np.bool_)
-        ptr = stripes.data_ptr() if hasattr(stripes, "data_ptr") else stripes.ctypes.data
+        assert nsym == self.k + self.r
+        ptr = self._host_ptr(stripes)
         rc = _lib.rsg_decode_host(self._h, P(ptr), nsym * S, S, n, S, _np_ptr(er), int(er.sum()))
         if check and rc:
             raise RSError(rc, "rsg_decode_host")

@@ -52,7 +52,7 @@ int main(int argc, char** argv) {
     uint8_t* keep = malloc((size_t)calls * k * S);
     for (int c = 0; c < calls; ++c)
         for (int i = 0; i < k; ++i) memcpy(keep + ((size_t)c * k + i) * S, st[c]->symbols[i]->data, S);
-    for (int w = 0; w < 10; ++w) { /* warm: plan, then its specialised kernel (9th launch of a plan) */
+    for (int w = 0; w < 10; ++w) { /* warm: plan, then its specialised kernel (a decode plan is specialised at its 3rd call, dec_jit_uses) */
         for (int i = 0; i < k + r; ++i)
             if (er[i]) memset(st[0]->symbols[i]->data, 0, S);
         if (rs_restore_symbols(rs, k, r, st[0], er, t)) return 4;

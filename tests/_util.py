@@ -229,3 +229,105 @@ def gf_apply(M, X):
         prod[M[:, i] == 0] = 0
         out ^= prod
     return out
+
+
+# ---------------------------------------------------------------- symbol ops / transforms (fixtures)
+EXTRA_OPS = ("gf_add", "gf_mul", "gf_madd", "fft_t", "fft_tc", "fft_p", "fft_pc")
+
+
+def pos_gen(seed, i):
+    """Position / component i of the fft cases (oracle/gen_golden.c:pos_gen)."""
+    with np.errstate(over="ignore"):
+        v = _mix64(np.uint64(seed) ^ (np.uint64(i + 1) * _G))
+    return int(v % np.uint64(65535))
+
+
+def _words(buf):
+    """LE uint16 words of the first len // 2 * 2 bytes."""
+    n = buf.size // 2
+    return buf[:2 * n].view("<u2").astype(np.int64)
+
+
+_REPR = {}
+
+
+def normal_repr_table(m):
+    """repr[d] = bits of alpha^d in the normal basis of GF(2^m) (oracle orc_normal_repr)."""
+    if m not in _REPR:
+        o = oracle()
+        o.orc_normal_repr.restype = ctypes.c_uint16
+        o.orc_normal_repr.argtypes = [ctypes.c_uint8, ctypes.c_uint16]
+        _REPR[m] = np.array([o.orc_normal_repr(m, d) for d in range(65535)], np.int64)
+    return _REPR[m]
+
+
+def normal_basis(m):
+    exp, _ = gf_tables()
+    rep = normal_repr_table(m)
+    return [int(exp[int(np.nonzero(rep == (1 << j))[0][0])]) for j in range(m)]
+
+
+def extra_inputs(c):
+    """Inputs of a symbol-op / transform case: (a, b) byte arrays, or (f [k][S], positions / cosets)."""
+    S, seed = c["S"], c["seed"]
+    if c["op"].startswith("gf_"):
+        return gen_info(seed, 0, S), gen_info(seed, 1, S)
+    f = gen_info(seed, 0, c["k"] * S).reshape(c["k"], S) if c["k"] else np.zeros((0, S), np.uint8)
+    if c["op"] in ("fft_t", "fft_tc"):
+        arg = [pos_gen(seed, i) for i in range(c["k"])]
+    elif c["op"] == "fft_p":
+        arg = [pos_gen(seed, j) for j in range(c["r"])]
+    else:
+        arg = [tuple(x) for x in c["cosets"]]
+    return f, arg
+
+
+def transform_matrix(c, arg):
+    """The transform's GF(2^16) matrix [r][k] as the reference evaluates it (src/rs/fft.c)."""
+    exp, _ = gf_tables()
+    N = 65535
+    k, r = c["k"], c["r"]
+    i = np.arange(k, dtype=np.int64)
+    if c["op"] in ("fft_t", "fft_tc"):
+        return exp[(np.array(arg, np.int64)[None, :] * np.arange(r, dtype=np.int64)[:, None]) % N].astype(np.uint16)
+    if c["op"] == "fft_p":
+        j = (N - np.array(arg, np.int64)) % N
+        return exp[(i[None, :] * j[:, None]) % N].astype(np.uint16)
+    rows = []
+    for leader, m in arg:  # fft.c:142-169
+        nb = normal_basis(m)
+        rep = normal_repr_table(m)[((N - leader) % 65536 * i) % N]
+        for jj in range(m):
+            v = np.zeros(k, np.int64)
+            for t in range(m):
+                v ^= np.where((rep >> t) & 1, nb[(jj + t) % m], 0)
+            rows.append(v)
+    return np.array(rows, np.int64).reshape(r, k).astype(np.uint16)
+
+
+def run_extra_numpy(c):
+    """CPU restatement of a symbol-op / transform case (numpy GF(2^16)); raw output bytes."""
+    exp, log = gf_tables()
+    S = c["S"]
+    if c["op"].startswith("gf_"):
+        a, b = extra_inputs(c)
+        a = a.copy()
+        wa, wb = _words(a), _words(b)
+        coef = c["t"]
+        if c["op"] == "gf_add":
+            wa ^= wb
+        elif c["op"] == "gf_mul":
+            wa = np.zeros_like(wa) if coef == 0 else np.where(wa != 0, exp[(log[wa] + log[coef]) % 65535], 0)
+            if coef == 0:
+                a[:] = 0
+        elif coef:
+            wa ^= np.where(wb != 0, exp[(log[wb] + log[coef]) % 65535], 0)
+        a[:2 * wa.size] = wa.astype("<u2").view(np.uint8)
+        return a.tobytes()
+    f, arg = extra_inputs(c)
+    M = transform_matrix(c, arg)
+    X = np.stack([_words(x) for x in f]).astype(np.uint16) if len(f) else np.zeros((0, S // 2), np.uint16)
+    Y = gf_apply(M, X) if len(f) else np.zeros((c["r"], S // 2), np.uint16)
+    out = np.zeros((c["r"], S), np.uint8)
+    out[:, :2 * (S // 2)] = Y.astype("<u2").view(np.uint8).reshape(c["r"], -1)
+    return out.tobytes()

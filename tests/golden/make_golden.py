@@ -39,8 +39,11 @@ def rand_pattern(k, r, t, seed, info_only=False):
 
 def cases():
     c = []
-    add = lambda name, op, k, r, S, n, t=0, er=(): c.append(
-        dict(name=name, op=op, k=k, r=r, S=S, n=n, seed=SEED, t=t, erased=list(er)))
+    def add(name, op, k, r, S, n, t=0, er=(), cosets=None):
+        d = dict(name=name, op=op, k=k, r=r, S=S, n=n, seed=SEED, t=t, erased=list(er))
+        if cosets is not None:
+            d["cosets"] = [list(x) for x in cosets]
+        c.append(d)
     # config 1 (k=4, r=2, 256 B) -- full vectors
     add("c1_enc", "encode", 4, 2, 256, 1)
     add("c1_dec_info_rep", "decode", 4, 2, 256, 1, 2, [1, 4])
@@ -96,7 +99,43 @@ def cases():
     add("wide_r_dec", "decode", 2000, 2000, 4, 1, 2000, rand_pattern(2000, 2000, 2000, 7))
     add("m4_k7r8_enc", "encode", 7, 8, 32, 3)
     add("m8_k200r55_dec", "decode", 200, 55, 32, 2, 40, rand_pattern(200, 55, 40, 8))
+    # symbol-wide ops (reference include/rs/gf65536.h:146-167): a = stripe-0 bytes, b = stripe-1 bytes,
+    # coefficient in the t field; odd sizes pin the reference's NDEBUG word count (symbol_size / 2)
+    add("gf_add_64", "gf_add", 1, 0, 64, 1)
+    add("gf_add_odd", "gf_add", 1, 0, 9, 1)
+    add("gf_mul_c", "gf_mul", 1, 0, 256, 1, 31981)
+    add("gf_mul_0", "gf_mul", 1, 0, 64, 1, 0)
+    add("gf_mul_1", "gf_mul", 1, 0, 64, 1, 1)
+    add("gf_mul_odd", "gf_mul", 1, 0, 9, 1, 4660)
+    add("gf_madd_c", "gf_madd", 1, 0, 256, 1, 12345)
+    add("gf_madd_0", "gf_madd", 1, 0, 64, 1, 0)
+    add("gf_madd_1", "gf_madd", 1, 0, 64, 1, 1)
+    add("gf_madd_odd", "gf_madd", 1, 0, 9, 1, 777)
+    # transforms (reference include/rs/fft.h:29-65): f = k symbols, r outputs
+    add("fft_t_small", "fft_t", 20, 12, 64, 1)
+    add("fft_tc_small", "fft_tc", 20, 12, 64, 1)
+    add("fft_tc_r64", "fft_tc", 300, 64, 128, 1)
+    add("fft_t_odd", "fft_t", 7, 5, 11, 1)
+    add("fft_tc_r1000", "fft_tc", 1100, 1000, 32, 1)
+    add("fft_p_small", "fft_p", 16, 10, 64, 1)
+    add("fft_p_odd", "fft_p", 9, 6, 11, 1)
+    cs = [(0, 1), (21845, 2), (4369, 4), (257, 8), (1, 16), (3, 16)]
+    add("fft_pc_mixed", "fft_pc", 40, sum(m for _, m in cs), 64, 1, cosets=cs)
+    add("fft_pc_badsize", "fft_pc", 10, 12, 64, 1, cosets=[(1, 8), (5, 4)])  # sizes not the cosets' own
+    cs = size16_leaders(64)
+    add("fft_pc_c5", "fft_pc", 1024, 1024, 32, 1, cosets=cs)
     return c
+
+
+def size16_leaders(count):
+    """The first `count` leaders (smallest elements) of 2-cyclotomic cosets of size 16 mod 65535."""
+    out, x = [], 1
+    while len(out) < count:
+        rots = {((x << a) | (x >> (16 - a))) & 0xFFFF for a in range(16)}
+        if min(rots) == x and len(rots) == 16:
+            out.append((x, 16))
+        x += 1
+    return out
 
 
 def main():
@@ -108,6 +147,8 @@ def main():
         with open(spec, "w") as f:
             for c in cs:
                 er = ",".join(map(str, c["erased"])) or "-"
+                if "cosets" in c:
+                    er = ",".join(f"{l}:{m}" for l, m in c["cosets"])
                 f.write(f"{c['name']} {c['op']} {c['k']} {c['r']} {c['S']} {c['n']} {c['seed']} {c['t']} {er}\n")
         out = subprocess.check_output([gen, spec, tmp], text=True)
         rcs = dict(line.split() for line in out.strip().splitlines())

@@ -10,7 +10,8 @@ import pytest
 torch = pytest.importorskip("torch")
 
 import rs_amd  # noqa: E402
-from _util import case, case_inputs, check_golden, gen_info, manifest, oracle_decode, oracle_encode  # noqa: E402
+from _util import (EXTRA_OPS, case, case_inputs, check_golden, extra_inputs, gen_info, manifest,  # noqa: E402
+                   oracle_decode, oracle_encode)
 
 pytestmark = pytest.mark.gpu
 
@@ -54,9 +55,10 @@ def run_case_gpu(c, variant):
     return rc, out.tobytes(), codec.last_kernel, codec.subfield
 
 
-GPU_CASES = [c["name"] for c in manifest()["cases"]]
+GPU_CASES = [c["name"] for c in manifest()["cases"] if c["op"] not in EXTRA_OPS]
+EXTRA_CASES = [c["name"] for c in manifest()["cases"] if c["op"] in EXTRA_OPS]
 # kernels (rsg_last_kernel) of the production GF(2^16) path over full 1 KiB column chunks
-M16_PRODUCTION = ("apply_m16_v1",)
+M16_PRODUCTION = ("apply_m16_v1", "apply_m16_rt16", "apply_m16_rt32")  # R <= 32: the compiled tiles
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
@@ -648,3 +650,89 @@ print("ok", c.last_kernel)
     env = dict(os.environ, RS_XJ_ABLATE="1", RS_XJ_ALIAS="1", PYTHONPATH=os.path.dirname(rs_amd.__file__))
     p = subprocess.run([sys.executable, "-c", code, here], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and p.stdout.startswith("ok rs_xj"), p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("name", EXTRA_CASES)
+def test_golden_symbol_ops_and_transforms(name):
+    """gf_add / gf_mul / gf_madd and fft_transform(_cycl) / fft_partial_transform(_cycl) through the C ABI
+    (host symbols in, GPU compute, host symbols out) against the reference's outputs."""
+    c = case(name)
+    S = c["S"]
+    if c["op"].startswith("gf_"):
+        a, b = extra_inputs(c)
+        a = a.copy()
+        gf = rs_amd.lib.gf_create()
+        {"gf_add": lambda: rs_amd.symbol_add(a, b), "gf_mul": lambda: rs_amd.symbol_mul(a, c["t"], gf),
+         "gf_madd": lambda: rs_amd.symbol_madd(a, c["t"], b, gf)}[c["op"]]()
+        rs_amd.lib.gf_destroy(gf)
+        check_golden(c, a.tobytes())
+        return
+    f, arg = extra_inputs(c)
+    res = [np.full(S, 0xA5, np.uint8) for _ in range(c["r"])]  # outputs are overwritten
+    kind = {"fft_t": "transform", "fft_tc": "transform_cycl", "fft_p": "partial", "fft_pc": "partial_cycl"}[c["op"]]
+    gf = rs_amd.lib.gf_create()
+    rc = rs_amd.fft(kind, [np.ascontiguousarray(x) for x in f], res, arg, gf)
+    rs_amd.lib.gf_destroy(gf)
+    assert rc == c["rc"]
+    check_golden(c, b"".join(x.tobytes() for x in res))
+
+
+def test_symbol_ops_large_and_aliased():
+    """gf_madd over a 1 MiB symbol and gf_add with a == b (zeroes it), vs the numpy restatement."""
+    from _util import gf_tables
+    exp, log = gf_tables()
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    b = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    wa, wb = a.view("<u2").astype(np.int64), b.view("<u2").astype(np.int64)
+    want = wa ^ np.where(wb != 0, exp[(log[wb] + log[40000]) % 65535], 0)
+    rs_amd.symbol_madd(a, 40000, b)
+    assert np.array_equal(a.view("<u2"), want.astype(np.uint16))
+    rs_amd.symbol_add(a, a)
+    assert not a.any()
+
+
+def test_reference_surface_program(tmp_path):
+    """tests/c/ref_surface.c calls every function of the reference's rs/ and memory/ headers, built
+    against this repo's headers and linked against librs_amd.so; its outputs equal the goldens."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "ref_surface")
+    assert os.path.exists(exe), "build it with make -C tests/c (part of __graft_entry__.build)"
+    p = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    for name in ("gf_add_64", "gf_mul_c", "gf_madd_c", "fft_t_small", "fft_tc_small", "fft_p_small", "fft_pc_mixed",
+                 "c1_enc", "c1_dec_info_rep"):
+        check_golden(case(name), (tmp_path / f"{name}.bin").read_bytes())
+
+
+@pytest.mark.parametrize("lost", ["scattered", "contiguous"])
+def test_drop_in_m8_repeated_pattern_chunked(lost):
+    """Per-call restore of one pattern, 5 calls on a GF(256) code with 64 KiB symbols: the first two run
+    the generic kernel over the whole symbol, the third specialises the plan and from then on the call is
+    pipelined in 4 column chunks. Every call bit-exact vs the oracle, for a scattered lost set (rows
+    packed on the device, k_gather_rows) and a contiguous one (one span copied back)."""
+    k, r, S = 128, 32, 65536
+    rng = np.random.default_rng(81 if lost == "scattered" else 82)
+    er = np.zeros(k + r, bool)
+    if lost == "scattered":
+        er[rng.choice(k, 20, replace=False)] = True
+        er[k + rng.choice(r, 5, replace=False)] = True
+    else:
+        er[40:64] = True
+    rs = rs_amd.RS()
+    for call in range(5):
+        syms = [np.zeros(S, np.uint8) for _ in range(k + r)]
+        for i in range(k):
+            syms[i][:] = rng.integers(0, 256, S, dtype=np.uint8)
+        assert rs.generate_repair_symbols(syms[:k], syms[k:]) == 0
+        full = np.stack(syms).copy()
+        for i in np.nonzero(er)[0]:
+            syms[i][:] = 0
+        ref = np.stack(syms).copy()
+        assert rs.restore_symbols(k, r, syms, er, int(er.sum())) == 0
+        assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
+        got = np.stack(syms)
+        assert np.array_equal(got, ref), f"call {call}"
+        assert np.array_equal(got[:k], full[:k]), f"call {call}"
+    rs.close()

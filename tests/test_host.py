@@ -10,9 +10,9 @@ import numpy as np
 import pytest
 
 import rs_amd
-from _util import REPO, case, case_inputs, check_golden, gf_apply, gf_tables, manifest, run_case_oracle
+from _util import EXTRA_OPS, REPO, case, case_inputs, check_golden, gf_apply, gf_tables, manifest, run_case_oracle
 
-HEADERS = ["include/rs/reed_solomon.h", "include/rs/gf65536.h", "include/rs/cyclotomic_coset.h",
+HEADERS = ["include/rs/reed_solomon.h", "include/rs/gf65536.h", "include/rs/cyclotomic_coset.h", "include/rs/fft.h",
            "include/memory/seq.h", "include/memory/symbol.h", "include/rs_amd/rsg.h"]
 
 
@@ -119,7 +119,8 @@ def _apply_case(c):
 
 
 NP_CASES = [c["name"] for c in manifest()["cases"]
-            if c["k"] * max(c["r"], 1) * c["S"] * c["n"] <= 40_000_000 and not c["name"].startswith("gmat")]
+            if c["k"] * max(c["r"], 1) * c["S"] * c["n"] <= 40_000_000 and not c["name"].startswith("gmat")
+            and c["op"] not in EXTRA_OPS]
 
 
 @pytest.mark.parametrize("name", NP_CASES)
@@ -194,3 +195,40 @@ def test_release_build_has_no_ablation_kernels():
                 "k_apply_m8_lds<0, true>", "k_apply_m8_v1<1>", "k_apply_m16_v1<1>", "k_apply_m8_idx<4, 4>"):
         assert bad not in out, bad
     assert "DIAGNOSTIC" not in rs_amd.version()
+
+
+REF_INC = "/root/reference/include"
+LAYOUT_C = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include <memory/seq.h>
+#include <memory/symbol.h>
+#include <rs/cyclotomic_coset.h>
+#include <rs/fft.h>
+#include <rs/gf65536.h>
+#include <rs/reed_solomon.h>
+int main(void) {
+    printf("%zu %zu %zu %zu %zu\n", sizeof(GF_t), offsetof(GF_t, log_table), offsetof(GF_t, normal_bases),
+           offsetof(GF_t, normal_repr_by_subfield), offsetof(GF_t, _normal_repr_by_subfield_memory));
+    printf("%zu %zu %zu %zu\n", sizeof(CC_t), sizeof(coset_t), sizeof(symbol_t), sizeof(symbol_seq_t));
+    printf("%zu %zu %zu\n", offsetof(RS_t, gf), offsetof(RS_t, cc), offsetof(symbol_seq_t, symbols));
+    printf("%d %d %d %d %d\n", N, GF_FIELD_SIZE, GF_PRIMITIVE_POLY, RS_ERR_CANNOT_RESTORE, RS_COSET_LOCATOR_MAX_LEN);
+    return 0;
+}
+"""
+
+
+def test_header_layouts_match_reference(tmp_path):
+    """The public structs and constants have the reference's layout and values (compiled once against
+    the reference's headers, once against this repo's); needs /root/reference (this container)."""
+    import subprocess
+    if not os.path.isdir(REF_INC):
+        pytest.skip("reference headers absent")
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_C)
+    outs = []
+    for inc in (REF_INC, os.path.join(REPO, "include")):
+        exe = tmp_path / ("ref" if inc == REF_INC else "ours")
+        subprocess.check_call(["gcc", "-std=c11", "-w", f"-I{inc}", "-o", str(exe), str(src)])
+        outs.append(subprocess.check_output([str(exe)], text=True))
+    assert outs[0] == outs[1], outs

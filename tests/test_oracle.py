@@ -3,7 +3,7 @@ generated from the compiled reference (tests/golden/make_golden.py)."""
 import numpy as np
 import pytest
 
-from _util import case, check_golden, manifest, oracle, oracle_positions, ptr, run_case_oracle
+from _util import EXTRA_OPS, case, check_golden, manifest, oracle, oracle_positions, ptr, run_case_oracle, run_extra_numpy
 
 # test/src/rs/gf65536/test_gf_mul_ee.c:36-42 and test_gf_div_ee.c:36-42 (SageMath vectors)
 MUL_KAT = [(1, 645, 645), (46478, 0, 0), (31981, 38739, 42167), (2491, 54249, 5290),
@@ -63,7 +63,8 @@ def test_positions_survey_fingerprints():
     assert p[10:].tolist() == [4369, 8738, 17476, 34952]
 
 
-CASES = [c["name"] for c in manifest()["cases"]]
+CASES = [c["name"] for c in manifest()["cases"] if c["op"] not in EXTRA_OPS]
+EXTRA = [c["name"] for c in manifest()["cases"] if c["op"] in EXTRA_OPS]
 FAST = [n for n in CASES if not n.startswith(("gmat_4096", "c5_", "c3_dec_bench_64k"))]
 SLOW = [n for n in CASES if n not in FAST]
 
@@ -83,3 +84,11 @@ def test_oracle_matches_golden_slow(name):
     rc, out = run_case_oracle(c)
     assert rc == c["rc"]
     check_golden(c, out)
+
+
+@pytest.mark.parametrize("name", EXTRA)
+def test_transforms_and_symbol_ops_match_golden(name):
+    """gf_add / gf_mul / gf_madd and the four fft_* transforms restated in numpy (the matrices the
+    product forms, src/rs/fft.c entry by entry) against the reference's outputs."""
+    c = case(name)
+    check_golden(c, run_extra_numpy(c))
