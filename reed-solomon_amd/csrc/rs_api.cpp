@@ -145,10 +145,34 @@ struct DevPlan {
     bool xj_failed = false;
     int64_t uses = 0;                // launches of this plan (JIT policy)
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
+    // stream-ordered build: the upload (and device fill) ran on `built_on`; `ready` marks its end, so a
+    // launch on another stream waits for it; the pinned source of the upload lives until then
+    hipEvent_t ready = nullptr;
+    hipStream_t built_on = nullptr;
+    void* h_stage = nullptr;
+    // called before a launch on stream st: orders it after the build, releases the build's resources
+    // once the build is complete
+    int order_after_build(hipStream_t st) {
+        if (!ready) return 0;
+        if (hipEventQuery(ready) == hipSuccess) {
+            (void)hipEventDestroy(ready);
+            ready = nullptr;
+            if (h_stage) (void)hipHostFree(h_stage);
+            h_stage = nullptr;
+            return 0;
+        }
+        if (st != built_on && hipStreamWaitEvent(st, ready, 0) != hipSuccess) return RS_ERR_DEVICE;
+        return 0;
+    }
     ~DevPlan() {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(device);
+        if (ready) {  // the build may still be in flight: its buffers must outlive it
+            (void)hipEventSynchronize(ready);
+            (void)hipEventDestroy(ready);
+        }
+        if (h_stage) (void)hipHostFree(h_stage);
         if (blob) {
             (void)hipFree(blob);
         } else {
@@ -175,9 +199,21 @@ struct PlanBlob {
         }
         return o;
     }
-    int upload(DevPlan& p) {
+    // Allocates the plan's buffer and uploads the prefix on stream st, from a pinned copy the plan keeps
+    // until the copy is done (no null-stream copy: a new pattern must not stall unrelated streams).
+    int upload(DevPlan& p, hipStream_t st) {
         HIP_TRY(hipMalloc(&p.blob, total));
-        HIP_TRY(hipMemcpy(p.blob, host.data(), host.size(), hipMemcpyHostToDevice));
+        p.built_on = st;
+        if (host.empty()) return 0;
+        HIP_TRY(hipHostMalloc(&p.h_stage, host.size(), hipHostMallocDefault));
+        std::memcpy(p.h_stage, host.data(), host.size());
+        HIP_TRY(hipMemcpyAsync(p.blob, p.h_stage, host.size(), hipMemcpyHostToDevice, st));
+        return 0;
+    }
+    // marks the end of the plan's build work queued on its stream
+    static int finish(DevPlan& p) {
+        HIP_TRY(hipEventCreateWithFlags(&p.ready, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(p.ready, p.built_on));
         return 0;
     }
     template <class T>
@@ -191,7 +227,7 @@ int upload(void** dst, const void* src, size_t bytes) {
 }
 
 int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::vector<int32_t> in_slots,
-               std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out) {
+               std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out, hipStream_t st) {
     auto p = std::make_unique<DevPlan>();
     p->device = device;
     p->m = m <= 8 ? 8 : 16;
@@ -265,7 +301,7 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
     const size_t o_in = blob.add(in_slots.data(), in_slots.size() * 4);
     const size_t o_out = blob.add(out_slots.data(), out_slots.size() * 4);
     const size_t o_coef = blob.add(coef.data(), coef.size() * 4);
-    if ((rc = blob.upload(*p))) return rc;
+    if ((rc = blob.upload(*p, st)) || (rc = PlanBlob::finish(*p))) return rc;
     if (o_idx != SIZE_MAX) p->d_idx = PlanBlob::at<uint32_t>(*p, o_idx);
     p->d_in = PlanBlob::at<int32_t>(*p, o_in);
     p->d_out = PlanBlob::at<int32_t>(*p, o_out);
@@ -286,7 +322,7 @@ int build_plan(int device, int m, std::vector<uint16_t> M, int K, int R, std::ve
 // index records: tens of ms on the host, well under one on the GPU). Synchronous, like build_plan.
 int build_plan_m16_device(int device, const std::vector<uint16_t>& targets, const std::vector<int>& emit,
                           const std::vector<uint16_t>& sources, std::vector<int32_t> in_slots,
-                          std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out) {
+                          std::vector<int32_t> out_slots, std::unique_ptr<DevPlan>& out, hipStream_t st) {
     const Field& F = field();
     const int K = int(sources.size()), R = int(emit.size()), d = int(targets.size());
     auto p = std::make_unique<DevPlan>();
@@ -306,45 +342,42 @@ int build_plan_m16_device(int device, const std::vector<uint16_t>& targets, cons
     std::vector<uint16_t> y(static_cast<size_t>(K)), x(static_cast<size_t>(d));
     for (int q = 0; q < K; ++q) y[size_t(q)] = F.exp[sources[size_t(q)]];
     for (int e = 0; e < d; ++e) x[size_t(e)] = F.exp[targets[size_t(e)]];
-    // plan arrays in one allocation: [in][out] uploaded, then [coef][records] zeroed and filled on the
-    // device; the build's temporaries [y][x][emit][lp][ld] in a second one, freed on return
+    // one allocation: [in][out][y][x][emit] uploaded on the caller's stream, then [lp][ld][coef][records]
+    // zeroed and filled on the device there too (the build's temporaries y .. ld stay with the plan:
+    // freeing them here would wait for the device)
     out_slots.resize(std::max(size_t(p->ntiles) * p->rt, size_t((R + 31) / 32) * 32), 0);
     in_slots.resize(in_slots.size() + 16, 0);
     PlanBlob blob;
     const size_t o_in = blob.add(in_slots.data(), in_slots.size() * 4);
     const size_t o_out = blob.add(out_slots.data(), out_slots.size() * 4);
+    const size_t o_y = blob.add(y.data(), y.size() * 2), o_x = blob.add(x.data(), x.size() * 2);
+    const size_t o_emit = blob.add(emit.data(), emit.size() * 4);
     const size_t up = blob.host.size();
+    const size_t o_lp = blob.add(nullptr, size_t(K) * 4), o_ld = blob.add(nullptr, size_t(R) * 4);
     const size_t o_coef = blob.add(nullptr, coef_bytes);
     const size_t o_idx = records ? blob.add(nullptr, rec_bytes) : SIZE_MAX;
-    if ((rc = blob.upload(*p))) return rc;
-    HIP_TRY(hipMemsetAsync(PlanBlob::at<uint8_t>(*p, up), 0, blob.total - up, nullptr));
+    if ((rc = blob.upload(*p, st))) return rc;
+    HIP_TRY(hipMemsetAsync(PlanBlob::at<uint8_t>(*p, up), 0, blob.total - up, st));
     p->d_in = PlanBlob::at<int32_t>(*p, o_in);
     p->d_out = PlanBlob::at<int32_t>(*p, o_out);
     p->d_coef = PlanBlob::at<uint32_t>(*p, o_coef);
     if (records) p->d_idx = PlanBlob::at<uint32_t>(*p, o_idx);
-    PlanBlob tb;
-    const size_t o_y = tb.add(y.data(), y.size() * 2), o_x = tb.add(x.data(), x.size() * 2);
-    const size_t o_emit = tb.add(emit.data(), emit.size() * 4);
-    const size_t o_lp = tb.add(nullptr, size_t(K) * 4), o_ld = tb.add(nullptr, size_t(R) * 4);
-    DevPlan tmp;  // owns the temporaries' allocation
-    tmp.device = device;
-    if ((rc = tb.upload(tmp))) return rc;
     Plan16Args a{};
-    a.src_el = PlanBlob::at<const uint16_t>(tmp, o_y);
-    a.tgt_el = PlanBlob::at<const uint16_t>(tmp, o_x);
-    a.emit = PlanBlob::at<const int32_t>(tmp, o_emit);
+    a.src_el = PlanBlob::at<const uint16_t>(*p, o_y);
+    a.tgt_el = PlanBlob::at<const uint16_t>(*p, o_x);
+    a.emit = PlanBlob::at<const int32_t>(*p, o_emit);
     a.logt = logt;
     a.expt = expt;
-    a.lp = PlanBlob::at<uint32_t>(tmp, o_lp);
-    a.ld = PlanBlob::at<uint32_t>(tmp, o_ld);
+    a.lp = PlanBlob::at<uint32_t>(*p, o_lp);
+    a.ld = PlanBlob::at<uint32_t>(*p, o_ld);
     a.coef = p->d_coef;
     a.rec = records ? reinterpret_cast<uint8_t*>(p->d_idx) : nullptr;
     a.K = K;
     a.d = d;
     a.R = R;
     a.rt = p->rt;
-    HIP_TRY(launch_plan_m16(a, nullptr));
-    HIP_TRY(hipStreamSynchronize(nullptr));
+    HIP_TRY(launch_plan_m16(a, st));
+    if ((rc = PlanBlob::finish(*p))) return rc;
     in_slots.resize(size_t(K));
     p->in_slots = std::move(in_slots);
     p->out_slots = std::move(out_slots);
@@ -459,16 +492,16 @@ static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r
 
 // The device plan of the encode (erased == NULL) or decode matrix: GF(2^16) codes with large matrices
 // are built on the device, everything else from the host matrix.
-static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out) {
+static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
     std::vector<uint16_t> targets, sources;
     std::vector<int> emit;
     std::vector<int32_t> in, outs;
     codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
     const int K = int(in.size()), R = int(outs.size());
     if (c->m > 8 && R > 0 && (c->m16_plans == 1 || (c->m16_plans == 2 && int64_t(K) * R >= (int64_t(1) << 16))))
-        return build_plan_m16_device(c->device, targets, emit, sources, std::move(in), std::move(outs), out);
+        return build_plan_m16_device(c->device, targets, emit, sources, std::move(in), std::move(outs), out, st);
     std::vector<uint16_t> M = solve_matrix(targets, emit, sources);
-    return build_plan(c->device, c->m, std::move(M), K, R, std::move(in), std::move(outs), out);
+    return build_plan(c->device, c->m, std::move(M), K, R, std::move(in), std::move(outs), out, st);
 }
 
 extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t** out) {
@@ -493,7 +526,8 @@ extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t*
     c->m = subfield_degree(c->positions);
     int rc = device_tables(device, &c->d_ltab);
     if (rc) return rc;
-    if ((rc = make_plan(c.get(), nullptr, c->enc))) return rc;
+    if ((rc = make_plan(c.get(), nullptr, c->enc, nullptr))) return rc;
+    HIP_TRY(hipStreamSynchronize(nullptr));  // the encode plan is complete before any stream uses it
     *out = c.release();
     return 0;
 }
@@ -550,7 +584,8 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
             HIP_TRY(hipSetDevice(c->device));
             HIP_TRY(hipDeviceSynchronize());  // the old encode plan may still be in use
             std::unique_ptr<DevPlan> e;
-            if (int rc = make_plan(c, nullptr, e)) return rc;
+            if (int rc = make_plan(c, nullptr, e, nullptr)) return rc;
+            HIP_TRY(hipStreamSynchronize(nullptr));
             c->enc = std::move(e);
         }
         return 0;
@@ -579,6 +614,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
                     const int32_t* d_ids = nullptr, bool dst_local = false) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
+    if (int rc = p.order_after_build(st)) return rc;
     const int64_t align = p.m == 8 ? 8 : 4;
     if ((S & 1) || (uintptr_t(src) % align) || (uintptr_t(dst) % align) || (src_stripe % align) ||
         (src_sym % align) || (dst_stripe % align) || (dst_sym % align))
@@ -693,7 +729,7 @@ extern "C" int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stri
                     int64_t(rep_symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
 }
 
-static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out) {
+static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out, hipStream_t st) {
     const size_t n = size_t(c->k) + c->r;
     if (t > c->r) return RS_ERR_CANNOT_RESTORE;
     std::vector<uint8_t> key(n);
@@ -703,7 +739,7 @@ static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPla
     auto it = c->dec.find(key);
     if (it == c->dec.end()) {
         std::unique_ptr<DevPlan> p;
-        if (int rc = make_plan(c, is_erased, p)) return rc;
+        if (int rc = make_plan(c, is_erased, p, st)) return rc;
         if (c->dec_lru.size() >= 16) {
             c->dec.erase(c->dec_lru.front());
             c->dec_lru.erase(c->dec_lru.begin());
@@ -720,7 +756,7 @@ extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, u
     if (!c || !is_erased) return RS_ERR_INVALID;
     if (t > c->r) return RS_ERR_CANNOT_RESTORE;
     DevPlan* p = nullptr;
-    int rc = decode_plan(c, is_erased, t, &p);
+    int rc = decode_plan(c, is_erased, t, &p, static_cast<hipStream_t>(stream));
     if (rc) return rc;
     uint8_t* base = static_cast<uint8_t*>(d_rcv);
     return run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
@@ -762,7 +798,8 @@ static bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
         for (int i = 0; i < n; ++i) in[size_t(i)] = i;
         for (int j = 0; j < c->r; ++j) out[size_t(j)] = j;
         std::unique_ptr<DevPlan> p;
-        if (build_plan(c->device, 8, std::move(H), n, c->r, std::move(in), std::move(out), p) || !p) {
+        if (build_plan(c->device, 8, std::move(H), n, c->r, std::move(in), std::move(out), p, nullptr) || !p ||
+            hipStreamSynchronize(nullptr) != hipSuccess) {
             c->syn_failed = true;
             return false;
         }
@@ -1187,7 +1224,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         uint16_t t = 0;
         for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.first[i] != 0));
         DevPlan* p = nullptr;
-        int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p);
+        int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
         if (rc) return rc;
         rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
                       int64_t(symbol_stride), g.second.size(), symbol_size, st, c->d_ids + first[gi]);
@@ -1487,7 +1524,7 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     // column chunks. Plans that are never specialised (GF(2^16) codes, jit = 0, a failed compile) keep
     // the chunked pipeline.
     DevPlan* dplan = nullptr;
-    if ((rc = decode_plan(c, is_erased, t, &dplan))) return rc;
+    if ((rc = decode_plan(c, is_erased, t, &dplan, im.stream))) return rc;
     const bool pending = c->m <= 8 && c->jit != 0 && !dplan->xj && !dplan->jit && !dplan->xj_failed && !dplan->jit_failed;
     const size_t P = pad16(S), W = pending ? S : chunk_width(S), nch = (S + W - 1) / W,
                  nl = lost.size();
@@ -1862,7 +1899,8 @@ int transform_apply(std::vector<uint16_t> M, const symbol_seq_t* f, symbol_seq_t
     for (size_t i = 0; i < K; ++i) in[i] = int32_t(i);
     for (size_t j = 0; j < R; ++j) out[j] = int32_t(j);
     std::unique_ptr<DevPlan> plan;
-    if (int rc = build_plan(o.device, 16, std::move(M), int(K), int(R), std::move(in), std::move(out), plan)) return rc;
+    if (int rc = build_plan(o.device, 16, std::move(M), int(K), int(R), std::move(in), std::move(out), plan, o.stream))
+        return rc;
     uint8_t* dres = o.d + K * P;
     if (int rc = run_plan(o.codec.get(), *plan, o.d, 0, int64_t(P), dres, 0, int64_t(P), 1, Se, o.stream)) return rc;
     HIP_TRY(hipMemcpyAsync(o.h + K * P, dres, R * P, hipMemcpyDeviceToHost, o.stream));

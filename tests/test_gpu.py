@@ -736,3 +736,41 @@ def test_drop_in_m8_repeated_pattern_chunked(lost):
         assert np.array_equal(got, ref), f"call {call}"
         assert np.array_equal(got[:k], full[:k]), f"call {call}"
     rs.close()
+
+
+def test_new_pattern_does_not_stall_other_streams():
+    """A decode with a new erasure pattern builds its plan on the caller's stream (pinned upload, no
+    null-stream copy): while another (blocking) stream is busy with a long encode, the decode call
+    returns with that stream still running, and its result is bit-exact."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    k, r, S = 128, 32, 65536
+    busy = torch.empty((1024, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(busy, k, 3)
+    small = torch.zeros((4, k + r, 4096), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(small, k, 4)
+    codec = rs_amd.Codec(k, r)
+    codec.encode(small)
+    codec.encode(busy[:1])  # encode kernel loaded
+    torch.cuda.synchronize()
+    full = small.cpu().numpy()
+    sa, sb = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(sa)) == 0  # default flags: a blocking stream
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(sb), 1) == 0
+    rng = np.random.default_rng(11)
+    try:
+        for trial in range(3):
+            er = np.zeros(k + r, bool)
+            er[rng.choice(k + r, 25, replace=False)] = True
+            er[trial] = True  # a new pattern with at least one information erasure
+            small[:, torch.from_numpy(er)] = 0
+            torch.cuda.synchronize()
+            for _ in range(30):  # ~90 ms of encode work on the blocking stream
+                assert codec.encode(busy, stream=sa.value) == 0
+            assert codec.decode(small, er, stream=sb.value) == 0
+            still_busy = hip.hipStreamQuery(sa) != 0  # hipErrorNotReady
+            assert hip.hipStreamSynchronize(sb) == 0 and hip.hipStreamSynchronize(sa) == 0
+            assert still_busy, "the decode call waited for the other stream"
+            assert np.array_equal(small.cpu().numpy()[:, :k], full[:, :k]), trial
+    finally:
+        hip.hipStreamDestroy(sa)
+        hip.hipStreamDestroy(sb)
