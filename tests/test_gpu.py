@@ -762,6 +762,7 @@ def test_new_pattern_does_not_stall_other_streams():
             er = np.zeros(k + r, bool)
             er[rng.choice(k + r, 25, replace=False)] = True
             er[trial] = True  # a new pattern with at least one information erasure
+            small.copy_(torch.from_numpy(full))  # the last trial left its erased repair slots zero
             small[:, torch.from_numpy(er)] = 0
             torch.cuda.synchronize()
             for _ in range(30):  # ~90 ms of encode work on the blocking stream
