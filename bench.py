@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
     ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c"],
                     help="auto = library default policy (matrix-specialised kernels, generic fallback)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="codec option (rsg_set_option), e.g. m16_route=0; repeatable")
     ap.add_argument("--cpu-stripes", type=int, default=128, help="CPU-baseline sample (stripes, resident)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (passes repeat)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
@@ -329,6 +331,9 @@ def main():
     codec = rs_amd.Codec(k, r, device=local, **opts)
     if args.kernel == "m16c":  # GF(2^16) codes: the compiled kernel
         codec.set_option("m16_mode", 2)
+    for o in args.opt:
+        name, _, value = o.partition("=")
+        codec.set_option(name, int(value))
     stripes = torch.empty((n, k + r, S), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     stripe0, _ = rs_dist.weak_shard(n, rank)  # this rank's global stripe ids: [stripe0, stripe0 + n)

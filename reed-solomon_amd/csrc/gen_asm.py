@@ -214,6 +214,56 @@ if variant in ("m16_v1", "m16_v1_plain"):
     emit(out)
     sys.exit(0)
 
+if variant == "cs16":
+    # m = 16 cyclotomic syndromes (k_cs16), one dword (two GF(2^16) words) per lane per group step.
+    # A group is 16 inputs f_a at positions L * 2^a (a cyclotomic coset, empty slots zero); a syndrome
+    # coset s owns 16 accumulators u_t (normal-basis coordinates of GF(2^16)):
+    #     u_t ^= sum_a f_a * bit_((t - a) mod 16)(z),   z = normal repr of alpha^(s * L)
+    # (alpha^(s L 2^a) is z rotated by a: Frobenius permutes the normal basis cyclically). Four 16-entry
+    # subset tables T_q over inputs 4q .. 4q + 3 make that 64 lookups per (group, coset): the index
+    # for accumulator t from table q depends only on t - 4q, so ONE gpr-index switch e(t') feeds four
+    # XORs, into accumulators t' + 4q (q = 0..3). Register contract:
+    #   T_q   v[8 + 16q : 23 + 16q]   entry e = XOR of f_(4q + d) over the set bits d of e
+    #   acc   v[72 : 199]             coset c (of the wave's 8), accumulator t in v[72 + 16c + t]
+    #   s[40:55] / s[56:71]           the (group, tile) record in two halves of 4 cosets x 16 byte indices
+    #                                 (byte t' of coset c = e(t')); s[40:55] arrives from the previous step
+    #   s[72:73]                      shift scratch
+    # Inputs %[y0] .. %[y15] (the group's 16 input dwords), %[cp] (this record; the next group's is at +128).
+    T, ACC = 8, 72
+    e("s_set_gpr_idx_off")
+    for q in range(4):
+        b = T + 16 * q
+        e(f"v_mov_b32 v{b}, 0")
+        for d, slot in enumerate((1, 2, 4, 8)):
+            e(f"v_mov_b32 v{b + slot}, %[y{4 * q + d}]")
+    for row in [(3, 1, 2), (5, 4, 1), (6, 4, 2), (7, 4, 3)] + [(8 + k, 8, k) for k in range(1, 8)]:
+        for q in range(4):
+            b = T + 16 * q
+            e(f"v_xor_b32 v{b + row[0]}, v{b + row[1]}, v{b + row[2]}")
+    first = True
+    for half in range(2):
+        buf, nxt = (40, 56) if half == 0 else (56, 40)
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (half + 1))}")
+        for cl in range(4):
+            c = 4 * half + cl
+            for pair in range(2):  # dwords (4cl + 2pair, 4cl + 2pair + 1): indices t' = 8 pair + (0..3, 4..7)
+                lo = buf + 4 * cl + 2 * pair
+                for byte in range(4):
+                    if byte:
+                        e(f"s_lshr_b64 s[72:73], s[{lo}:{lo + 1}], {8 * byte}")
+                    for h in range(2):
+                        tp = 8 * pair + 4 * h + byte
+                        sreg = f"s{lo + h}" if byte == 0 else f"s{72 + h}"
+                        e(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if first else f"s_set_gpr_idx_idx {sreg}")
+                        first = False
+                        for q in range(4):
+                            acc = ACC + 16 * c + (tp + 4 * q) % 16
+                            e(f"v_xor_b32 v{acc}, v{T + 16 * q}, v{acc}")
+    e("s_set_gpr_idx_off")
+    emit(out)
+    sys.exit(0)
+
 if variant in ("v1", "v1_plain"):
     # one dword per lane per step (k_apply_m8_v1): Tl v[8:23], Th v[24:39], acc v[40:71]; temps t0, t1
     tl, th, acc = 8, 24, 40

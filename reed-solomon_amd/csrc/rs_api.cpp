@@ -143,6 +143,22 @@ struct DevPlan {
     bool jit_failed = false;         // compile failed once: stay on the generic kernels
     std::unique_ptr<XjKernel> xj;    // bit-plane XOR kernel (rs_xj.hpp), if built
     bool xj_failed = false;
+    // GF(2^16) syndrome route (k_cs16, then `second`): set when this plan applies its matrix as
+    //   out = M2 * S,  S_j = sum_i X_i^j in_i (j < D)  -- the reference's own factorisation (syndromes by
+    // the cyclotomic FFT, evaluator + Forney). The arrays live in this plan's blob; `dense` is the
+    // plain matrix plan, built on demand for launches the route does not cover (stripe-id lists,
+    // symbol sizes that are not a multiple of 1 KiB).
+    struct Cs {
+        int D = 0, ngroups = 0, ntiles = 0, fin_stride = 0;
+        int32_t* groups = nullptr;
+        uint32_t* rec = nullptr;
+        int32_t* fin = nullptr;
+        int32_t* fin_off = nullptr;
+        uint32_t nblog[16] = {};
+    };
+    std::unique_ptr<Cs> cs;
+    std::unique_ptr<DevPlan> second, dense;
+    std::vector<uint8_t> erased;  // the pattern (empty: encode), to build `dense`
     int64_t uses = 0;                // launches of this plan (JIT policy)
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
     // stream-ordered build: the upload (and device fill) ran on `built_on`; `ready` marks its end, so a
@@ -397,6 +413,9 @@ struct rsg_codec {
     int m8_mode = 18;
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
+    int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
+    void* d_cs = nullptr;  // syndrome route scratch: [chunk][D][S]
+    size_t cs_cap = 0;
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
@@ -448,7 +467,7 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn, d_bp16, d_bp16_rec})
+                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -492,7 +511,192 @@ static int codec_matrix(const std::vector<uint16_t>& pos, uint16_t k, uint16_t r
 
 // The device plan of the encode (erased == NULL) or decode matrix: GF(2^16) codes with large matrices
 // are built on the device, everything else from the host matrix.
+static const std::vector<uint16_t>* normal_repr_tables();  // [li][d]: alpha^d in the normal basis of GF(2^(1 << li))
+static uint16_t normal_basis_element(int m, int i);          // i-th element of the normal basis of GF(2^m)
+
+// Second stage of the syndrome route: out_p = sum_{j < D} M2[p][j] S_j for the emitted targets p, with
+// E = all D targets. This is the reference's evaluator + Forney restore (reed_solomon.c:186-336, the same
+// for encode, E = repair positions, and decode, E = erased positions):
+//   Omega = S * Lambda_E mod x^D,  out_p = F_p * sum_{i < D} X_p^-i Omega_i,  F_p = X_p / Lambda_E'(X_p^-1)
+// so M2[p][j] = F_p x^j sum_{d = 0}^{D - 1 - j} Lambda_d x^d with x = X_p^-1 (O(D) per row).
+static std::vector<uint16_t> syndrome_solve_matrix(const std::vector<uint16_t>& targets, const std::vector<int>& emit) {
+    const Field& F = field();
+    const size_t D = targets.size(), R = emit.size();
+    std::vector<uint16_t> lam(D + 1, 0);  // Lambda_E(x) = prod (1 + X_e x), reference _rs_get_locator_poly
+    lam[0] = 1;
+    for (size_t d = 0; d < D; ++d) {
+        const uint16_t xe = F.exp[targets[d]];
+        for (size_t i = d + 1; i > 0; --i) lam[i] ^= F.mul(lam[i - 1], xe);
+    }
+    std::vector<uint16_t> M(R * D), pw(D), q(D);
+    for (size_t r = 0; r < R; ++r) {
+        const uint16_t pos = targets[size_t(emit[r])];
+        const uint16_t x = F.exp[(kN - pos) % kN];  // X_p^-1
+        pw[0] = 1;
+        for (size_t d = 1; d < D; ++d) pw[d] = F.mul(pw[d - 1], x);
+        uint16_t dl = 0;  // Lambda'(x) = sum over odd i of Lambda_i x^(i - 1)
+        for (size_t i = 1; i <= D; i += 2) dl ^= F.mul(lam[i], pw[i - 1]);
+        const uint16_t fp = F.div(F.exp[pos], dl);
+        uint16_t acc = 0;  // q[m] = sum_{d <= m} Lambda_d x^d
+        for (size_t d = 0; d < D; ++d) q[d] = acc ^= F.mul(lam[d], pw[d]);
+        for (size_t j = 0; j < D; ++j) M[r * D + j] = F.mul(F.mul(fp, pw[j]), q[D - 1 - j]);
+    }
+    return M;
+}
+
+// The syndrome route's k_cs16 plan: input groups (the codec's cyclotomic cosets, a slot per coset
+// element, -1 where the slot is not an input), syndrome cosets of j < D in tiles of 8, gpr-index records
+// and the finish lists (gen_asm.py cs16, rs_kernels.hip:k_cs16).
+struct CsHost {
+    int D = 0, ngroups = 0, ntiles = 0, fin_stride = 1;
+    std::vector<int32_t> groups, fin, fin_off;
+    std::vector<uint8_t> rec;
+};
+
+static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int32_t>& in_slots, int D) {
+    const size_t n = pos.size();
+    std::vector<char> is_in(n, 0);
+    for (int32_t v : in_slots) is_in[size_t(v)] = 1;
+    // groups: runs of slots whose positions double (a coset in cc_cosets_to_positions order), <= 16
+    std::vector<int32_t> groups;
+    std::vector<uint16_t> lead;
+    for (size_t i = 0; i < n;) {
+        size_t j = i + 1;
+        while (j < n && j - i < 16 && pos[j] == uint16_t((uint32_t(pos[j - 1]) << 1) % kN)) ++j;
+        bool any = false;
+        for (size_t a = i; a < j; ++a) any |= is_in[a] != 0;
+        if (any) {
+            for (size_t a = 0; a < 16; ++a) groups.push_back(i + a < j && is_in[i + a] ? int32_t(i + a) : -1);
+            lead.push_back(pos[i]);
+        }
+        i = j;
+    }
+    const int ng = int(lead.size());
+    // syndrome cosets: j < D grouped by s * 2^b (mod N), s the smallest member
+    std::vector<uint16_t> cs_s;
+    std::vector<std::vector<std::pair<int, int>>> cs_need;  // (b, j)
+    std::vector<char> seen(size_t(D), 0);
+    for (int j = 0; j < D; ++j) {
+        if (seen[size_t(j)]) continue;
+        cs_s.push_back(uint16_t(j));
+        cs_need.emplace_back();
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t jj = uint32_t((uint64_t(j) << b) % kN);
+            if (jj < uint32_t(D) && !seen[jj]) {
+                seen[jj] = 1;
+                cs_need.back().emplace_back(b, int(jj));
+            }
+        }
+    }
+    const int C = int(cs_s.size()), ntiles = (C + 7) / 8;
+    int fin_stride = 0;
+    for (int t = 0; t < ntiles; ++t) {
+        int cnt = 0;
+        for (int c = 8 * t; c < std::min(C, 8 * t + 8); ++c) cnt += int(cs_need[size_t(c)].size());
+        fin_stride = std::max(fin_stride, cnt);
+    }
+    const std::vector<uint16_t>& rep = normal_repr_tables()[4];
+    std::vector<uint8_t> rec(size_t(ntiles) * size_t(ng + 1) * 128, 0);
+    std::vector<int32_t> fin(size_t(ntiles) * size_t(std::max(fin_stride, 1)), 0), fin_off(size_t(ntiles) * 9, 0);
+    for (int t = 0; t < ntiles; ++t) {
+        int e = 0;
+        for (int cl = 0; cl < 8; ++cl) {
+            const int c = 8 * t + cl;
+            fin_off[size_t(t) * 9 + size_t(cl)] = e;
+            if (c >= C) continue;
+            for (auto& bj : cs_need[size_t(c)]) fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (bj.first << 4) | (bj.second << 8);
+            for (int g = 0; g < ng; ++g) {
+                const uint32_t z = rep[(uint64_t(cs_s[size_t(c)]) * lead[size_t(g)]) % kN];
+                uint8_t* r = rec.data() + ((size_t(t) * size_t(ng + 1) + size_t(g)) * 8 + size_t(cl)) * 16;
+                for (int tp = 0; tp < 16; ++tp) {  // bit d of e(t') = bit (t' - d) mod 16 of z
+                    uint8_t v = 0;
+                    for (int d = 0; d < 4; ++d) v = uint8_t(v | (((z >> ((tp - d + 16) % 16)) & 1u) << d));
+                    r[tp] = v;
+                }
+            }
+        }
+        fin_off[size_t(t) * 9 + 8] = e;
+    }
+    CsHost h;
+    h.D = D;
+    h.ngroups = ng;
+    h.ntiles = ntiles;
+    h.fin_stride = std::max(fin_stride, 1);
+    h.groups = std::move(groups);
+    h.rec = std::move(rec);
+    h.fin = std::move(fin);
+    h.fin_off = std::move(fin_off);
+    return h;
+}
+
+static int build_cs16(DevPlan& p, const std::vector<uint16_t>& pos, const std::vector<int32_t>& in_slots, int D,
+                      hipStream_t st) {
+    const CsHost h = cs16_host(pos, in_slots, D);
+    PlanBlob blob;  // groups, records and finish lists in the plan's one allocation
+    const size_t o_g = blob.add(h.groups.data(), h.groups.size() * 4), o_r = blob.add(h.rec.data(), h.rec.size());
+    const size_t o_f = blob.add(h.fin.data(), h.fin.size() * 4), o_fo = blob.add(h.fin_off.data(), h.fin_off.size() * 4);
+    if (int rc = blob.upload(p, st)) return rc;
+    if (int rc = PlanBlob::finish(p)) return rc;
+    auto cs = std::make_unique<DevPlan::Cs>();
+    cs->D = h.D;
+    cs->ngroups = h.ngroups;
+    cs->ntiles = h.ntiles;
+    cs->fin_stride = h.fin_stride;
+    cs->groups = PlanBlob::at<int32_t>(p, o_g);
+    cs->rec = PlanBlob::at<uint32_t>(p, o_r);
+    cs->fin = PlanBlob::at<int32_t>(p, o_f);
+    cs->fin_off = PlanBlob::at<int32_t>(p, o_fo);
+    for (int t = 0; t < 16; ++t) cs->nblog[t] = field().log[normal_basis_element(16, t)];
+    p.cs = std::move(cs);
+    return 0;
+}
+
+// the syndrome route pays when both sides of the matrix are large
+static bool cs_route_eligible(const rsg_codec_t* c, int K, int R, int D) {
+    return c->m > 8 && c->m16_route == 1 && K >= 64 && R >= 64 && D <= 32768;
+}
+
+static int make_plan_dense(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st);
+
+// GF(2^16) matrix on the syndrome route: the k_cs16 plan over the sources + the D x R second stage
+static int make_plan_cs(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
+    const int K = int(in.size()), R = int(outs.size()), D = int(targets.size());
+    auto p = std::make_unique<DevPlan>();
+    p->device = c->device;
+    p->m = 16;
+    p->K = K;
+    p->R = R;
+    p->in_slots = in;
+    p->out_slots = outs;
+    if (erased) p->erased.assign(erased, erased + size_t(c->k) + c->r);
+    if (int rc = build_cs16(*p, c->positions, in, D, st)) return rc;
+    std::vector<int32_t> sin(static_cast<size_t>(D));
+    for (int j = 0; j < D; ++j) sin[size_t(j)] = j;
+    std::unique_ptr<DevPlan> second;
+    if (int rc = build_plan(c->device, 16, syndrome_solve_matrix(targets, emit), D, R, std::move(sin), std::move(outs),
+                            second, st))
+        return rc;
+    p->second = std::move(second);
+    out = std::move(p);
+    return 0;
+}
+
 static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
+    const int K = int(in.size()), R = int(outs.size());
+    if (cs_route_eligible(c, K, R, int(targets.size()))) return make_plan_cs(c, erased, out, st);
+    return make_plan_dense(c, erased, out, st);
+}
+
+// the plain matrix plan (host- or device-built)
+static int make_plan_dense(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
     std::vector<uint16_t> targets, sources;
     std::vector<int> emit;
     std::vector<int32_t> in, outs;
@@ -590,6 +794,23 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "m16_route")) {  // new plans follow the setting; cached ones are dropped
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        if (c->m16_route != int(value)) {
+            c->m16_route = int(value);
+            c->dec.clear();
+            c->dec_lru.clear();
+            if (c->m > 8) {
+                HIP_TRY(hipSetDevice(c->device));
+                HIP_TRY(hipDeviceSynchronize());  // the old encode plan may still be in use
+                std::unique_ptr<DevPlan> e;
+                if (int rc = make_plan(c, nullptr, e, nullptr)) return rc;
+                HIP_TRY(hipStreamSynchronize(nullptr));
+                c->enc = std::move(e);
+            }
+        }
+        return 0;
+    }
     if (!std::strcmp(name, "syn_route")) {
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->syn_route = int(value);
@@ -610,11 +831,77 @@ static int scratch_release(rsg_codec_t* c, hipStream_t st);
 
 constexpr uint64_t kJitMinBytes = uint64_t(1) << 20;
 
+// Syndrome route launch (p.cs): k_cs16 writes the D syndromes of a chunk of stripes to scratch, then the
+// second stage applies the D x R matrix from there into the outputs.
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
-                    const int32_t* d_ids = nullptr, bool dst_local = false) {
+                    const int32_t* d_ids = nullptr, bool dst_local = false);
+
+static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
+                  int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st) {
+    const DevPlan::Cs& cs = *p.cs;
+    if ((uintptr_t(src) | uintptr_t(dst) | uint64_t(src_stripe) | uint64_t(src_sym) | uint64_t(dst_stripe) |
+         uint64_t(dst_sym)) % 4)
+        return RS_ERR_INVALID;
+    const int64_t per = int64_t(cs.D) * int64_t(S);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
+    if (int rc = scratch_acquire(c, st)) return rc;
+    if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
+    std::string second;
+    for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
+        const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
+        Cs16Args a{};
+        a.src = src + c0 * src_stripe;
+        a.src_stripe = src_stripe;
+        a.src_sym = src_sym;
+        a.groups = cs.groups;
+        a.rec = cs.rec;
+        a.fin = cs.fin;
+        a.fin_off = cs.fin_off;
+        a.fin_stride = cs.fin_stride;
+        a.dst = static_cast<uint8_t*>(c->d_cs);
+        a.dst_stripe = per;
+        a.dst_sym = int64_t(S);
+        a.logt = logt;
+        a.expt = expt;
+        for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
+        a.ngroups = cs.ngroups;
+        a.ntiles = cs.ntiles;
+        a.nchunks = int64_t(S) / 1024;
+        a.units = cn * a.nchunks;
+        HIP_TRY(launch_cs16(a, st));
+        if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,
+                              dst_stripe, dst_sym, uint64_t(cn), S, st))
+            return rc;
+        second = c->last_kernel;
+    }
+    c->last_kernel = "cs16+" + second;
+    return scratch_release(c, st);
+}
+
+static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
+                    int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
+                    const int32_t* d_ids, bool dst_local) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
     if (int rc = p.order_after_build(st)) return rc;
+    if (p.cs) {
+        HIP_TRY(hipSetDevice(c->device));
+        if (!d_ids && !dst_local && S % 1024 == 0)
+            return run_cs(c, p, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st);
+        if (!p.dense) {  // launches the route does not cover run the plain matrix plan
+            std::unique_ptr<bool[]> er;
+            if (!p.erased.empty()) {
+                er.reset(new bool[p.erased.size()]);
+                for (size_t i = 0; i < p.erased.size(); ++i) er[i] = p.erased[i] != 0;
+            }
+            if (int rc = make_plan_dense(c, er.get(), p.dense, st)) return rc;
+        }
+        return run_plan(c, *p.dense, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st, d_ids,
+                        dst_local);
+    }
     const int64_t align = p.m == 8 ? 8 : 4;
     if ((S & 1) || (uintptr_t(src) % align) || (uintptr_t(dst) % align) || (src_stripe % align) ||
         (src_sym % align) || (dst_stripe % align) || (dst_sym % align))
@@ -1703,6 +1990,8 @@ static const std::vector<uint16_t>* normal_repr_tables() {
     return tab;
 }
 
+static uint16_t normal_basis_element(int m, int i) { return kNormalBases[m_index(uint8_t(m)) + i]; }
+
 extern "C" GF_t* gf_create(void) {
     GF_t* gf = static_cast<GF_t*>(std::calloc(1, sizeof(GF_t)));
     if (!gf) return nullptr;
@@ -2001,4 +2290,34 @@ extern "C" int fft_partial_transform_cycl(GF_t* gf, const symbol_seq_t* f, const
             }
     }
     return transform_apply(std::move(M), f, res);
+}
+
+// Host-only view of the GF(2^16) syndrome route of the encode (is_erased == NULL) or decode matrix: the
+// k_cs16 plan (groups, records, finish lists) and the second-stage matrix M2 [R][D]. info = {D, ngroups,
+// ntiles, fin_stride, R}; array arguments may be NULL (query the sizes first). No GPU is used.
+extern "C" int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
+                              uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2) {
+    if (uint32_t(k) + r > kN || (is_erased && t > r)) return RS_ERR_INVALID;
+    const std::vector<uint16_t> pos = code_positions(k, r);
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(pos, k, r, is_erased, targets, emit, sources, in, outs);
+    const CsHost h = cs16_host(pos, in, int(targets.size()));
+    if (info) {
+        info[0] = h.D;
+        info[1] = h.ngroups;
+        info[2] = h.ntiles;
+        info[3] = h.fin_stride;
+        info[4] = int32_t(outs.size());
+    }
+    if (groups) std::memcpy(groups, h.groups.data(), h.groups.size() * 4);
+    if (rec) std::memcpy(rec, h.rec.data(), h.rec.size());
+    if (fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
+    if (fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);
+    if (m2) {
+        const std::vector<uint16_t> M = syndrome_solve_matrix(targets, emit);
+        std::memcpy(m2, M.data(), M.size() * 2);
+    }
+    return 0;
 }

@@ -650,6 +650,108 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
     if ((threadIdx.x & 63) == 0) atomicXor(out + s, (unsigned long long)h);
 }
 
+// ------------------------------------------- m = 16 cyclotomic syndromes (k_cs16, gen_asm.py cs16)
+// Block = 4 waves on one 1 KiB column chunk of one stripe (one dword per lane), one tile of 8 syndrome
+// cosets (128 accumulators per lane). Per input group (a cyclotomic coset of up to 16 slots) the step
+// builds four subset tables and runs 8 x 16 gpr-index switches, each feeding four XORs (the
+// circulant structure of alpha^(s L 2^a), see gen_asm.py). Then the needed syndromes of each coset,
+// S_(s 2^b) = sum_t nb_((t + b) mod 16) * u_t, are formed with log / exp gathers and stored.
+__device__ __forceinline__ void cs16_step(const uint32_t (&y)[16], const uint32_t* cp, u32x16& plane, u32x16& a0,
+                                          u32x16& a1, u32x16& a2, u32x16& a3, u32x16& a4, u32x16& a5, u32x16& a6,
+                                          u32x16& a7) {
+    u32x16 T0, T1, T2, T3;
+    asm volatile(
+#include "gen/m8_idx_asm_cs16.inc"
+        : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "+{v[136:151]}"(a4),
+          "+{v[152:167]}"(a5), "+{v[168:183]}"(a6), "+{v[184:199]}"(a7), "=&{v[8:23]}"(T0), "=&{v[24:39]}"(T1),
+          "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), "+{s[40:55]}"(plane)
+        : [y0] "v"(y[0]), [y1] "v"(y[1]), [y2] "v"(y[2]), [y3] "v"(y[3]), [y4] "v"(y[4]), [y5] "v"(y[5]),
+          [y6] "v"(y[6]), [y7] "v"(y[7]), [y8] "v"(y[8]), [y9] "v"(y[9]), [y10] "v"(y[10]), [y11] "v"(y[11]),
+          [y12] "v"(y[12]), [y13] "v"(y[13]), [y14] "v"(y[14]), [y15] "v"(y[15]), [cp] "s"(cp)
+        : "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
+          "s72", "s73");
+}
+
+// needed syndromes of local coset c from its 16 accumulators u (both words of the lane's dword)
+__device__ __forceinline__ void cs16_finish(const Cs16Args& a, const u32x16& u, int c, int tile, uint8_t* out) {
+    const int e0 = sload(a.fin_off + tile * 9 + c), e1 = sload(a.fin_off + tile * 9 + c + 1);
+    if (e0 >= e1) return;
+    uint32_t lg[16];  // log of each word, 0xFFFF marks a zero word
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const uint32_t lo = u[t] & 0xFFFFu, hi = u[t] >> 16;
+        lg[t] = (lo ? uint32_t(a.logt[lo]) : 0xFFFFu) | ((hi ? uint32_t(a.logt[hi]) : 0xFFFFu) << 16);
+    }
+    for (int e = e0; e < e1; ++e) {
+        const int32_t ent = sload(a.fin + int64_t(tile) * a.fin_stride + e);
+        const int b = (ent >> 4) & 15;
+        const int64_t j = ent >> 8;
+        uint32_t slo = 0, shi = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t nl = a.nblog[(t + b) & 15];
+            const uint32_t l0 = lg[t] & 0xFFFFu, l1 = lg[t] >> 16;
+            if (l0 != 0xFFFFu) {
+                const uint32_t x = l0 + nl;
+                slo ^= a.expt[x >= 65535u ? x - 65535u : x];
+            }
+            if (l1 != 0xFFFFu) {
+                const uint32_t x = l1 + nl;
+                shi ^= a.expt[x >= 65535u ? x - 65535u : x];
+            }
+        }
+        *reinterpret_cast<uint32_t*>(out + j * a.dst_sym) = slo | (shi << 16);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
+    const int64_t slot = blockIdx.x >> 3;  // XCD-aware: the tiles of one unit run back to back on one XCD
+    const int tile = int(slot % a.ntiles);
+    const int64_t unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
+    if (unit >= a.units) return;
+    const int64_t local = unit / a.nchunks;
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t col = (unit - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
+    const uint8_t* base = a.src + stripe * a.src_stripe + col;
+    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 1) * 32;
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+    u32x16 plane;  // first half of the current group's record, requested one step ahead (s[40:55])
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");
+    uint32_t yn[16];
+    auto load = [&](int g, uint32_t(&y)[16]) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int32_t sl = sload(a.groups + g * 16 + s);
+            y[s] = sl >= 0 ? *reinterpret_cast<const uint32_t*>(base + int64_t(sl) * a.src_sym) : 0u;
+        }
+    };
+    load(0, yn);
+    for (int g = 0; g < a.ngroups; ++g) {
+        uint32_t y[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) y[s] = yn[s];
+        if (g + 1 < a.ngroups) load(g + 1, yn);
+        cs16_step(y, rec + size_t(g) * 32, plane, a0, a1, a2, a3, a4, a5, a6, a7);
+    }
+    uint8_t* out = a.dst + local * a.dst_stripe + col;
+    cs16_finish(a, a0, 0, tile, out);
+    cs16_finish(a, a1, 1, tile, out);
+    cs16_finish(a, a2, 2, tile, out);
+    cs16_finish(a, a3, 3, tile, out);
+    cs16_finish(a, a4, 4, tile, out);
+    cs16_finish(a, a5, 5, tile, out);
+    cs16_finish(a, a6, 6, tile, out);
+    cs16_finish(a, a7, 7, tile, out);
+}
+
+hipError_t launch_cs16(const Cs16Args& a, hipStream_t st) {
+    if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
+    const int64_t blocks = (a.units + 7) / 8 * 8 * a.ntiles;
+    if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_cs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------- symbol-wide ops (gf_add / gf_mul / gf_madd)
 // One word (LE u16) per lane, reference src/rs/gf65536.c:155-219: add a ^= b; mul a = c * a; madd
 // a ^= c * b, products through the log / exp tables with zero words skipped (lc = log c, c != 0, 1).

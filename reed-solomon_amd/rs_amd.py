@@ -87,6 +87,7 @@ _sig("rsg_fingerprint", ctypes.c_int, P, u64, u64, u64, u32, u32, u64, P, P)
 _sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
 _sig("rsg_jit_precompile", ctypes.c_int, u16, u16, P, u16)
 _sig("rsg_gamma_tables", ctypes.c_int, P, P, P)
+_sig("rsg_route_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P, P)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("gf_create", P)
 _sig("gf_destroy", None, P)
@@ -135,6 +136,29 @@ def coding_matrix(k, r, is_erased=None):
     if rc:
         raise RSError(rc, "rsg_coding_matrix")
     return M, ins, outs
+
+
+def route_dump(k, r, is_erased=None):
+    """The GF(2^16) syndrome route of the encode / decode matrix (host only): dict with D, groups
+    [ngroups][16], rec [ntiles][ngroups + 1][8][16] (bytes), fin [ntiles][fin_stride], fin_off
+    [ntiles][9], m2 [R][D]."""
+    er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
+    t = 0 if er is None else int(er.sum())
+    info = np.zeros(5, np.int32)
+    rc = _lib.rsg_route_dump(k, r, _np_ptr(er), t, _np_ptr(info), None, None, None, None, None)
+    if rc:
+        raise RSError(rc, "rsg_route_dump")
+    D, ng, nt, fs, R = (int(v) for v in info)
+    groups = np.zeros((ng, 16), np.int32)
+    rec = np.zeros((nt, ng + 1, 8, 16), np.uint8)
+    fin = np.zeros((nt, fs), np.int32)
+    fin_off = np.zeros((nt, 9), np.int32)
+    m2 = np.zeros((R, D), np.uint16)
+    rc = _lib.rsg_route_dump(k, r, _np_ptr(er), t, None, _np_ptr(groups), _np_ptr(rec), _np_ptr(fin), _np_ptr(fin_off),
+                             _np_ptr(m2))
+    if rc:
+        raise RSError(rc, "rsg_route_dump")
+    return dict(D=D, groups=groups, rec=rec, fin=fin, fin_off=fin_off, m2=m2)
 
 
 def gamma_tables():

@@ -70,7 +70,7 @@ def test_golden_batch_api(name, variant):
     rc, out, kern, m = run_case_gpu(c, variant)
     assert rc == c["rc"], (rc, kern)
     if name.startswith("c5_") and name.endswith(("_1k", "_2k")):  # full 1 KiB chunks: the production GF(2^16) path
-        assert kern in M16_PRODUCTION, kern
+        assert kern in M16_PRODUCTION or kern.startswith("cs16+"), kern
     check_golden(c, out)
 
 

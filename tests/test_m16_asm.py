@@ -107,3 +107,46 @@ def test_m8_v1_step_matches_gf256_multiply(tmp_path):
     w.run(text.splitlines(), [])
     for p in range(32):
         assert np.array_equal(w.v[40 + p], gf256_mul_bytes(y, coef[p]) ^ acc0[p]), p
+
+
+def cs16_record(z):
+    """Byte t' of coset c = e(t'), bit d of e(t') = bit (t' - d) mod 16 of z_c (gen_asm.py cs16)."""
+    rec = np.zeros((8, 16), np.uint8)
+    for c in range(8):
+        for tp in range(16):
+            rec[c, tp] = sum(((int(z[c]) >> ((tp - d) % 16)) & 1) << d for d in range(4))
+    return rec.reshape(-1)
+
+
+def test_cs16_step_circulant_xor(tmp_path):
+    """k_cs16's group step (gen_asm.py variant cs16): for each of the wave's 8 syndrome cosets and each
+    accumulator t, acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c), both words of every lane; the record
+    halves load as the kernel expects (second half by the step, the next group's first half too)."""
+    out = os.path.join(str(tmp_path), "cs16.inc")
+    subprocess.check_call([sys.executable, GEN, out, "cs16"])
+    lines = [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(out) if ln.startswith('"')]
+    rng = np.random.default_rng(1616)
+    for trial in range(3):
+        z = rng.integers(0, 65536, 8)
+        z[:3] = [0, 0xFFFF, 1]
+        mem = Memory(8192)
+        mem.b[1024:1152] = cs16_record(z)
+        f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
+        f[5] = 0  # an empty slot
+        acc0 = rng.integers(0, 2 ** 32, (128, 64), dtype=np.uint64).astype(np.uint32)
+        text = "\n".join(lines).replace("%[cp]", "s[90:91]")
+        for a in range(16):
+            text = text.replace(f"%[y{a}]", f"v{200 + a}")
+        w = Wave(mem, {})
+        for a in range(16):
+            w.v[200 + a] = f[a]
+        w.v[72:200] = acc0
+        w.s[90], w.s[91] = 1024, 0
+        w.run(["s_load_dwordx16 s[40:55], s[90:91], 0x0"] + text.splitlines(), [])
+        for c in range(8):
+            for t in range(16):
+                want = acc0[16 * c + t].copy()
+                for a in range(16):
+                    if (int(z[c]) >> ((t - a) % 16)) & 1:
+                        want ^= f[a]
+                assert np.array_equal(w.v[72 + 16 * c + t], want), (trial, c, t)
