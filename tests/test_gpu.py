@@ -416,6 +416,7 @@ def test_m16_kernels_vs_oracle(S, mode, plans):
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route", 0)  # the dense kernels under test (the syndrome route has its own tests)
     codec.set_option("m16_mode", mode)
     codec.set_option("m16_plans", plans)  # rebuilds the encode plan
     assert codec.subfield == 16
@@ -523,20 +524,25 @@ def test_xor_kernel_shapes_vs_oracle(k, r):
 
 @pytest.mark.parametrize("k,r,S", [(250, 33, 1024), (300, 64, 2048 + 40), (200, 65, 1024 + 1000), (1000, 100, 2048),
                                    (400, 129, 3072 + 4), (2000, 100, 1024)])
-def test_m16_kernel_shapes_vs_oracle(k, r, S):
+@pytest.mark.parametrize("route", [0, 1])
+def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
     1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle. Two
-    stripes make small grids, so every case also runs split-K (k=2000: 31 input slices)."""
+    stripes make small grids, so every case also runs split-K (k=2000: 31 input slices). Route 0: the
+    dense kernel; route 1: the syndrome route where it applies (R, K >= 64, whole 1 KiB chunks; other
+    launches of a route plan fall back to its dense plan)."""
     rng = np.random.default_rng(k + 7 * r + S)
     n = 2
     host = np.zeros((n, k + r, S), np.uint8)
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route", route)
     assert codec.subfield == 16
     codec.encode(dev)
     torch.cuda.synchronize()
-    assert codec.last_kernel == "apply_m16_v1"
+    routed = route == 1 and k >= 64 and r >= 64 and S % 1024 == 0
+    assert codec.last_kernel == ("cs16+apply_m16_v1" if routed else "apply_m16_v1"), codec.last_kernel
     got = dev.cpu().numpy()
     want = host.copy()
     for s in range(n):
