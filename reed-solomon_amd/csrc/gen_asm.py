@@ -214,6 +214,19 @@ if variant in ("m16_v1", "m16_v1_plain"):
     emit(out)
     sys.exit(0)
 
+if variant == "cs16_pro":
+    # k_cs16 prologue: group 0's inputs in flight into v[200:215], group 1's slot offsets in s[76:91],
+    # group 0's first record half in s[40:55] (operands %[g0] offsets array, %[r0] records, %[rsrc], %[lane])
+    e("s_load_dwordx16 s[76:91], %[g0], 0x0")
+    e("s_waitcnt lgkmcnt(0)")
+    for a in range(16):
+        e(f"v_add_u32 %[t0], s{76 + a}, %[lane]")
+        e(f"buffer_load_dword v{200 + a}, %[t0], %[rsrc], 0 offen")
+    e("s_load_dwordx16 s[76:91], %[g0], 0x40")
+    e("s_load_dwordx16 s[40:55], %[r0], 0x0")
+    emit(out)
+    sys.exit(0)
+
 if variant == "cs16":
     # m = 16 cyclotomic syndromes (k_cs16), one dword (two GF(2^16) words) per lane per group step.
     # A group is 16 inputs f_a at positions L * 2^a (a cyclotomic coset, empty slots zero); a syndrome
@@ -225,26 +238,40 @@ if variant == "cs16":
     # XORs, into accumulators t' + 4q (q = 0..3). Register contract:
     #   T_q   v[8 + 16q : 23 + 16q]   entry e = XOR of f_(4q + d) over the set bits d of e
     #   acc   v[72 : 199]             coset c (of the wave's 8), accumulator t in v[72 + 16c + t]
+    #   L     v[200 : 215]            the next group's inputs, loaded by this step (raw buffer loads at
+    #                                 voffset = %[lane] + slot offset; an empty slot's offset 0x80000000 is
+    #                                 out of range, so it loads 0)
     #   s[40:55] / s[56:71]           the (group, tile) record in two halves of 4 cosets x 16 byte indices
     #                                 (byte t' of coset c = e(t')); s[40:55] arrives from the previous step
     #   s[72:73]                      shift scratch
-    # Inputs %[y0] .. %[y15] (the group's 16 input dwords), %[cp] (this record; the next group's is at +128).
-    T, ACC = 8, 72
-    e("s_set_gpr_idx_off")
+    #   s[76:91]                      byte offsets of the next group's 16 slots (from the previous step)
+    # Operands: %[cp] this record (the next group's at +128), %[gp] the group-offset record of the group
+    # after next, %[rsrc] the stripe's V#, %[lane] the lane's byte column, %[t0] %[t1] address scratch.
+    T, ACC, LD = 8, 72, 200
+    e("s_waitcnt vmcnt(0)")  # this group's inputs (loaded by the previous step)
     for q in range(4):
         b = T + 16 * q
         e(f"v_mov_b32 v{b}, 0")
         for d, slot in enumerate((1, 2, 4, 8)):
-            e(f"v_mov_b32 v{b + slot}, %[y{4 * q + d}]")
+            e(f"v_mov_b32 v{b + slot}, v{LD + 4 * q + d}")
+    e("s_waitcnt lgkmcnt(0)")  # record half 0 and the next group's slot offsets
+    for a in range(16):  # the next group's inputs
+        t = "%[t0]" if a % 2 == 0 else "%[t1]"
+        e(f"v_add_u32 {t}, s{76 + a}, %[lane]")
+        e(f"buffer_load_dword v{LD + a}, {t}, %[rsrc], 0 offen")
     for row in [(3, 1, 2), (5, 4, 1), (6, 4, 2), (7, 4, 3)] + [(8 + k, 8, k) for k in range(1, 8)]:
         for q in range(4):
             b = T + 16 * q
             e(f"v_xor_b32 v{b + row[0]}, v{b + row[1]}, v{b + row[2]}")
     first = True
     for half in range(2):
-        buf, nxt = (40, 56) if half == 0 else (56, 40)
-        e("s_waitcnt lgkmcnt(0)")
-        e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (half + 1))}")
+        buf = 40 if half == 0 else 56
+        if half == 0:
+            e("s_load_dwordx16 s[56:71], %[cp], 0x40")
+        else:
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_load_dwordx16 s[40:55], %[cp], 0x80")  # the next group's first half
+            e("s_load_dwordx16 s[76:91], %[gp], 0x0")   # slot offsets of the group after next
         for cl in range(4):
             c = 4 * half + cl
             for pair in range(2):  # dwords (4cl + 2pair, 4cl + 2pair + 1): indices t' = 8 pair + (0..3, 4..7)

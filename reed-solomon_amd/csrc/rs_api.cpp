@@ -150,7 +150,8 @@ struct DevPlan {
     // symbol sizes that are not a multiple of 1 KiB).
     struct Cs {
         int D = 0, ngroups = 0, ntiles = 0, fin_stride = 0;
-        int32_t* groups = nullptr;
+        int64_t max_slot = 0;       // largest input slot (the loads' byte range)
+        int32_t* groups = nullptr;  // [ngroups + 2][16] input slots, -1 = none
         uint32_t* rec = nullptr;
         int32_t* fin = nullptr;
         int32_t* fin_off = nullptr;
@@ -416,6 +417,8 @@ struct rsg_codec {
     int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
     void* d_cs = nullptr;  // syndrome route scratch: [chunk][D][S]
     size_t cs_cap = 0;
+    void* d_goff = nullptr;  // syndrome route: the plan's input slots as byte offsets of this launch
+    size_t goff_cap = 0;
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
@@ -467,7 +470,7 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs})
+                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_goff})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -572,6 +575,7 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
         i = j;
     }
     const int ng = int(lead.size());
+    groups.resize(groups.size() + 32, -1);  // two padding groups: the kernel prefetches two groups ahead
     // syndrome cosets: j < D grouped by s * 2^b (mod N), s the smallest member
     std::vector<uint16_t> cs_s;
     std::vector<std::vector<std::pair<int, int>>> cs_need;  // (b, j)
@@ -646,6 +650,7 @@ static int build_cs16(DevPlan& p, const std::vector<uint16_t>& pos, const std::v
     cs->rec = PlanBlob::at<uint32_t>(p, o_r);
     cs->fin = PlanBlob::at<int32_t>(p, o_f);
     cs->fin_off = PlanBlob::at<int32_t>(p, o_fo);
+    for (int32_t v : in_slots) cs->max_slot = std::max<int64_t>(cs->max_slot, v);
     for (int t = 0; t < 16; ++t) cs->nblog[t] = field().log[normal_basis_element(16, t)];
     p.cs = std::move(cs);
     return 0;
@@ -847,6 +852,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
     if (int rc = scratch_acquire(c, st)) return rc;
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
+    const int ngo = (cs.ngroups + 2) * 16;
+    if (int rc = grow(&c->d_goff, c->goff_cap, size_t(ngo) * 4)) return rc;
+    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff), ngo, src_sym, st));
     const uint16_t *logt = nullptr, *expt = nullptr;
     const uint8_t* g8 = nullptr;
     if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
@@ -857,7 +865,8 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.src = src + c0 * src_stripe;
         a.src_stripe = src_stripe;
         a.src_sym = src_sym;
-        a.groups = cs.groups;
+        a.goff = static_cast<const uint32_t*>(c->d_goff);
+        a.in_bytes = uint32_t(cs.max_slot * src_sym + int64_t(S));
         a.rec = cs.rec;
         a.fin = cs.fin;
         a.fin_off = cs.fin_off;
@@ -889,7 +898,7 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     if (int rc = p.order_after_build(st)) return rc;
     if (p.cs) {
         HIP_TRY(hipSetDevice(c->device));
-        if (!d_ids && !dst_local && S % 1024 == 0)
+        if (!d_ids && !dst_local && S % 1024 == 0 && p.cs->max_slot * src_sym + int64_t(S) < (int64_t(1) << 31))
             return run_cs(c, p, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st);
         if (!p.dense) {  // launches the route does not cover run the plain matrix plan
             std::unique_ptr<bool[]> er;
@@ -2311,7 +2320,7 @@ extern "C" int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uin
         info[3] = h.fin_stride;
         info[4] = int32_t(outs.size());
     }
-    if (groups) std::memcpy(groups, h.groups.data(), h.groups.size() * 4);
+    if (groups) std::memcpy(groups, h.groups.data(), size_t(h.ngroups) * 16 * 4);  // without the padding groups
     if (rec) std::memcpy(rec, h.rec.data(), h.rec.size());
     if (fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
     if (fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);

@@ -654,22 +654,25 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
 // Block = 4 waves on one 1 KiB column chunk of one stripe (one dword per lane), one tile of 8 syndrome
 // cosets (128 accumulators per lane). Per input group (a cyclotomic coset of up to 16 slots) the step
 // builds four subset tables and runs 8 x 16 gpr-index switches, each feeding four XORs (the
-// circulant structure of alpha^(s L 2^a), see gen_asm.py). Then the needed syndromes of each coset,
-// S_(s 2^b) = sum_t nb_((t + b) mod 16) * u_t, are formed with log / exp gathers and stored.
-__device__ __forceinline__ void cs16_step(const uint32_t (&y)[16], const uint32_t* cp, u32x16& plane, u32x16& a0,
-                                          u32x16& a1, u32x16& a2, u32x16& a3, u32x16& a4, u32x16& a5, u32x16& a6,
-                                          u32x16& a7) {
+// circulant structure of alpha^(s L 2^a), see gen_asm.py), and loads the next group's inputs with
+// raw buffer loads (empty slots read out of range, i.e. zero). Then the needed syndromes of each
+// coset, S_(s 2^b) = sum_t nb_((t + b) mod 16) * u_t, are formed with log / exp gathers and stored.
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void cs16_step(const uint32_t* cp, const uint32_t* gp, u32x4s rsrc, uint32_t lane,
+                                          u32x16& ld, u32x16& plane, u32x16& goff, u32x16& a0, u32x16& a1,
+                                          u32x16& a2, u32x16& a3, u32x16& a4, u32x16& a5, u32x16& a6, u32x16& a7) {
     u32x16 T0, T1, T2, T3;
+    uint32_t t0, t1;
     asm volatile(
 #include "gen/m8_idx_asm_cs16.inc"
         : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "+{v[136:151]}"(a4),
           "+{v[152:167]}"(a5), "+{v[168:183]}"(a6), "+{v[184:199]}"(a7), "=&{v[8:23]}"(T0), "=&{v[24:39]}"(T1),
-          "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), "+{s[40:55]}"(plane)
-        : [y0] "v"(y[0]), [y1] "v"(y[1]), [y2] "v"(y[2]), [y3] "v"(y[3]), [y4] "v"(y[4]), [y5] "v"(y[5]),
-          [y6] "v"(y[6]), [y7] "v"(y[7]), [y8] "v"(y[8]), [y9] "v"(y[9]), [y10] "v"(y[10]), [y11] "v"(y[11]),
-          [y12] "v"(y[12]), [y13] "v"(y[13]), [y14] "v"(y[14]), [y15] "v"(y[15]), [cp] "s"(cp)
+          "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), "+{v[200:215]}"(ld), "+{s[40:55]}"(plane), "+{s[76:91]}"(goff),
+          [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [cp] "s"(cp), [gp] "s"(gp), [rsrc] "s"(rsrc), [lane] "v"(lane)
         : "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
-          "s72", "s73");
+          "s72", "s73", "memory");
 }
 
 // needed syndromes of local coset c from its 16 accumulators u (both words of the lane's dword)
@@ -711,28 +714,28 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     if (unit >= a.units) return;
     const int64_t local = unit / a.nchunks;
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const int64_t col = (unit - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
-    const uint8_t* base = a.src + stripe * a.src_stripe + col;
+    const uint32_t col = uint32_t((unit - local * a.nchunks) * 1024) + threadIdx.x * 4u;
+    const uint64_t base = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
+    // raw buffer V#: base, stride 0, num_records = the inputs' byte range, 32-bit data format
+    const u32x4s rsrc = {uint32_t(base), uint32_t(base >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
     const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 1) * 32;
+    const uint32_t* goffs = a.goff;  // [ngroups + 2][16] slot byte offsets (0x80000000 = empty)
     u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
-    u32x16 plane;  // first half of the current group's record, requested one step ahead (s[40:55])
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");
-    uint32_t yn[16];
-    auto load = [&](int g, uint32_t(&y)[16]) {
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int32_t sl = sload(a.groups + g * 16 + s);
-            y[s] = sl >= 0 ? *reinterpret_cast<const uint32_t*>(base + int64_t(sl) * a.src_sym) : 0u;
-        }
-    };
-    load(0, yn);
-    for (int g = 0; g < a.ngroups; ++g) {
-        uint32_t y[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) y[s] = yn[s];
-        if (g + 1 < a.ngroups) load(g + 1, yn);
-        cs16_step(y, rec + size_t(g) * 32, plane, a0, a1, a2, a3, a4, a5, a6, a7);
-    }
+    u32x16 ld, plane, goff;
+    uint32_t t0;
+    // prologue: group 0's inputs in flight, group 1's offsets and group 0's first record half requested
+    asm volatile(
+#include "gen/m8_idx_asm_cs16_pro.inc"
+        : "={v[200:215]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(plane), [t0] "=&v"(t0)
+        : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
+        : "memory");
+    for (int g = 0; g < a.ngroups; ++g)
+        cs16_step(rec + size_t(g) * 32, goffs + size_t(g + 2) * 16, rsrc, col, ld, plane, goff, a0, a1, a2, a3, a4,
+                  a5, a6, a7);
+    // the last step's prefetches (padding group / records) must land before these registers are reused
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+{v[200:215]}"(ld), "+{s[40:55]}"(plane), "+{s[76:91]}"(goff)
+                 :
+                 : "memory");
     uint8_t* out = a.dst + local * a.dst_stripe + col;
     cs16_finish(a, a0, 0, tile, out);
     cs16_finish(a, a1, 1, tile, out);
@@ -742,6 +745,17 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     cs16_finish(a, a5, 5, tile, out);
     cs16_finish(a, a6, 6, tile, out);
     cs16_finish(a, a7, 7, tile, out);
+}
+
+// slot lists -> byte offsets for k_cs16 (slot * sym; -1 -> 0x80000000, out of the V#'s range)
+__global__ void k_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) goff[i] = slots[i] < 0 ? 0x80000000u : uint32_t(int64_t(slots[i]) * sym);
+}
+
+hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym, hipStream_t st) {
+    hipLaunchKernelGGL(k_cs16_goff, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, slots, goff, n, sym);
+    return hipGetLastError();
 }
 
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st) {

@@ -101,7 +101,9 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
 struct Cs16Args {
     const uint8_t* src;       // stripe 0 of the input layout
     int64_t src_stripe, src_sym;
-    const int32_t* groups;    // [ngroups][16] input slot of position L_g * 2^a, or -1 (zero input)
+    const uint32_t* goff;     // [ngroups + 2][16] byte offset (slot * src_sym) of the input at position
+                              // L_g * 2^a; 0x80000000 = no input there (loads out of range: zero)
+    uint32_t in_bytes;        // inputs' byte range past the stripe base (< 2^31; the V#'s num_records)
     const uint32_t* rec;      // [ntiles][ngroups + 1][32] packed gpr-index records (gen_asm.py cs16)
     const int32_t* fin;       // [ntiles][fin_stride] needed syndromes: local coset | b << 4 | j << 8
     const int32_t* fin_off;   // [ntiles][9] entries of local coset c: [fin_off[c], fin_off[c + 1])
@@ -117,6 +119,8 @@ struct Cs16Args {
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);
+// goff[i] = slots[i] * sym (0x80000000 for slots[i] < 0), i < n
+hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym, hipStream_t st);
 
 // symbol-wide word ops over nw words: op 0 a ^= b, 1 a = c * a, 2 a ^= c * b (lc = log c; logt / expt:
 // discrete log and alpha^i tables, i < 65535)

@@ -120,8 +120,10 @@ def cs16_record(z):
 
 def test_cs16_step_circulant_xor(tmp_path):
     """k_cs16's group step (gen_asm.py variant cs16): for each of the wave's 8 syndrome cosets and each
-    accumulator t, acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c), both words of every lane; the record
-    halves load as the kernel expects (second half by the step, the next group's first half too)."""
+    accumulator t, acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) from the current inputs in v[200:215],
+    both words of every lane; meanwhile the next group's inputs load into v[200:215] at lane + slot
+    offset (an offset of 0x80000000 is out of the V#'s range: zero) and the record / offset buffers for
+    the following step are requested."""
     out = os.path.join(str(tmp_path), "cs16.inc")
     subprocess.check_call([sys.executable, GEN, out, "cs16"])
     lines = [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(out) if ln.startswith('"')]
@@ -129,20 +131,31 @@ def test_cs16_step_circulant_xor(tmp_path):
     for trial in range(3):
         z = rng.integers(0, 65536, 8)
         z[:3] = [0, 0xFFFF, 1]
-        mem = Memory(8192)
+        mem = Memory(1 << 16)
         mem.b[1024:1152] = cs16_record(z)
+        mem.b[1152:1280] = cs16_record(rng.integers(0, 65536, 8))  # the next group's record
+        data = rng.integers(0, 256, 16384, dtype=np.uint8)
+        mem.b[32768:32768 + 16384] = data  # stripe inputs: 16 symbols of 1 KiB at the V# base
+        offs = np.array([1024 * ((a * 7) % 16) for a in range(16)], np.uint32)
+        offs[3] = 0x80000000  # an empty slot
+        mem.b[4096:4160] = offs.astype("<u4").view(np.uint8)  # next group's offsets (already in s[76:91])
+        mem.b[4160:4224] = rng.integers(0, 2 ** 31, 16).astype("<u4").view(np.uint8)  # the group after next
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
-        f[5] = 0  # an empty slot
+        f[5] = 0  # an empty slot of the current group
         acc0 = rng.integers(0, 2 ** 32, (128, 64), dtype=np.uint64).astype(np.uint32)
-        text = "\n".join(lines).replace("%[cp]", "s[90:91]")
-        for a in range(16):
-            text = text.replace(f"%[y{a}]", f"v{200 + a}")
+        text = "\n".join(lines)
+        text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[92:93]").replace("%[rsrc]", "s[96:99]")
+                .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
         w = Wave(mem, {})
-        for a in range(16):
-            w.v[200 + a] = f[a]
+        w.v[200:216] = f
         w.v[72:200] = acc0
-        w.s[90], w.s[91] = 1024, 0
-        w.run(["s_load_dwordx16 s[40:55], s[90:91], 0x0"] + text.splitlines(), [])
+        lane = (np.arange(64) * 4 + 256).astype(np.uint32)
+        w.v[230] = lane
+        w.s[100], w.s[101] = 1024, 0
+        w.s[92], w.s[93] = 4160, 0
+        w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
+        w.s[76:92] = offs.astype(np.uint64)
+        w.run(["s_load_dwordx16 s[40:55], s[100:101], 0x0"] + text.splitlines(), [])
         for c in range(8):
             for t in range(16):
                 want = acc0[16 * c + t].copy()
@@ -150,3 +163,9 @@ def test_cs16_step_circulant_xor(tmp_path):
                     if (int(z[c]) >> ((t - a) % 16)) & 1:
                         want ^= f[a]
                 assert np.array_equal(w.v[72 + 16 * c + t], want), (trial, c, t)
+        words = data.view("<u4")
+        for a in range(16):
+            want = np.zeros(64, np.uint32) if offs[a] == 0x80000000 else words[(offs[a] + lane) // 4]
+            assert np.array_equal(w.v[200 + a], want), (trial, a)
+        assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
+        assert list(w.s[40:56]) == list(mem.load32(np.uint64(1152) + 4 * np.arange(16, dtype=np.uint64)))

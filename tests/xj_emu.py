@@ -136,7 +136,8 @@ class Wave:
             elif op == "v_mov_b32":
                 self.vset(a[0], self.val(a[1]))
             elif op == "v_add_u32":
-                self.vset(a[0], (self.val(a[1]).astype(np.uint64) + self.val(a[2])) & np.uint64(0xFFFFFFFF))
+                self.vset(a[0], (np.asarray(self.val(a[1]), np.uint64) + np.asarray(self.val(a[2]), np.uint64))
+                          & np.uint64(0xFFFFFFFF))
             elif op == "v_xor_b32":
                 self.vset(a[0], self.val(a[1]) ^ self.val(a[2]))
             elif op == "v_and_b32":
@@ -217,8 +218,13 @@ class Wave:
                 self.vset(a[0], h << np.uint32(16) if op.endswith("_hi") else h)
             elif op == "buffer_load_dword":
                 assert a[3].endswith("offen"), ln
-                addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
-                self.vset(a[0], self.mem.load32(addr))
+                voff = self.val(a[1]).astype(np.uint64)
+                addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + voff
+                # raw buffer (stride 0) range check on the VGPR offset: out of range loads return 0
+                nrec = int(self.s[int(re.match(r"s\[(\d+):", a[2]).group(1)) + 2])
+                inb = voff < np.uint64(nrec)
+                data = self.mem.load32(np.where(inb, addr, np.uint64(0)))
+                self.vset(a[0], np.where(inb, data, np.uint32(0)))
             elif op == "buffer_store_dword":
                 addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
                 self.mem.store32(addr, self.val(a[0]))
