@@ -118,8 +118,8 @@ int rsg_xj_basis(int32_t* pivots, uint16_t* beta_y, uint8_t* bits256);
 /* GF(256)^2 coordinate tables used by the m <= 8 kernels (lbyte/ibyte: 2 x 256 entries each). */
 int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
 /* GF(2^16) syndrome route of the encode (is_erased == NULL) or decode matrix:
- * the k_cs16 plan -- groups [ngroups][16] input slots (-1 = none), records [ntiles][ngroups + 1][128]
- * bytes, finish lists [ntiles][fin_stride] and [ntiles][9] -- and the second-stage matrix m2 [R][D]
+ * the k_cs16 plan -- groups [ngroups][16] input slots (-1 = none), records [ntiles][ngroups + 2][64]
+ * bytes, finish lists [ntiles][fin_stride] and [ntiles][5] -- and the second-stage matrix m2 [R][D]
  * (out = m2 * syndromes). info = {D, ngroups, ntiles, fin_stride, R}; arrays may be NULL. Host only. */
 int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                    uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2);

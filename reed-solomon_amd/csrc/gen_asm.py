@@ -215,19 +215,19 @@ if variant in ("m16_v1", "m16_v1_plain"):
     sys.exit(0)
 
 if variant == "cs16_pro":
-    # k_cs16 prologue: group 0's inputs in flight into v[200:215], group 1's slot offsets in s[76:91],
-    # group 0's first record half in s[40:55] (operands %[g0] offsets array, %[r0] records, %[rsrc], %[lane])
+    # k_cs16 prologue: group 0's inputs in flight into v[136:151], group 1's slot offsets in s[76:91],
+    # group 0's record in s[40:55] (operands %[g0] offsets array, %[r0] records, %[rsrc], %[lane])
     e("s_load_dwordx16 s[76:91], %[g0], 0x0")
     e("s_waitcnt lgkmcnt(0)")
     for a in range(16):
         e(f"v_add_u32 %[t0], s{76 + a}, %[lane]")
-        e(f"buffer_load_dword v{200 + a}, %[t0], %[rsrc], 0 offen")
+        e(f"buffer_load_dword v{136 + a}, %[t0], %[rsrc], 0 offen")
     e("s_load_dwordx16 s[76:91], %[g0], 0x40")
     e("s_load_dwordx16 s[40:55], %[r0], 0x0")
     emit(out)
     sys.exit(0)
 
-if variant == "cs16":
+if variant in ("cs16a", "cs16b"):
     # m = 16 cyclotomic syndromes (k_cs16), one dword (two GF(2^16) words) per lane per group step.
     # A group is 16 inputs f_a at positions L * 2^a (a cyclotomic coset, empty slots zero); a syndrome
     # coset s owns 16 accumulators u_t (normal-basis coordinates of GF(2^16)):
@@ -235,58 +235,53 @@ if variant == "cs16":
     # (alpha^(s L 2^a) is z rotated by a: Frobenius permutes the normal basis cyclically). Four 16-entry
     # subset tables T_q over inputs 4q .. 4q + 3 make that 64 lookups per (group, coset): the index
     # for accumulator t from table q depends only on t - 4q, so ONE gpr-index switch e(t') feeds four
-    # XORs, into accumulators t' + 4q (q = 0..3). Register contract:
-    #   T_q   v[8 + 16q : 23 + 16q]   entry e = XOR of f_(4q + d) over the set bits d of e
-    #   acc   v[72 : 199]             coset c (of the wave's 8), accumulator t in v[72 + 16c + t]
-    #   L     v[200 : 215]            the next group's inputs, loaded by this step (raw buffer loads at
+    # XORs, into accumulators t' + 4q (q = 0..3). A wave holds 4 cosets (152 VGPRs: 3 waves per SIMD).
+    # Register contract:
+    #   T_q   v[8 + 16q : 23 + 16q]   entry e = XOR of f_(4q + d) over the set bits d of e (entry 0 stays 0)
+    #   acc   v[72 : 135]             coset c (of the wave's 4), accumulator t in v[72 + 16c + t]
+    #   L     v[136 : 151]            the next group's inputs, loaded by this step (raw buffer loads at
     #                                 voffset = %[lane] + slot offset; an empty slot's offset 0x80000000 is
     #                                 out of range, so it loads 0)
-    #   s[40:55] / s[56:71]           the (group, tile) record in two halves of 4 cosets x 16 byte indices
-    #                                 (byte t' of coset c = e(t')); s[40:55] arrives from the previous step
+    #   records                       4 cosets x 16 byte indices (byte t' of coset c = e(t')) per group:
+    #                                 this step's in s[40:55] (cs16a) / s[56:71] (cs16b), the next group's
+    #                                 loaded into the other buffer; the kernel alternates a, b
     #   s[72:73]                      shift scratch
     #   s[76:91]                      byte offsets of the next group's 16 slots (from the previous step)
-    # Operands: %[cp] this record (the next group's at +128), %[gp] the group-offset record of the group
+    # Operands: %[cp] this record (the next group's at +64), %[gp] the group-offset record of the group
     # after next, %[rsrc] the stripe's V#, %[lane] the lane's byte column, %[t0] %[t1] address scratch.
-    T, ACC, LD = 8, 72, 200
+    T, ACC, LD = 8, 72, 136
+    cur, nxt = (40, 56) if variant == "cs16a" else (56, 40)
     e("s_waitcnt vmcnt(0)")  # this group's inputs (loaded by the previous step)
     for q in range(4):
         b = T + 16 * q
-        e(f"v_mov_b32 v{b}, 0")
         for d, slot in enumerate((1, 2, 4, 8)):
             e(f"v_mov_b32 v{b + slot}, v{LD + 4 * q + d}")
-    e("s_waitcnt lgkmcnt(0)")  # record half 0 and the next group's slot offsets
+    e("s_waitcnt lgkmcnt(0)")  # this record and the next group's slot offsets
     for a in range(16):  # the next group's inputs
         t = "%[t0]" if a % 2 == 0 else "%[t1]"
         e(f"v_add_u32 {t}, s{76 + a}, %[lane]")
         e(f"buffer_load_dword v{LD + a}, {t}, %[rsrc], 0 offen")
+    e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], 0x40")  # the next group's record
+    e("s_load_dwordx16 s[76:91], %[gp], 0x0")  # slot offsets of the group after next
     for row in [(3, 1, 2), (5, 4, 1), (6, 4, 2), (7, 4, 3)] + [(8 + k, 8, k) for k in range(1, 8)]:
         for q in range(4):
             b = T + 16 * q
             e(f"v_xor_b32 v{b + row[0]}, v{b + row[1]}, v{b + row[2]}")
     first = True
-    for half in range(2):
-        buf = 40 if half == 0 else 56
-        if half == 0:
-            e("s_load_dwordx16 s[56:71], %[cp], 0x40")
-        else:
-            e("s_waitcnt lgkmcnt(0)")
-            e("s_load_dwordx16 s[40:55], %[cp], 0x80")  # the next group's first half
-            e("s_load_dwordx16 s[76:91], %[gp], 0x0")   # slot offsets of the group after next
-        for cl in range(4):
-            c = 4 * half + cl
-            for pair in range(2):  # dwords (4cl + 2pair, 4cl + 2pair + 1): indices t' = 8 pair + (0..3, 4..7)
-                lo = buf + 4 * cl + 2 * pair
-                for byte in range(4):
-                    if byte:
-                        e(f"s_lshr_b64 s[72:73], s[{lo}:{lo + 1}], {8 * byte}")
-                    for h in range(2):
-                        tp = 8 * pair + 4 * h + byte
-                        sreg = f"s{lo + h}" if byte == 0 else f"s{72 + h}"
-                        e(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if first else f"s_set_gpr_idx_idx {sreg}")
-                        first = False
-                        for q in range(4):
-                            acc = ACC + 16 * c + (tp + 4 * q) % 16
-                            e(f"v_xor_b32 v{acc}, v{T + 16 * q}, v{acc}")
+    for c in range(4):
+        for pair in range(2):  # dwords (4c + 2pair, 4c + 2pair + 1): indices t' = 8 pair + (0..3, 4..7)
+            lo = cur + 4 * c + 2 * pair
+            for byte in range(4):
+                if byte:
+                    e(f"s_lshr_b64 s[72:73], s[{lo}:{lo + 1}], {8 * byte}")
+                for h in range(2):
+                    tp = 8 * pair + 4 * h + byte
+                    sreg = f"s{lo + h}" if byte == 0 else f"s{72 + h}"
+                    e(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if first else f"s_set_gpr_idx_idx {sreg}")
+                    first = False
+                    for q in range(4):
+                        acc = ACC + 16 * c + (tp + 4 * q) % 16
+                        e(f"v_xor_b32 v{acc}, v{T + 16 * q}, v{acc}")
     e("s_set_gpr_idx_off")
     emit(out)
     sys.exit(0)

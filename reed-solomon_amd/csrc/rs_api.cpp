@@ -574,8 +574,10 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
         }
         i = j;
     }
-    const int ng = int(lead.size());
-    groups.resize(groups.size() + 32, -1);  // two padding groups: the kernel prefetches two groups ahead
+    // the kernel steps two groups per iteration (record buffers alternate) and prefetches the inputs of
+    // the next group and the slot offsets of the one after: pad to an even count, plus 3 empty groups
+    const int ng = int(lead.size()) + int(lead.size() & 1);
+    groups.resize(size_t(ng + 3) * 16, -1);
     // syndrome cosets: j < D grouped by s * 2^b (mod N), s the smallest member
     std::vector<uint16_t> cs_s;
     std::vector<std::vector<std::pair<int, int>>> cs_need;  // (b, j)
@@ -592,26 +594,30 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
             }
         }
     }
-    const int C = int(cs_s.size()), ntiles = (C + 7) / 8;
+    constexpr int CW = 4;  // syndrome cosets per wave (k_cs16 tile)
+    const int C = int(cs_s.size()), ntiles = (C + CW - 1) / CW, nlead = int(lead.size());
     int fin_stride = 0;
     for (int t = 0; t < ntiles; ++t) {
         int cnt = 0;
-        for (int c = 8 * t; c < std::min(C, 8 * t + 8); ++c) cnt += int(cs_need[size_t(c)].size());
+        for (int c = CW * t; c < std::min(C, CW * t + CW); ++c) cnt += int(cs_need[size_t(c)].size());
         fin_stride = std::max(fin_stride, cnt);
     }
     const std::vector<uint16_t>& rep = normal_repr_tables()[4];
-    std::vector<uint8_t> rec(size_t(ntiles) * size_t(ng + 1) * 128, 0);
-    std::vector<int32_t> fin(size_t(ntiles) * size_t(std::max(fin_stride, 1)), 0), fin_off(size_t(ntiles) * 9, 0);
+    // records [tile][ng + 2][CW cosets][16 byte indices]; padding groups keep index 0 (table entry 0 = 0)
+    std::vector<uint8_t> rec(size_t(ntiles) * size_t(ng + 2) * CW * 16, 0);
+    std::vector<int32_t> fin(size_t(ntiles) * size_t(std::max(fin_stride, 1)), 0),
+        fin_off(size_t(ntiles) * (CW + 1), 0);
     for (int t = 0; t < ntiles; ++t) {
         int e = 0;
-        for (int cl = 0; cl < 8; ++cl) {
-            const int c = 8 * t + cl;
-            fin_off[size_t(t) * 9 + size_t(cl)] = e;
+        for (int cl = 0; cl < CW; ++cl) {
+            const int c = CW * t + cl;
+            fin_off[size_t(t) * (CW + 1) + size_t(cl)] = e;
             if (c >= C) continue;
-            for (auto& bj : cs_need[size_t(c)]) fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (bj.first << 4) | (bj.second << 8);
-            for (int g = 0; g < ng; ++g) {
+            for (auto& bj : cs_need[size_t(c)])
+                fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (bj.first << 4) | (bj.second << 8);
+            for (int g = 0; g < nlead; ++g) {
                 const uint32_t z = rep[(uint64_t(cs_s[size_t(c)]) * lead[size_t(g)]) % kN];
-                uint8_t* r = rec.data() + ((size_t(t) * size_t(ng + 1) + size_t(g)) * 8 + size_t(cl)) * 16;
+                uint8_t* r = rec.data() + ((size_t(t) * size_t(ng + 2) + size_t(g)) * CW + size_t(cl)) * 16;
                 for (int tp = 0; tp < 16; ++tp) {  // bit d of e(t') = bit (t' - d) mod 16 of z
                     uint8_t v = 0;
                     for (int d = 0; d < 4; ++d) v = uint8_t(v | (((z >> ((tp - d + 16) % 16)) & 1u) << d));
@@ -619,7 +625,7 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
                 }
             }
         }
-        fin_off[size_t(t) * 9 + 8] = e;
+        fin_off[size_t(t) * (CW + 1) + CW] = e;
     }
     CsHost h;
     h.D = D;
@@ -852,7 +858,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
     if (int rc = scratch_acquire(c, st)) return rc;
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
-    const int ngo = (cs.ngroups + 2) * 16;
+    const int ngo = (cs.ngroups + 3) * 16;
     if (int rc = grow(&c->d_goff, c->goff_cap, size_t(ngo) * 4)) return rc;
     HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff), ngo, src_sym, st));
     const uint16_t *logt = nullptr, *expt = nullptr;
@@ -2320,7 +2326,7 @@ extern "C" int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uin
         info[3] = h.fin_stride;
         info[4] = int32_t(outs.size());
     }
-    if (groups) std::memcpy(groups, h.groups.data(), size_t(h.ngroups) * 16 * 4);  // without the padding groups
+    if (groups) std::memcpy(groups, h.groups.data(), size_t(h.ngroups) * 16 * 4);  // even count, without the tail
     if (rec) std::memcpy(rec, h.rec.data(), h.rec.size());
     if (fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
     if (fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);

@@ -650,34 +650,43 @@ __global__ void k_fingerprint(const uint8_t* base, int64_t stripe_stride, int64_
     if ((threadIdx.x & 63) == 0) atomicXor(out + s, (unsigned long long)h);
 }
 
-// ------------------------------------------- m = 16 cyclotomic syndromes (k_cs16, gen_asm.py cs16)
-// Block = 4 waves on one 1 KiB column chunk of one stripe (one dword per lane), one tile of 8 syndrome
-// cosets (128 accumulators per lane). Per input group (a cyclotomic coset of up to 16 slots) the step
-// builds four subset tables and runs 8 x 16 gpr-index switches, each feeding four XORs (the
-// circulant structure of alpha^(s L 2^a), see gen_asm.py), and loads the next group's inputs with
-// raw buffer loads (empty slots read out of range, i.e. zero). Then the needed syndromes of each
-// coset, S_(s 2^b) = sum_t nb_((t + b) mod 16) * u_t, are formed with log / exp gathers and stored.
+// ------------------------------------------- m = 16 cyclotomic syndromes (k_cs16, gen_asm.py cs16a/b)
+// Block = 4 waves on one 1 KiB column chunk of one stripe (one dword per lane), one tile of 4 syndrome
+// cosets (64 accumulators per lane; 152 VGPRs, 3 waves per SIMD). Per input group (a cyclotomic coset
+// of up to 16 slots) the step builds four subset tables and runs 4 x 16 gpr-index switches, each feeding
+// four XORs (the circulant structure of alpha^(s L 2^a), see gen_asm.py), and loads the next group's
+// inputs with raw buffer loads (empty slots read out of range, i.e. zero). Then the needed syndromes of
+// each coset, S_(s 2^b) = sum_t nb_((t + b) mod 16) * u_t, are formed with log / exp gathers and stored.
 typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
 
+#define RS_CS16_OPERANDS                                                                                      \
+    : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "+{v[8:23]}"(T0),        \
+      "+{v[24:39]}"(T1), "+{v[40:55]}"(T2), "+{v[56:71]}"(T3), "+{v[136:151]}"(ld), "+{s[40:55]}"(ra),           \
+      "+{s[56:71]}"(rb), "+{s[76:91]}"(goff), [t0] "=&v"(t0), [t1] "=&v"(t1)                                     \
+    : [cp] "s"(cp), [gp] "s"(gp), [rsrc] "s"(rsrc), [lane] "v"(lane)                                           \
+    : "s72", "s73", "memory"
+
+// one group step; B selects the record buffer (A: this record in s[40:55], B: in s[56:71])
+template <bool B>
 __device__ __forceinline__ void cs16_step(const uint32_t* cp, const uint32_t* gp, u32x4s rsrc, uint32_t lane,
-                                          u32x16& ld, u32x16& plane, u32x16& goff, u32x16& a0, u32x16& a1,
-                                          u32x16& a2, u32x16& a3, u32x16& a4, u32x16& a5, u32x16& a6, u32x16& a7) {
-    u32x16 T0, T1, T2, T3;
+                                          u32x16& ld, u32x16& ra, u32x16& rb, u32x16& goff, u32x16& T0, u32x16& T1,
+                                          u32x16& T2, u32x16& T3, u32x16& a0, u32x16& a1, u32x16& a2, u32x16& a3) {
     uint32_t t0, t1;
-    asm volatile(
-#include "gen/m8_idx_asm_cs16.inc"
-        : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "+{v[136:151]}"(a4),
-          "+{v[152:167]}"(a5), "+{v[168:183]}"(a6), "+{v[184:199]}"(a7), "=&{v[8:23]}"(T0), "=&{v[24:39]}"(T1),
-          "=&{v[40:55]}"(T2), "=&{v[56:71]}"(T3), "+{v[200:215]}"(ld), "+{s[40:55]}"(plane), "+{s[76:91]}"(goff),
-          [t0] "=&v"(t0), [t1] "=&v"(t1)
-        : [cp] "s"(cp), [gp] "s"(gp), [rsrc] "s"(rsrc), [lane] "v"(lane)
-        : "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
-          "s72", "s73", "memory");
+    if constexpr (!B) {
+        asm volatile(
+#include "gen/m8_idx_asm_cs16a.inc"
+            RS_CS16_OPERANDS);
+    } else {
+        asm volatile(
+#include "gen/m8_idx_asm_cs16b.inc"
+            RS_CS16_OPERANDS);
+    }
 }
+#undef RS_CS16_OPERANDS
 
 // needed syndromes of local coset c from its 16 accumulators u (both words of the lane's dword)
 __device__ __forceinline__ void cs16_finish(const Cs16Args& a, const u32x16& u, int c, int tile, uint8_t* out) {
-    const int e0 = sload(a.fin_off + tile * 9 + c), e1 = sload(a.fin_off + tile * 9 + c + 1);
+    const int e0 = sload(a.fin_off + tile * 5 + c), e1 = sload(a.fin_off + tile * 5 + c + 1);
     if (e0 >= e1) return;
     uint32_t lg[16];  // log of each word, 0xFFFF marks a zero word
 #pragma unroll
@@ -718,22 +727,28 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     const uint64_t base = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
     // raw buffer V#: base, stride 0, num_records = the inputs' byte range, 32-bit data format
     const u32x4s rsrc = {uint32_t(base), uint32_t(base >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
-    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 1) * 32;
-    const uint32_t* goffs = a.goff;  // [ngroups + 2][16] slot byte offsets (0x80000000 = empty)
-    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
-    u32x16 ld, plane, goff;
+    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 16;  // [tile][ngroups + 2][16]
+    const uint32_t* goffs = a.goff;  // [ngroups + 3][16] slot byte offsets (0x80000000 = empty)
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    u32x16 T0 = 0, T1 = 0, T2 = 0, T3 = 0;  // entry 0 of each table stays zero
+    u32x16 ld, ra, rb, goff;
     uint32_t t0;
-    // prologue: group 0's inputs in flight, group 1's offsets and group 0's first record half requested
+    // prologue: group 0's inputs in flight, group 1's offsets and group 0's record requested
     asm volatile(
 #include "gen/m8_idx_asm_cs16_pro.inc"
-        : "={v[200:215]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(plane), [t0] "=&v"(t0)
+        : "={v[136:151]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(ra), [t0] "=&v"(t0)
         : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
         : "memory");
-    for (int g = 0; g < a.ngroups; ++g)
-        cs16_step(rec + size_t(g) * 32, goffs + size_t(g + 2) * 16, rsrc, col, ld, plane, goff, a0, a1, a2, a3, a4,
-                  a5, a6, a7);
+    rb = 0;
+    for (int g = 0; g < a.ngroups; g += 2) {  // ngroups is padded to even on the host
+        cs16_step<false>(rec + size_t(g) * 16, goffs + size_t(g + 2) * 16, rsrc, col, ld, ra, rb, goff, T0, T1, T2,
+                         T3, a0, a1, a2, a3);
+        cs16_step<true>(rec + size_t(g + 1) * 16, goffs + size_t(g + 3) * 16, rsrc, col, ld, ra, rb, goff, T0, T1,
+                        T2, T3, a0, a1, a2, a3);
+    }
     // the last step's prefetches (padding group / records) must land before these registers are reused
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+{v[200:215]}"(ld), "+{s[40:55]}"(plane), "+{s[76:91]}"(goff)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : "+{v[136:151]}"(ld), "+{s[40:55]}"(ra), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff)
                  :
                  : "memory");
     uint8_t* out = a.dst + local * a.dst_stripe + col;
@@ -741,10 +756,6 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     cs16_finish(a, a1, 1, tile, out);
     cs16_finish(a, a2, 2, tile, out);
     cs16_finish(a, a3, 3, tile, out);
-    cs16_finish(a, a4, 4, tile, out);
-    cs16_finish(a, a5, 5, tile, out);
-    cs16_finish(a, a6, 6, tile, out);
-    cs16_finish(a, a7, 7, tile, out);
 }
 
 // slot lists -> byte offsets for k_cs16 (slot * sym; -1 -> 0x80000000, out of the V#'s range)

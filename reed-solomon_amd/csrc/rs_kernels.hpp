@@ -97,23 +97,23 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
 
 // m = 16 cyclotomic syndromes (k_cs16, the reference's fft_transform_cycl structure, src/rs/fft.c:39-100):
 // S_j = sum_i X_i^j in_i for the needed j, inputs grouped by cyclotomic coset (16 slots at positions
-// L * 2^a), syndromes by coset s (16 normal-basis accumulators each, 8 cosets per wave = one tile).
+// L * 2^a), syndromes by coset s (16 normal-basis accumulators each, 4 cosets per wave = one tile).
 struct Cs16Args {
     const uint8_t* src;       // stripe 0 of the input layout
     int64_t src_stripe, src_sym;
-    const uint32_t* goff;     // [ngroups + 2][16] byte offset (slot * src_sym) of the input at position
+    const uint32_t* goff;     // [ngroups + 3][16] byte offset (slot * src_sym) of the input at position
                               // L_g * 2^a; 0x80000000 = no input there (loads out of range: zero)
     uint32_t in_bytes;        // inputs' byte range past the stripe base (< 2^31; the V#'s num_records)
-    const uint32_t* rec;      // [ntiles][ngroups + 1][32] packed gpr-index records (gen_asm.py cs16)
+    const uint32_t* rec;      // [ntiles][ngroups + 2][16] packed gpr-index records (gen_asm.py cs16a/b)
     const int32_t* fin;       // [ntiles][fin_stride] needed syndromes: local coset | b << 4 | j << 8
-    const int32_t* fin_off;   // [ntiles][9] entries of local coset c: [fin_off[c], fin_off[c + 1])
+    const int32_t* fin_off;   // [ntiles][5] entries of local coset c: [fin_off[c], fin_off[c + 1])
     int32_t fin_stride;
     uint8_t* dst;             // syndrome j of launch-local stripe s at dst + s * dst_stripe + j * dst_sym
     int64_t dst_stripe, dst_sym;
     const uint16_t* logt;     // [65536] discrete log
     const uint16_t* expt;     // [65536] alpha^e, e < 65535
     uint32_t nblog[16];       // log of the GF(2^16) normal basis elements nb_t
-    int32_t ngroups, ntiles;
+    int32_t ngroups, ntiles;  // ngroups even (padded with empty groups)
     int64_t nchunks;          // 1 KiB column chunks per symbol
     int64_t units;            // n_stripes * nchunks
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)

@@ -140,8 +140,8 @@ def coding_matrix(k, r, is_erased=None):
 
 def route_dump(k, r, is_erased=None):
     """The GF(2^16) syndrome route of the encode / decode matrix (host only): dict with D, groups
-    [ngroups][16], rec [ntiles][ngroups + 1][8][16] (bytes), fin [ntiles][fin_stride], fin_off
-    [ntiles][9], m2 [R][D]."""
+    [ngroups][16] (ngroups even), rec [ntiles][ngroups + 2][4][16] (bytes), fin [ntiles][fin_stride],
+    fin_off [ntiles][5], m2 [R][D]."""
     er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
     t = 0 if er is None else int(er.sum())
     info = np.zeros(5, np.int32)
@@ -150,9 +150,9 @@ def route_dump(k, r, is_erased=None):
         raise RSError(rc, "rsg_route_dump")
     D, ng, nt, fs, R = (int(v) for v in info)
     groups = np.zeros((ng, 16), np.int32)
-    rec = np.zeros((nt, ng + 1, 8, 16), np.uint8)
+    rec = np.zeros((nt, ng + 2, 4, 16), np.uint8)
     fin = np.zeros((nt, fs), np.int32)
-    fin_off = np.zeros((nt, 9), np.int32)
+    fin_off = np.zeros((nt, 5), np.int32)
     m2 = np.zeros((R, D), np.uint16)
     rc = _lib.rsg_route_dump(k, r, _np_ptr(er), t, None, _np_ptr(groups), _np_ptr(rec), _np_ptr(fin), _np_ptr(fin_off),
                              _np_ptr(m2))

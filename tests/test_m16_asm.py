@@ -8,6 +8,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from xj_emu import Memory, Wave
 
@@ -110,62 +111,64 @@ def test_m8_v1_step_matches_gf256_multiply(tmp_path):
 
 
 def cs16_record(z):
-    """Byte t' of coset c = e(t'), bit d of e(t') = bit (t' - d) mod 16 of z_c (gen_asm.py cs16)."""
-    rec = np.zeros((8, 16), np.uint8)
-    for c in range(8):
+    """Byte t' of coset c = e(t'), bit d of e(t') = bit (t' - d) mod 16 of z_c (gen_asm.py cs16a/b)."""
+    rec = np.zeros((len(z), 16), np.uint8)
+    for c in range(len(z)):
         for tp in range(16):
             rec[c, tp] = sum(((int(z[c]) >> ((tp - d) % 16)) & 1) << d for d in range(4))
     return rec.reshape(-1)
 
 
-def test_cs16_step_circulant_xor(tmp_path):
-    """k_cs16's group step (gen_asm.py variant cs16): for each of the wave's 8 syndrome cosets and each
-    accumulator t, acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) from the current inputs in v[200:215],
-    both words of every lane; meanwhile the next group's inputs load into v[200:215] at lane + slot
-    offset (an offset of 0x80000000 is out of the V#'s range: zero) and the record / offset buffers for
-    the following step are requested."""
+@pytest.mark.parametrize("variant", ["cs16a", "cs16b"])
+def test_cs16_step_circulant_xor(tmp_path, variant):
+    """k_cs16's group step (gen_asm.py variants cs16a / cs16b): for each of the wave's 4 syndrome cosets
+    and each accumulator t, acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) from the current inputs in
+    v[136:151], both words of every lane; meanwhile the next group's inputs load into v[136:151] at lane
+    + slot offset (an offset of 0x80000000 is out of the V#'s range: zero), the next record loads into
+    the other record buffer and the slot offsets of the group after next into s[76:91]."""
     out = os.path.join(str(tmp_path), "cs16.inc")
-    subprocess.check_call([sys.executable, GEN, out, "cs16"])
+    subprocess.check_call([sys.executable, GEN, out, variant])
     lines = [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(out) if ln.startswith('"')]
+    cur, nxt = (40, 56) if variant == "cs16a" else (56, 40)
     rng = np.random.default_rng(1616)
     for trial in range(3):
-        z = rng.integers(0, 65536, 8)
+        z = rng.integers(0, 65536, 4)
         z[:3] = [0, 0xFFFF, 1]
         mem = Memory(1 << 16)
-        mem.b[1024:1152] = cs16_record(z)
-        mem.b[1152:1280] = cs16_record(rng.integers(0, 65536, 8))  # the next group's record
+        mem.b[1024:1088] = cs16_record(z)
+        mem.b[1088:1152] = cs16_record(rng.integers(0, 65536, 4))  # the next group's record
         data = rng.integers(0, 256, 16384, dtype=np.uint8)
         mem.b[32768:32768 + 16384] = data  # stripe inputs: 16 symbols of 1 KiB at the V# base
         offs = np.array([1024 * ((a * 7) % 16) for a in range(16)], np.uint32)
         offs[3] = 0x80000000  # an empty slot
-        mem.b[4096:4160] = offs.astype("<u4").view(np.uint8)  # next group's offsets (already in s[76:91])
         mem.b[4160:4224] = rng.integers(0, 2 ** 31, 16).astype("<u4").view(np.uint8)  # the group after next
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
         f[5] = 0  # an empty slot of the current group
-        acc0 = rng.integers(0, 2 ** 32, (128, 64), dtype=np.uint64).astype(np.uint32)
+        acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
         text = "\n".join(lines)
         text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[92:93]").replace("%[rsrc]", "s[96:99]")
                 .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
         w = Wave(mem, {})
-        w.v[200:216] = f
-        w.v[72:200] = acc0
+        w.v[136:152] = f
+        w.v[72:136] = acc0
         lane = (np.arange(64) * 4 + 256).astype(np.uint32)
         w.v[230] = lane
         w.s[100], w.s[101] = 1024, 0
         w.s[92], w.s[93] = 4160, 0
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
         w.s[76:92] = offs.astype(np.uint64)
-        w.run(["s_load_dwordx16 s[40:55], s[100:101], 0x0"] + text.splitlines(), [])
-        for c in range(8):
+        w.run([f"s_load_dwordx16 s[{cur}:{cur + 15}], s[100:101], 0x0"] + text.splitlines(), [])
+        for c in range(4):
             for t in range(16):
                 want = acc0[16 * c + t].copy()
                 for a in range(16):
                     if (int(z[c]) >> ((t - a) % 16)) & 1:
                         want ^= f[a]
                 assert np.array_equal(w.v[72 + 16 * c + t], want), (trial, c, t)
+        assert not w.v[8:72:16].any()  # table entry 0 stays zero
         words = data.view("<u4")
         for a in range(16):
             want = np.zeros(64, np.uint32) if offs[a] == 0x80000000 else words[(offs[a] + lane) // 4]
-            assert np.array_equal(w.v[200 + a], want), (trial, a)
+            assert np.array_equal(w.v[136 + a], want), (trial, a)
         assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
-        assert list(w.s[40:56]) == list(mem.load32(np.uint64(1152) + 4 * np.arange(16, dtype=np.uint64)))
+        assert list(w.s[nxt:nxt + 16]) == list(mem.load32(np.uint64(1088) + 4 * np.arange(16, dtype=np.uint64)))

@@ -58,7 +58,7 @@ def _model_syndromes(d, X, nb):
     nt, W = rec.shape[0], X.shape[1]
     S = np.zeros((d["D"], W), np.int64)
     for tile in range(nt):
-        acc = np.zeros((8, 16, W), np.int64)
+        acc = np.zeros((4, 16, W), np.int64)
         for g in range(groups.shape[0]):
             f = np.array([X[s] if s >= 0 else np.zeros(W, np.int64) for s in groups[g]])
             for q in range(4):
@@ -67,10 +67,10 @@ def _model_syndromes(d, X, nb):
                     for dd in range(4):
                         if e >> dd & 1:
                             tab[e] ^= f[4 * q + dd]
-                idx = rec[tile, g]  # [8][16]: e(t') per local coset
+                idx = rec[tile, g]  # [4][16]: e(t') per local coset
                 for tp in range(16):
                     acc[:, (tp + 4 * q) % 16] ^= tab[idx[:, tp]]
-        for c in range(8):
+        for c in range(4):
             for e in range(fin_off[tile, c], fin_off[tile, c + 1]):
                 ent = int(fin[tile, e])
                 assert ent & 15 == c
