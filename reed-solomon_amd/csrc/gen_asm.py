@@ -227,6 +227,60 @@ if variant == "cs16_pro":
     emit(out)
     sys.exit(0)
 
+if variant == "bs16":
+    # m = 16 binary accumulation with per-accumulator indices (k_bs16): the GF(2^16) syndrome route's
+    # encode second stage. Output coset c (16 accumulators u_t, normal-basis coordinates) accumulates
+    #     u_t ^= sum_j bit_t(z_(c, j)) * S_j,   z = normal repr of the coefficient of S_j
+    # over the step's 16 inputs (four subset tables T_q over inputs 4q .. 4q + 3 as in cs16); the
+    # coefficients have no circulant structure here, so each (coset, table, t) has its own index: 64
+    # gpr-index switches per coset. Registers as cs16a (tables, 4 cosets' accumulators, L ring,
+    # s[76:91] slot offsets); the record of (tile, group) is 4 cosets x 64 byte indices (byte 16q + t
+    # of coset c = index of (q, t)), read one coset at a time into s[40:55] / s[56:71] alternately
+    # (coset c in buffer c % 2; the next step's coset 0 is requested while coset 3 runs).
+    T, ACC, LD = 8, 72, 136
+    e("s_waitcnt vmcnt(0)")
+    for q in range(4):
+        b = T + 16 * q
+        for d, slot in enumerate((1, 2, 4, 8)):
+            e(f"v_mov_b32 v{b + slot}, v{LD + 4 * q + d}")
+    e("s_waitcnt lgkmcnt(0)")  # coset 0's record and the next group's slot offsets
+    for a in range(16):
+        t = "%[t0]" if a % 2 == 0 else "%[t1]"
+        e(f"v_add_u32 {t}, s{76 + a}, %[lane]")
+        e(f"buffer_load_dword v{LD + a}, {t}, %[rsrc], 0 offen")
+    e("s_load_dwordx16 s[56:71], %[cp], 0x40")  # coset 1's record
+    e("s_load_dwordx16 s[76:91], %[gp], 0x0")
+    for row in [(3, 1, 2), (5, 4, 1), (6, 4, 2), (7, 4, 3)] + [(8 + k, 8, k) for k in range(1, 8)]:
+        for q in range(4):
+            b = T + 16 * q
+            e(f"v_xor_b32 v{b + row[0]}, v{b + row[1]}, v{b + row[2]}")
+    first = True
+    for c in range(4):
+        buf = 40 if c % 2 == 0 else 56
+        if c:
+            if first is False:
+                e("s_set_gpr_idx_off")  # s_load / s_waitcnt outside gpr-index mode
+                first = True
+            e("s_waitcnt lgkmcnt(0)")
+            nxt = 56 if c % 2 == 0 else 40
+            e(f"s_load_dwordx16 s[{nxt}:{nxt + 15}], %[cp], {hex(64 * (c + 1))}")  # coset c + 1 / next step's 0
+        for pair in range(8):  # dwords (2 pair, 2 pair + 1): bytes 8 pair + (0..3, 4..7)
+            lo = buf + 2 * pair
+            for byte in range(4):
+                if byte:
+                    e(f"s_lshr_b64 s[72:73], s[{lo}:{lo + 1}], {8 * byte}")
+                for h in range(2):
+                    bi = 8 * pair + 4 * h + byte
+                    q, t = divmod(bi, 16)
+                    sreg = f"s{lo + h}" if byte == 0 else f"s{72 + h}"
+                    e(f"s_set_gpr_idx_on {sreg}, gpr_idx(SRC0)" if first else f"s_set_gpr_idx_idx {sreg}")
+                    first = False
+                    acc = ACC + 16 * c + t
+                    e(f"v_xor_b32 v{acc}, v{T + 16 * q}, v{acc}")
+    e("s_set_gpr_idx_off")
+    emit(out)
+    sys.exit(0)
+
 if variant in ("cs16a", "cs16b"):
     # m = 16 cyclotomic syndromes (k_cs16), one dword (two GF(2^16) words) per lane per group step.
     # A group is 16 inputs f_a at positions L * 2^a (a cyclotomic coset, empty slots zero); a syndrome

@@ -149,6 +149,7 @@ struct DevPlan {
     // plain matrix plan, built on demand for launches the route does not cover (stripe-id lists,
     // symbol sizes that are not a multiple of 1 KiB).
     struct Cs {
+        int kind = 0;  // 0: k_cs16 syndromes into scratch, then `second`; 1: k_bs16 straight into the outputs
         int D = 0, ngroups = 0, ntiles = 0, fin_stride = 0;
         int64_t max_slot = 0;       // largest input slot (the loads' byte range)
         int32_t* groups = nullptr;  // [ngroups + 2][16] input slots, -1 = none
@@ -417,8 +418,8 @@ struct rsg_codec {
     int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
     void* d_cs = nullptr;  // syndrome route scratch: [chunk][D][S]
     size_t cs_cap = 0;
-    void* d_goff = nullptr;  // syndrome route: the plan's input slots as byte offsets of this launch
-    size_t goff_cap = 0;
+    void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
+    size_t goff_cap[2] = {0, 0};
     int jit = 2;  // 0 off, 1 every eligible plan, 2 encode plans + decode plans from their 2nd use
     int dec_jit_uses = 2;  // jit = 2: decode plans are specialised from this many launches on
     int xj = 1;   // specialised kernel family: 1 bit-plane XOR kernels (rs_xj), 0 nibble-table rs_v1jit
@@ -470,7 +471,7 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_goff})
+                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_goff[0], d_goff[1]})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -639,15 +640,21 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
     return h;
 }
 
+static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<int32_t>& in_slots, hipStream_t st);
+
 static int build_cs16(DevPlan& p, const std::vector<uint16_t>& pos, const std::vector<int32_t>& in_slots, int D,
                       hipStream_t st) {
-    const CsHost h = cs16_host(pos, in_slots, D);
+    return upload_cs(p, cs16_host(pos, in_slots, D), 0, in_slots, st);
+}
+
+static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<int32_t>& in_slots, hipStream_t st) {
     PlanBlob blob;  // groups, records and finish lists in the plan's one allocation
     const size_t o_g = blob.add(h.groups.data(), h.groups.size() * 4), o_r = blob.add(h.rec.data(), h.rec.size());
     const size_t o_f = blob.add(h.fin.data(), h.fin.size() * 4), o_fo = blob.add(h.fin_off.data(), h.fin_off.size() * 4);
     if (int rc = blob.upload(p, st)) return rc;
     if (int rc = PlanBlob::finish(p)) return rc;
     auto cs = std::make_unique<DevPlan::Cs>();
+    cs->kind = kind;
     cs->D = h.D;
     cs->ngroups = h.ngroups;
     cs->ntiles = h.ntiles;
@@ -660,6 +667,82 @@ static int build_cs16(DevPlan& p, const std::vector<uint16_t>& pos, const std::v
     for (int t = 0; t < 16; ++t) cs->nblog[t] = field().log[normal_basis_element(16, t)];
     p.cs = std::move(cs);
     return 0;
+}
+
+// The encode second stage on k_bs16: E = the repair positions (whole cosets) makes Lambda binary, so
+// the rows of M2 along an output coset are Frobenius conjugates, M2[L 2^b][j] = M2[L][j]^(2^b): output
+// coset c accumulates u_t = sum_j bit_t(z_(c, j)) S_j with z = normal repr of M2[L][j], and the finish
+// S_(L 2^b) = sum_t nb_((t + b) mod 16) u_t gives all its outputs (as k_cs16's). Returns false when the
+// rows do not have that structure (then the plain matrix plan applies M2).
+static bool bs16_host(const std::vector<uint16_t>& M2, int D, const std::vector<uint16_t>& targets,
+                      const std::vector<int>& emit, const std::vector<int32_t>& out_slots, CsHost& h) {
+    const Field& F = field();
+    const int R = int(emit.size());
+    // output cosets: runs of rows whose positions double
+    std::vector<std::pair<int, int>> cos;  // (first row, size)
+    for (int r = 0; r < R;) {
+        int e = r + 1;
+        while (e < R && e - r < 16 &&
+               targets[size_t(emit[size_t(e)])] == uint16_t((uint32_t(targets[size_t(emit[size_t(e - 1)])]) << 1) % kN))
+            ++e;
+        cos.emplace_back(r, e - r);
+        r = e;
+    }
+    for (auto& c : cos)  // M2[r0 + b][j] = M2[r0 + b - 1][j]^2
+        for (int b = 1; b < c.second; ++b)
+            for (int j = 0; j < D; ++j) {
+                const uint16_t x = M2[size_t(c.first + b - 1) * D + j];
+                if (M2[size_t(c.first + b) * D + j] != (x ? F.exp[(2u * F.log[x]) % kN] : 0)) return false;
+            }
+    constexpr int CW = 4;
+    const int ngr = (D + 15) / 16, ng = ngr + (ngr & 1), C = int(cos.size()), ntiles = (C + CW - 1) / CW;
+    h = CsHost();
+    h.D = D;
+    h.ngroups = ng;
+    h.ntiles = ntiles;
+    h.groups.assign(size_t(ng + 3) * 16, -1);
+    for (int j = 0; j < D; ++j) h.groups[size_t(j)] = j;  // group g = syndromes 16 g .. 16 g + 15
+    const std::vector<uint16_t>& rep = normal_repr_tables()[4];
+    std::vector<uint16_t> z(static_cast<size_t>(D));
+    h.rec.assign(size_t(ntiles) * size_t(ng + 2) * CW * 64, 0);
+    int fin_stride = 1;
+    for (int t = 0; t < ntiles; ++t) {
+        int cnt = 0;
+        for (int c = CW * t; c < std::min(C, CW * t + CW); ++c) cnt += cos[size_t(c)].second;
+        fin_stride = std::max(fin_stride, cnt);
+    }
+    h.fin_stride = fin_stride;
+    h.fin.assign(size_t(ntiles) * size_t(fin_stride), 0);
+    h.fin_off.assign(size_t(ntiles) * (CW + 1), 0);
+    for (int t = 0; t < ntiles; ++t) {
+        int e = 0;
+        for (int cl = 0; cl < CW; ++cl) {
+            const int c = CW * t + cl;
+            h.fin_off[size_t(t) * (CW + 1) + size_t(cl)] = e;
+            if (c >= C) continue;
+            const int r0 = cos[size_t(c)].first;
+            for (int b = 0; b < cos[size_t(c)].second; ++b)
+                h.fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (b << 4) | (out_slots[size_t(r0 + b)] << 8);
+            for (int j = 0; j < D; ++j) {
+                const uint16_t v = M2[size_t(r0) * D + j];
+                z[size_t(j)] = v ? rep[F.log[v]] : 0;
+            }
+            for (int g = 0; g < ngr; ++g) {
+                uint8_t* r = h.rec.data() + ((size_t(t) * size_t(ng + 2) + size_t(g)) * CW + size_t(cl)) * 64;
+                for (int q = 0; q < 4; ++q)
+                    for (int tb = 0; tb < 16; ++tb) {  // byte 16 q + t: bit d = bit t of z of input 16 g + 4 q + d
+                        uint8_t v = 0;
+                        for (int d = 0; d < 4; ++d) {
+                            const int j = 16 * g + 4 * q + d;
+                            if (j < D) v = uint8_t(v | (((z[size_t(j)] >> tb) & 1u) << d));
+                        }
+                        r[16 * q + tb] = v;
+                    }
+            }
+        }
+        h.fin_off[size_t(t) * (CW + 1) + CW] = e;
+    }
+    return true;
 }
 
 // the syndrome route pays when both sides of the matrix are large
@@ -687,10 +770,21 @@ static int make_plan_cs(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevP
     if (int rc = build_cs16(*p, c->positions, in, D, st)) return rc;
     std::vector<int32_t> sin(static_cast<size_t>(D));
     for (int j = 0; j < D; ++j) sin[size_t(j)] = j;
+    std::vector<uint16_t> M2 = syndrome_solve_matrix(targets, emit);
     std::unique_ptr<DevPlan> second;
-    if (int rc = build_plan(c->device, 16, syndrome_solve_matrix(targets, emit), D, R, std::move(sin), std::move(outs),
-                            second, st))
+    CsHost bh;
+    if (!erased && bs16_host(M2, D, targets, emit, outs, bh)) {  // encode: Frobenius rows, k_bs16
+        second = std::make_unique<DevPlan>();
+        second->device = c->device;
+        second->m = 16;
+        second->K = D;
+        second->R = R;
+        second->in_slots = sin;
+        second->out_slots = outs;
+        if (int rc = upload_cs(*second, bh, 1, sin, st)) return rc;
+    } else if (int rc = build_plan(c->device, 16, std::move(M2), D, R, std::move(sin), std::move(outs), second, st)) {
         return rc;
+    }
     p->second = std::move(second);
     out = std::move(p);
     return 0;
@@ -854,38 +948,48 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     if ((uintptr_t(src) | uintptr_t(dst) | uint64_t(src_stripe) | uint64_t(src_sym) | uint64_t(dst_stripe) |
          uint64_t(dst_sym)) % 4)
         return RS_ERR_INVALID;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
+    const int ngo = (cs.ngroups + 3) * 16;
+    if (int rc = grow(&c->d_goff[cs.kind], c->goff_cap[cs.kind], size_t(ngo) * 4)) return rc;
+    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
+    Cs16Args a{};
+    a.src_stripe = src_stripe;
+    a.src_sym = src_sym;
+    a.goff = static_cast<const uint32_t*>(c->d_goff[cs.kind]);
+    a.in_bytes = uint32_t(cs.max_slot * src_sym + int64_t(S));
+    a.rec = cs.rec;
+    a.fin = cs.fin;
+    a.fin_off = cs.fin_off;
+    a.fin_stride = cs.fin_stride;
+    a.dst_sym = int64_t(S);
+    a.logt = logt;
+    a.expt = expt;
+    for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
+    a.ngroups = cs.ngroups;
+    a.ntiles = cs.ntiles;
+    a.nchunks = int64_t(S) / 1024;
+    if (cs.kind == 1) {  // straight into the outputs
+        a.src = src;
+        a.dst = dst;
+        a.dst_stripe = dst_stripe;
+        a.dst_sym = dst_sym;
+        a.units = int64_t(n_stripes) * a.nchunks;
+        HIP_TRY(launch_bs16(a, st));
+        c->last_kernel = "bs16";
+        return 0;
+    }
     const int64_t per = int64_t(cs.D) * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
     if (int rc = scratch_acquire(c, st)) return rc;
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
-    const int ngo = (cs.ngroups + 3) * 16;
-    if (int rc = grow(&c->d_goff, c->goff_cap, size_t(ngo) * 4)) return rc;
-    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff), ngo, src_sym, st));
-    const uint16_t *logt = nullptr, *expt = nullptr;
-    const uint8_t* g8 = nullptr;
-    if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
     std::string second;
     for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
         const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
-        Cs16Args a{};
         a.src = src + c0 * src_stripe;
-        a.src_stripe = src_stripe;
-        a.src_sym = src_sym;
-        a.goff = static_cast<const uint32_t*>(c->d_goff);
-        a.in_bytes = uint32_t(cs.max_slot * src_sym + int64_t(S));
-        a.rec = cs.rec;
-        a.fin = cs.fin;
-        a.fin_off = cs.fin_off;
-        a.fin_stride = cs.fin_stride;
         a.dst = static_cast<uint8_t*>(c->d_cs);
         a.dst_stripe = per;
-        a.dst_sym = int64_t(S);
-        a.logt = logt;
-        a.expt = expt;
-        for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
-        a.ngroups = cs.ngroups;
-        a.ntiles = cs.ntiles;
-        a.nchunks = int64_t(S) / 1024;
         a.units = cn * a.nchunks;
         HIP_TRY(launch_cs16(a, st));
         if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,
@@ -904,8 +1008,11 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
     if (int rc = p.order_after_build(st)) return rc;
     if (p.cs) {
         HIP_TRY(hipSetDevice(c->device));
-        if (!d_ids && !dst_local && S % 1024 == 0 && p.cs->max_slot * src_sym + int64_t(S) < (int64_t(1) << 31))
+        // both stages index their inputs with 31-bit byte offsets (the second stage reads D syndrome rows)
+        if (!d_ids && !dst_local && S % 1024 == 0 && p.cs->max_slot * src_sym + int64_t(S) < (int64_t(1) << 31) &&
+            int64_t(p.cs->D) * int64_t(S) < (int64_t(1) << 31))
             return run_cs(c, p, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st);
+        if (p.cs->kind == 1) return RS_ERR_INVALID;  // a second stage runs only inside its route (run_cs)
         if (!p.dense) {  // launches the route does not cover run the plain matrix plan
             std::unique_ptr<bool[]> er;
             if (!p.erased.empty()) {

@@ -758,6 +758,67 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     cs16_finish(a, a3, 3, tile, out);
 }
 
+// m = 16 binary accumulation (k_bs16, gen_asm.py bs16): the syndrome route's encode second stage. Same
+// block / tile / input scheme as k_cs16 (the inputs are the D syndromes of a stripe, 16 per group), but
+// every (coset, table, accumulator) has its own gpr-index switch: the coefficients S_j -> output coset
+// are Frobenius-structured along the coset (finish as k_cs16), not along the inputs.
+__device__ __forceinline__ void bs16_step(const uint32_t* cp, const uint32_t* gp, u32x4s rsrc, uint32_t lane,
+                                          u32x16& ld, u32x16& ra, u32x16& rb, u32x16& goff, u32x16& T0, u32x16& T1,
+                                          u32x16& T2, u32x16& T3, u32x16& a0, u32x16& a1, u32x16& a2, u32x16& a3) {
+    uint32_t t0, t1;
+    asm volatile(
+#include "gen/m8_idx_asm_bs16.inc"
+        : "+{v[72:87]}"(a0), "+{v[88:103]}"(a1), "+{v[104:119]}"(a2), "+{v[120:135]}"(a3), "+{v[8:23]}"(T0),
+          "+{v[24:39]}"(T1), "+{v[40:55]}"(T2), "+{v[56:71]}"(T3), "+{v[136:151]}"(ld), "+{s[40:55]}"(ra),
+          "+{s[56:71]}"(rb), "+{s[76:91]}"(goff), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [cp] "s"(cp), [gp] "s"(gp), [rsrc] "s"(rsrc), [lane] "v"(lane)
+        : "s72", "s73", "memory");
+}
+
+__global__ void __launch_bounds__(256) k_bs16(Cs16Args a) {
+    const int64_t slot = blockIdx.x >> 3;
+    const int tile = int(slot % a.ntiles);
+    const int64_t unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
+    if (unit >= a.units) return;
+    const int64_t local = unit / a.nchunks;
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const uint32_t col = uint32_t((unit - local * a.nchunks) * 1024) + threadIdx.x * 4u;
+    const uint64_t base = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
+    const u32x4s rsrc = {uint32_t(base), uint32_t(base >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
+    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 64;  // [tile][ngroups + 2][4][16]
+    const uint32_t* goffs = a.goff;
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    u32x16 T0 = 0, T1 = 0, T2 = 0, T3 = 0;
+    u32x16 ld, ra, rb, goff;
+    uint32_t t0;
+    asm volatile(
+#include "gen/m8_idx_asm_cs16_pro.inc"
+        : "={v[136:151]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(ra), [t0] "=&v"(t0)
+        : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
+        : "memory");
+    rb = 0;
+    for (int g = 0; g < a.ngroups; ++g)
+        bs16_step(rec + size_t(g) * 64, goffs + size_t(g + 2) * 16, rsrc, col, ld, ra, rb, goff, T0, T1, T2, T3, a0, a1,
+                  a2, a3);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+                 : "+{v[136:151]}"(ld), "+{s[40:55]}"(ra), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff)
+                 :
+                 : "memory");
+    uint8_t* out = a.dst + stripe * a.dst_stripe + col;  // outputs go to the caller's stripes
+    cs16_finish(a, a0, 0, tile, out);
+    cs16_finish(a, a1, 1, tile, out);
+    cs16_finish(a, a2, 2, tile, out);
+    cs16_finish(a, a3, 3, tile, out);
+}
+
+hipError_t launch_bs16(const Cs16Args& a, hipStream_t st) {
+    if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
+    const int64_t blocks = (a.units + 7) / 8 * 8 * a.ntiles;
+    if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 // slot lists -> byte offsets for k_cs16 (slot * sym; -1 -> 0x80000000, out of the V#'s range)
 __global__ void k_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym) {
     const int i = blockIdx.x * 256 + threadIdx.x;

@@ -119,6 +119,9 @@ struct Cs16Args {
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);
+// binary accumulation with per-accumulator indices (k_bs16): records [ntiles][ngroups + 2][4][64] bytes,
+// finish entries' j = output slot, written at dst + stripe * dst_stripe + j * dst_sym
+hipError_t launch_bs16(const Cs16Args& a, hipStream_t st);
 // goff[i] = slots[i] * sym (0x80000000 for slots[i] < 0), i < n
 hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym, hipStream_t st);
 

@@ -542,7 +542,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     codec.encode(dev)
     torch.cuda.synchronize()
     routed = route == 1 and k >= 64 and r >= 64 and S % 1024 == 0
-    assert codec.last_kernel == ("cs16+apply_m16_v1" if routed else "apply_m16_v1"), codec.last_kernel
+    assert codec.last_kernel == ("cs16+bs16" if routed else "apply_m16_v1"), codec.last_kernel
     got = dev.cpu().numpy()
     want = host.copy()
     for s in range(n):

@@ -172,3 +172,51 @@ def test_cs16_step_circulant_xor(tmp_path, variant):
             assert np.array_equal(w.v[136 + a], want), (trial, a)
         assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
         assert list(w.s[nxt:nxt + 16]) == list(mem.load32(np.uint64(1088) + 4 * np.arange(16, dtype=np.uint64)))
+
+
+def test_bs16_step_binary_accumulation(tmp_path):
+    """k_bs16's group step (gen_asm.py bs16): for each of the wave's 4 output cosets and accumulator t,
+    acc_t ^= XOR_j bit_t(z_(c, j)) * f_j over the step's 16 inputs (one gpr-index switch per (coset,
+    table, t)); the coset records load one at a time, the next step's first one last."""
+    out = os.path.join(str(tmp_path), "bs16.inc")
+    subprocess.check_call([sys.executable, GEN, out, "bs16"])
+    lines = [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(out) if ln.startswith('"')]
+    rng = np.random.default_rng(1717)
+    z = rng.integers(0, 65536, (4, 16))
+    z[0, :] = 0
+    z[1, 3] = 0xFFFF
+    rec = np.zeros((4, 64), np.uint8)
+    for c in range(4):
+        for q in range(4):
+            for t in range(16):
+                rec[c, 16 * q + t] = sum(((int(z[c, 4 * q + d]) >> t) & 1) << d for d in range(4))
+    mem = Memory(1 << 16)
+    mem.b[1024:1280] = rec.reshape(-1)
+    nxt = rng.integers(0, 256, 64, dtype=np.uint8)
+    mem.b[1280:1344] = nxt  # the next step's coset-0 record
+    mem.b[4160:4224] = rng.integers(0, 2 ** 31, 16).astype("<u4").view(np.uint8)
+    data = rng.integers(0, 256, 16384, dtype=np.uint8)
+    mem.b[32768:32768 + 16384] = data
+    offs = np.array([1024 * a for a in range(16)], np.uint32)
+    f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
+    acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
+    text = "\n".join(lines)
+    text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[92:93]").replace("%[rsrc]", "s[96:99]")
+            .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
+    w = Wave(mem, {})
+    w.v[136:152] = f
+    w.v[72:136] = acc0
+    w.v[230] = (np.arange(64) * 4).astype(np.uint32)
+    w.s[100], w.s[101] = 1024, 0
+    w.s[92], w.s[93] = 4160, 0
+    w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
+    w.s[76:92] = offs.astype(np.uint64)
+    w.run(["s_load_dwordx16 s[40:55], s[100:101], 0x0"] + text.splitlines(), [])
+    for c in range(4):
+        for t in range(16):
+            want = acc0[16 * c + t].copy()
+            for j in range(16):
+                if (int(z[c, j]) >> t) & 1:
+                    want ^= f[j]
+            assert np.array_equal(w.v[72 + 16 * c + t], want), (c, t)
+    assert list(w.s[40:56]) == list(nxt.view("<u4"))
