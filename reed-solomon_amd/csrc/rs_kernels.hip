@@ -684,35 +684,55 @@ __device__ __forceinline__ void cs16_step(const uint32_t* cp, const uint32_t* gp
 }
 #undef RS_CS16_OPERANDS
 
-// needed syndromes of local coset c from its 16 accumulators u (both words of the lane's dword)
+// S = sum_t nb_((t + B) mod 16) * u_t on both packed words, without tables: nb_k = sum_q bit_q(nb_k) alpha^q,
+// so S = sum_q alpha^q w_q with w_q = XOR of the u_t whose nb_((t + B) mod 16) has bit q (a fixed XOR
+// network for each B), then Horner in alpha over q (x * alpha on packed words: shift, carry * 0x2D).
+// nb = the GF(2^16) normal basis of reference gf65536.c:21-57 (facts).
+__device__ constexpr uint16_t kNb16[16] = {2048, 2880, 7129, 30616, 2643, 6897, 29685, 7378,
+                                           30100, 2743, 20193, 36223, 24055, 41458, 41014, 61451};
+
+template <int B>
+__device__ __forceinline__ uint32_t nb_combine(const u32x16& u) {
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        w[q] = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            if ((kNb16[(t + B) & 15] >> q) & 1) w[q] ^= u[t];
+    }
+    uint32_t s = w[15];
+#pragma unroll
+    for (int q = 14; q >= 0; --q) s = (((s << 1) & 0xFFFEFFFEu) ^ (((s >> 15) & 0x10001u) * 0x2Du)) ^ w[q];
+    return s;
+}
+
+// needed syndromes / outputs of local coset c from its 16 accumulators u (both words of the lane's dword)
 __device__ __forceinline__ void cs16_finish(const Cs16Args& a, const u32x16& u, int c, int tile, uint8_t* out) {
     const int e0 = sload(a.fin_off + tile * 5 + c), e1 = sload(a.fin_off + tile * 5 + c + 1);
-    if (e0 >= e1) return;
-    uint32_t lg[16];  // log of each word, 0xFFFF marks a zero word
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        const uint32_t lo = u[t] & 0xFFFFu, hi = u[t] >> 16;
-        lg[t] = (lo ? uint32_t(a.logt[lo]) : 0xFFFFu) | ((hi ? uint32_t(a.logt[hi]) : 0xFFFFu) << 16);
-    }
     for (int e = e0; e < e1; ++e) {
         const int32_t ent = sload(a.fin + int64_t(tile) * a.fin_stride + e);
-        const int b = (ent >> 4) & 15;
         const int64_t j = ent >> 8;
-        uint32_t slo = 0, shi = 0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t nl = a.nblog[(t + b) & 15];
-            const uint32_t l0 = lg[t] & 0xFFFFu, l1 = lg[t] >> 16;
-            if (l0 != 0xFFFFu) {
-                const uint32_t x = l0 + nl;
-                slo ^= a.expt[x >= 65535u ? x - 65535u : x];
-            }
-            if (l1 != 0xFFFFu) {
-                const uint32_t x = l1 + nl;
-                shi ^= a.expt[x >= 65535u ? x - 65535u : x];
-            }
+        uint32_t v = 0;
+        switch ((ent >> 4) & 15) {  // wave-uniform
+        case 0: v = nb_combine<0>(u); break;
+        case 1: v = nb_combine<1>(u); break;
+        case 2: v = nb_combine<2>(u); break;
+        case 3: v = nb_combine<3>(u); break;
+        case 4: v = nb_combine<4>(u); break;
+        case 5: v = nb_combine<5>(u); break;
+        case 6: v = nb_combine<6>(u); break;
+        case 7: v = nb_combine<7>(u); break;
+        case 8: v = nb_combine<8>(u); break;
+        case 9: v = nb_combine<9>(u); break;
+        case 10: v = nb_combine<10>(u); break;
+        case 11: v = nb_combine<11>(u); break;
+        case 12: v = nb_combine<12>(u); break;
+        case 13: v = nb_combine<13>(u); break;
+        case 14: v = nb_combine<14>(u); break;
+        default: v = nb_combine<15>(u); break;
         }
-        *reinterpret_cast<uint32_t*>(out + j * a.dst_sym) = slo | (shi << 16);
+        *reinterpret_cast<uint32_t*>(out + j * a.dst_sym) = v;
     }
 }
 
