@@ -237,6 +237,20 @@ def scatter_leg(args, rank, world, dev):
             "gather_ms": round(t_ga.max_elapsed * 1e3, 3), "check": "ok" if ok else "MISMATCH"}
 
 
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions / s: 256 CUs x 4 SIMD-32, 2 cycles each, 2.4 GHz
+
+
+def compute_roofline(work_enc, enc_ms, work_dec, dec_ms):
+    """Issue rate of the hand-scheduled GF(2^16) kernels (their generated steps' VALU + SALU counts,
+    rsg_last_work) against the chip's VALU issue peak. gpr-indexed VALU (the table lookups) issue at half
+    rate on gfx950 (profiles/r1_issue_bench.log), so frac ~0.5 is the practical ceiling of these kernels."""
+    v = work_enc[0] + work_dec[0]
+    sa = work_enc[1] + work_dec[1]
+    t = (enc_ms + dec_ms) / 1e3
+    return {"bound": "valu-issue", "valu_insts": v, "salu_insts": sa, "achieved": round(v / t / 1e12, 4),
+            "peak": round(VALU_PEAK / 1e12, 4), "unit": "T wave-VALU/s", "frac": round(v / t / VALU_PEAK, 4)}
+
+
 def per_rank_times(enc_ms, dec_ms, dev):
     """[{rank, encode_ms, decode_ms}] of every rank (all_gather; one entry without a process group)."""
     import torch
@@ -356,10 +370,10 @@ def main():
         for i in range(args.steps):
             ev[i][0].record(stream)
             codec.encode(stripes, stream=stream)
-            kern_enc = codec.last_kernel
+            kern_enc, work_enc = codec.last_kernel, codec.last_work
             ev[i][1].record(stream)
             codec.decode(stripes, erased, stream=stream)
-            kern_dec = codec.last_kernel
+            kern_dec, work_dec = codec.last_kernel, codec.last_work
             ev[i][2].record(stream)
     elapsed = region.max_elapsed
 
@@ -405,6 +419,8 @@ def main():
     line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes}
+    if codec.subfield == 16:  # compute roofline of the GF(2^16) kernels (issue bound, not HBM)
+        line["roofline"]["compute"] = compute_roofline(work_enc, enc_ms, work_dec, dec_ms)
     line["encode_ms"] = round(enc_ms, 3)
     line["decode_ms"] = round(dec_ms, 3)
     line["per_rank"] = per_rank

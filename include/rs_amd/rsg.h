@@ -56,6 +56,10 @@ int rsg_codec_subfield(const rsg_codec_t* c);
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);
+/* Wave-instructions (VALU, SALU) the hand-scheduled GF(2^16) kernels issued in the last rsg_encode /
+ * rsg_decode: their generated steps' instruction counts times the steps run (0 for the other kernels).
+ * bench.py divides them by the launch time for the compute roofline of m = 16 codes. */
+int rsg_last_work(const rsg_codec_t* c, uint64_t* valu, uint64_t* salu);
 
 /* Repair symbols of n_stripes stripes: info at d_info (k symbols per stripe), repair written to
  * d_rep (r symbols per stripe). */

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "gen/asm_counts.h"
 #include "gf16.hpp"
 #include "rs_jit.hpp"
 #include "rs_kernels.hpp"
@@ -416,6 +417,9 @@ struct rsg_codec {
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
     int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
+    // wave-instructions issued by the hand-scheduled GF(2^16) kernels of the last rsg_encode / rsg_decode
+    // (their generated steps' VALU / SALU counts times the steps run; rsg_last_work)
+    uint64_t work_valu = 0, work_salu = 0;
     void* d_cs = nullptr;  // syndrome route scratch: [chunk][D][S]
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
@@ -977,6 +981,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst_sym = dst_sym;
         a.units = int64_t(n_stripes) * a.nchunks;
         HIP_TRY(launch_bs16(a, st));
+        const uint64_t steps = uint64_t(a.units) * 4 * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        c->work_valu += steps * kValu_bs16;
+        c->work_salu += steps * kSalu_bs16;
         c->last_kernel = "bs16";
         return 0;
     }
@@ -992,6 +999,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst_stripe = per;
         a.units = cn * a.nchunks;
         HIP_TRY(launch_cs16(a, st));
+        const uint64_t steps = uint64_t(a.units) * 4 * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
+        c->work_salu += steps * kSalu_cs16a;
         if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,
                               dst_stripe, dst_sym, uint64_t(cn), S, st))
             return rc;
@@ -1125,7 +1135,19 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
                      : (rt == 64 && p.d_idx && a.mode < 2) ? std::string(a.mode ? "apply_m16_v1_plain" : "apply_m16_v1")
                                                              : (std::string("apply_m16_rt") + std::to_string(rt));
     HIP_TRY(launch_apply(p.m, rt, a, int64_t(n_stripes), st));
+    if (p.m == 16 && rt == 64 && p.d_idx && a.mode < 2) {  // k_apply_m16_v1 over the full 1 KiB chunks
+        const uint64_t steps = n_stripes * (S / 1024) * uint64_t((p.R + 63) / 64) * 4 * uint64_t(p.K);
+        c->work_valu += steps * kValu_m16_v1;
+        c->work_salu += steps * kSalu_m16_v1;
+    }
     if (a.scratch) return scratch_release(c, st);  // split-K partials in flight on st
+    return 0;
+}
+
+extern "C" int rsg_last_work(const rsg_codec_t* c, uint64_t* valu, uint64_t* salu) {
+    if (!c) return RS_ERR_INVALID;
+    if (valu) *valu = c->work_valu;
+    if (salu) *salu = c->work_salu;
     return 0;
 }
 
@@ -1133,6 +1155,7 @@ extern "C" int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stri
                           void* d_rep, uint64_t rep_stripe_stride, uint64_t rep_symbol_stride, uint64_t n_stripes,
                           uint64_t symbol_size, void* stream) {
     if (!c) return RS_ERR_INVALID;
+    c->work_valu = c->work_salu = 0;
     return run_plan(c, *c->enc, static_cast<const uint8_t*>(d_info), int64_t(info_stripe_stride),
                     int64_t(info_symbol_stride), static_cast<uint8_t*>(d_rep), int64_t(rep_stripe_stride),
                     int64_t(rep_symbol_stride), n_stripes, symbol_size, static_cast<hipStream_t>(stream));
@@ -1163,6 +1186,7 @@ static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPla
 extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                           uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream) {
     if (!c || !is_erased) return RS_ERR_INVALID;
+    c->work_valu = c->work_salu = 0;
     if (t > c->r) return RS_ERR_CANNOT_RESTORE;
     DevPlan* p = nullptr;
     int rc = decode_plan(c, is_erased, t, &p, static_cast<hipStream_t>(stream));

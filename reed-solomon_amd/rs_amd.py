@@ -77,6 +77,7 @@ _sig("rsg_codec_destroy", None, P)
 _sig("rsg_codec_subfield", ctypes.c_int, P)
 _sig("rsg_set_option", ctypes.c_int, P, ctypes.c_char_p, i64)
 _sig("rsg_last_kernel", ctypes.c_char_p, P)
+_sig("rsg_last_work", ctypes.c_int, P, P, P)
 _sig("rsg_encode", ctypes.c_int, P, P, u64, u64, P, u64, u64, u64, u64, P)
 _sig("rsg_decode", ctypes.c_int, P, P, u64, u64, u64, u64, P, u16, P)
 _sig("rsg_decode_batch", ctypes.c_int, P, P, u64, u64, u64, u64, P, P)
@@ -321,6 +322,13 @@ class Codec:
     @property
     def last_kernel(self):
         return _lib.rsg_last_kernel(self._h).decode()
+
+    @property
+    def last_work(self):
+        """(VALU, SALU) wave-instructions of the hand-scheduled GF(2^16) kernels in the last call."""
+        v, s_ = u64(), u64()
+        _lib.rsg_last_work(self._h, ctypes.byref(v), ctypes.byref(s_))
+        return v.value, s_.value
 
     def set_option(self, name, value):
         rc = _lib.rsg_set_option(self._h, name.encode(), int(value))
