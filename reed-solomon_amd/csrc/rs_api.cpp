@@ -130,6 +130,110 @@ int grow(void** p, size_t& cap, size_t bytes) {
     return 0;
 }
 
+// Recycled plan memory. A new decode pattern used to cost a hipMalloc + hipHostMalloc for its plan
+// and, once the plan cache was full, a hipFree + hipHostFree for the evicted one: calls that
+// synchronise with the device or (un)pin pages, ~0.25 ms apiece, more than the launch they serve.
+// Released plan buffers go to per-size-class free lists instead: a device buffer together with an
+// event recorded after the last launch that used it (handed out again once that event has
+// completed), a pinned staging buffer once its upload has completed.
+struct PlanMemPool {
+    struct Dev {
+        void* p;
+        int device;
+        hipEvent_t guard;  // null: idle
+    };
+    std::mutex mu;
+    std::multimap<size_t, Dev> dev;
+    std::multimap<size_t, void*> host;
+    size_t dev_bytes = 0, host_bytes = 0;
+    static constexpr size_t kDevCap = size_t(512) << 20, kHostCap = size_t(64) << 20;
+    static size_t cls(size_t b) {
+        size_t c = 4096;
+        while (c < b) c <<= 1;
+        return c;
+    }
+};
+PlanMemPool& plan_pool() {
+    static PlanMemPool* p = new PlanMemPool;  // never destroyed: plans may outlive static destructors
+    return *p;
+}
+
+int pool_dev_acquire(size_t bytes, int device, void** out, size_t* cap) {
+    PlanMemPool& P = plan_pool();
+    const size_t c = PlanMemPool::cls(bytes);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        auto range = P.dev.equal_range(c);
+        for (auto it = range.first; it != range.second; ++it) {
+            if (it->second.device != device) continue;
+            if (it->second.guard) {
+                if (hipEventQuery(it->second.guard) != hipSuccess) continue;  // still in use (or unknown)
+                (void)hipEventDestroy(it->second.guard);
+            }
+            *out = it->second.p;
+            *cap = c;
+            P.dev_bytes -= c;
+            P.dev.erase(it);
+            return 0;
+        }
+    }
+    HIP_TRY(hipMalloc(out, c));
+    *cap = c;
+    return 0;
+}
+
+// takes ownership of guard; the current device is `device`
+void pool_dev_release(void* p, size_t cap, int device, hipEvent_t guard) {
+    if (!p) return;
+    PlanMemPool& P = plan_pool();
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (P.dev_bytes + cap <= PlanMemPool::kDevCap) {
+            P.dev.emplace(cap, PlanMemPool::Dev{p, device, guard});
+            P.dev_bytes += cap;
+            return;
+        }
+    }
+    if (guard) {
+        (void)hipEventSynchronize(guard);
+        (void)hipEventDestroy(guard);
+    }
+    (void)hipFree(p);
+}
+
+int pool_host_acquire(size_t bytes, void** out, size_t* cap) {
+    PlanMemPool& P = plan_pool();
+    const size_t c = PlanMemPool::cls(bytes);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        auto it = P.host.find(c);
+        if (it != P.host.end()) {
+            *out = it->second;
+            *cap = c;
+            P.host_bytes -= c;
+            P.host.erase(it);
+            return 0;
+        }
+    }
+    HIP_TRY(hipHostMalloc(out, c, hipHostMallocDefault));
+    *cap = c;
+    return 0;
+}
+
+void pool_host_release(void* p, size_t cap) {  // the copies reading p have completed
+    if (!p) return;
+    PlanMemPool& P = plan_pool();
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (P.host_bytes + cap <= PlanMemPool::kHostCap) {
+            P.host.emplace(cap, p);
+            P.host_bytes += cap;
+            return;
+        }
+    }
+    (void)hipHostFree(p);
+}
+
 // A coding matrix resident on one device, packed for the kernels.
 struct DevPlan {
     int device = 0;
@@ -164,11 +268,25 @@ struct DevPlan {
     std::vector<uint8_t> erased;  // the pattern (empty: encode), to build `dense`
     int64_t uses = 0;                // launches of this plan (JIT policy)
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
+    size_t blob_cap = 0;             // its size class (plan_pool)
     // stream-ordered build: the upload (and device fill) ran on `built_on`; `ready` marks its end, so a
     // launch on another stream waits for it; the pinned source of the upload lives until then
     hipEvent_t ready = nullptr;
     hipStream_t built_on = nullptr;
     void* h_stage = nullptr;
+    size_t stage_cap = 0;
+    // the last launch: `used` recorded on `used_on` after it. A plan launched on more than one stream
+    // is released with hipFree (device-synchronous) instead of to the pool
+    hipEvent_t used = nullptr;
+    hipStream_t used_on = nullptr;
+    bool multi_stream = false;
+    int note_use(hipStream_t st) {
+        if (used_on && used_on != st) multi_stream = true;
+        used_on = st;
+        if (!used) HIP_TRY(hipEventCreateWithFlags(&used, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(used, st));
+        return 0;
+    }
     // called before a launch on stream st: orders it after the build, releases the build's resources
     // once the build is complete
     int order_after_build(hipStream_t st) {
@@ -176,7 +294,7 @@ struct DevPlan {
         if (hipEventQuery(ready) == hipSuccess) {
             (void)hipEventDestroy(ready);
             ready = nullptr;
-            if (h_stage) (void)hipHostFree(h_stage);
+            pool_host_release(h_stage, stage_cap);
             h_stage = nullptr;
             return 0;
         }
@@ -191,8 +309,11 @@ struct DevPlan {
             (void)hipEventSynchronize(ready);
             (void)hipEventDestroy(ready);
         }
-        if (h_stage) (void)hipHostFree(h_stage);
-        if (blob) {
+        pool_host_release(h_stage, stage_cap);
+        if (blob && !multi_stream) {
+            pool_dev_release(blob, blob_cap, device, used);
+            used = nullptr;
+        } else if (blob) {
             (void)hipFree(blob);
         } else {
             (void)hipFree(d_in);
@@ -200,6 +321,7 @@ struct DevPlan {
             (void)hipFree(d_coef);
             (void)hipFree(d_idx);
         }
+        if (used) (void)hipEventDestroy(used);
         (void)hipSetDevice(cur);
     }
 };
@@ -221,10 +343,10 @@ struct PlanBlob {
     // Allocates the plan's buffer and uploads the prefix on stream st, from a pinned copy the plan keeps
     // until the copy is done (no null-stream copy: a new pattern must not stall unrelated streams).
     int upload(DevPlan& p, hipStream_t st) {
-        HIP_TRY(hipMalloc(&p.blob, total));
+        if (int rc = pool_dev_acquire(total, p.device, &p.blob, &p.blob_cap)) return rc;
         p.built_on = st;
         if (host.empty()) return 0;
-        HIP_TRY(hipHostMalloc(&p.h_stage, host.size(), hipHostMallocDefault));
+        if (int rc = pool_host_acquire(host.size(), &p.h_stage, &p.stage_cap)) return rc;
         std::memcpy(p.h_stage, host.data(), host.size());
         HIP_TRY(hipMemcpyAsync(p.blob, p.h_stage, host.size(), hipMemcpyHostToDevice, st));
         return 0;
@@ -1011,10 +1133,23 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     return scratch_release(c, st);
 }
 
+static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym,
+                         uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
+                         hipStream_t st, const int32_t* d_ids, bool dst_local);
+
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
                     const int32_t* d_ids, bool dst_local) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
+    const int rc = run_plan_body(c, p, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st, d_ids,
+                                 dst_local);
+    const int rc2 = p.note_use(st);  // after the launches (also a failed call's partial ones)
+    return rc ? rc : rc2;
+}
+
+static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym,
+                         uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
+                         hipStream_t st, const int32_t* d_ids, bool dst_local) {
     if (int rc = p.order_after_build(st)) return rc;
     if (p.cs) {
         HIP_TRY(hipSetDevice(c->device));
@@ -1778,6 +1913,96 @@ namespace {
 
 constexpr int kMaxChunks = 4;
 
+inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
+
+// Zero-copy eligibility of a per-call launch on arena-resident symbols: the plan runs as the
+// bit-plane XOR kernel (already specialised), which reads each input column once and writes each
+// output once, so it can stream the caller's page-locked symbols across PCIe itself -- one launch
+// instead of H2D DMA + launch + D2H DMA and their stream hand-offs. Kernels that re-read inputs per
+// output tile (m = 16 tiles, the syndrome route) stay on the DMA path.
+bool streams_once(const DevPlan& p, size_t S) { return p.m == 8 && p.xj && !p.xj_failed && S >= 2048; }
+
+// Page-locked symbol arenas. seq_create of a sequence of at least kArenaMin bytes places its symbols
+// in one hipHostMalloc block at stride pad16(S), so rs_generate_repair_symbols / rs_restore_symbols
+// DMA straight between the caller's symbols and HBM (no host gather / scatter, no staging copy). The
+// registry maps a block's start to its size, device-visible address and live symbol count;
+// symbol_destroy returns a block when its last symbol goes. RS_AMD_PINNED_SEQ=0 turns it off (plain
+// calloc per symbol, as before).
+constexpr size_t kArenaMin = size_t(1) << 20;
+struct Arena {
+    size_t bytes;
+    uint8_t* dev;  // device-visible address of the block start (nullptr: DMA only)
+    size_t live;
+};
+struct ArenaRegistry {
+    std::mutex mu;
+    std::map<uintptr_t, Arena> blocks;
+};
+ArenaRegistry& arenas() {
+    static ArenaRegistry* r = new ArenaRegistry;  // never destroyed: symbols may outlive static destructors
+    return *r;
+}
+
+uint8_t* arena_alloc(size_t length, size_t P) {
+    const char* e = std::getenv("RS_AMD_PINNED_SEQ");
+    if ((e && e[0] == '0') || length * P < kArenaMin) return nullptr;
+    void* h = nullptr;
+    if (hipHostMalloc(&h, length * P, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    std::memset(h, 0, length * P);
+    void* dv = nullptr;
+    if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        dv = nullptr;
+    }
+    ArenaRegistry& r = arenas();
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.blocks[uintptr_t(h)] = Arena{length * P, static_cast<uint8_t*>(dv), length};
+    return static_cast<uint8_t*>(h);
+}
+
+// true (and the block released when it was the last) when p lies in an arena
+bool arena_release(const uint8_t* p) {
+    ArenaRegistry& r = arenas();
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto it = r.blocks.upper_bound(uintptr_t(p));
+    if (it == r.blocks.begin()) return false;
+    --it;
+    if (uintptr_t(p) >= it->first + it->second.bytes) return false;
+    if (--it->second.live == 0) {
+        (void)hipHostFree(reinterpret_cast<void*>(it->first));
+        r.blocks.erase(it);
+    }
+    return true;
+}
+
+// The cnt symbols form one strided run inside one arena: symbols[i]->data == base + i * pitch with a
+// 16-byte aligned base and pitch >= pad16(S). Returns base (nullptr otherwise); *dev = the run's
+// device-visible address (nullptr when the block has none).
+const uint8_t* arena_run(symbol_t* const* syms, size_t cnt, size_t S, size_t* pitch, uint8_t** dev) {
+    if (!cnt || !syms[0]) return nullptr;
+    const uint8_t* b = syms[0]->data;
+    size_t p = pad16(S);
+    if (cnt > 1) {
+        if (!syms[1] || syms[1]->data <= b) return nullptr;
+        p = size_t(syms[1]->data - b);
+    }
+    if (p < pad16(S) || (p & 15) || (uintptr_t(b) & 15)) return nullptr;
+    for (size_t i = 2; i < cnt; ++i)
+        if (!syms[i] || syms[i]->data != b + i * p) return nullptr;
+    ArenaRegistry& r = arenas();
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto it = r.blocks.upper_bound(uintptr_t(b));
+    if (it == r.blocks.begin()) return nullptr;
+    --it;
+    if (uintptr_t(b) + (cnt - 1) * p + pad16(S) > it->first + it->second.bytes) return nullptr;
+    *pitch = p;
+    if (dev) *dev = it->second.dev ? it->second.dev + (uintptr_t(b) - it->first) : nullptr;
+    return b;
+}
+
 struct Impl {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1788,6 +2013,15 @@ struct Impl {
     size_t cap = 0;
     std::unique_ptr<HostPool> pool;  // gather / scatter workers
     hipEvent_t ev[kMaxChunks] = {};
+    // arena-resident symbols: chunk c + 1's H2D DMA runs on in_stream while chunk c is encoded /
+    // decoded and copied back on stream (ev_in[c] orders the kernel after its columns arrived)
+    hipStream_t in_stream = nullptr;
+    hipEvent_t ev_in[kMaxChunks] = {};
+    // arena-resident stripes: column chunks per call (RS_AMD_DROPIN_CHUNKS, 1..kMaxChunks) and whether
+    // repair symbols go back by k_put_rows writes instead of DMA (RS_AMD_DROPIN_PUT)
+    int arena_chunks = 2;
+    bool arena_put = true;
+    bool arena_zc = true;  // RS_AMD_DROPIN_ZC=0: no zero-copy launches (see streams_once)
     int32_t* h_rows = nullptr;  // pinned / device row list of the decode's packed copy-back
     int32_t* d_rows = nullptr;
     size_t rows_cap = 0;
@@ -1798,6 +2032,9 @@ struct Impl {
         if (d_rows) (void)hipFree(d_rows);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev_in)
+            if (e) (void)hipEventDestroy(e);
+        if (in_stream) (void)hipStreamDestroy(in_stream);
         if (h_buf) (void)hipHostFree(h_buf);
         if (d_buf) (void)hipFree(d_buf);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1834,12 +2071,11 @@ struct Impl {
 // Column chunks of one per-call stripe: large symbols are split into up to kMaxChunks column ranges
 // (multiples of the 2 KiB kernel block), so the host gather of chunk c + 1 and the scatter of chunk
 // c - 1 overlap the copies and kernel of chunk c.
-size_t chunk_width(size_t S) {
-    if (S < 4 * 8192) return S;
-    const size_t w = (S + kMaxChunks - 1) / kMaxChunks;
+size_t chunk_width(size_t S, int maxc = kMaxChunks) {
+    if (S < 4 * 8192 || maxc <= 1) return S;
+    const size_t w = (S + maxc - 1) / maxc;
     return (w + 2047) / 2048 * 2048;
 }
-inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
 
 }  // namespace
 
@@ -1867,9 +2103,14 @@ extern "C" RS_t* rs_create(void) {
     int workers = int(std::min(8u, std::max(1u, std::thread::hardware_concurrency()))) - 1;
     if (const char* e = std::getenv("RS_AMD_HOST_THREADS")) workers = std::max(0, std::atoi(e) - 1);
     impl->pool = std::make_unique<HostPool>(workers);
+    if (const char* e = std::getenv("RS_AMD_DROPIN_CHUNKS")) impl->arena_chunks = std::clamp(std::atoi(e), 1, kMaxChunks);
+    if (const char* e = std::getenv("RS_AMD_DROPIN_PUT")) impl->arena_put = e[0] == '1';
+    if (const char* e = std::getenv("RS_AMD_DROPIN_ZC")) impl->arena_zc = e[0] != '0';
     bool ev_ok = true;
     for (hipEvent_t& e : impl->ev) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-    if (!ev_ok || hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking) != hipSuccess) {
+    for (hipEvent_t& e : impl->ev_in) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok || hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&impl->in_stream, hipStreamNonBlocking) != hipSuccess) {
         delete impl;
         gf_destroy(rs->gf);
         cc_destroy(rs->cc);
@@ -1900,24 +2141,53 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
     rsg_codec* c = nullptr;
     int rc = im.codec(k, r, &c);
     if (rc) return rc;
-    const size_t P = pad16(S), n = size_t(k) + r, W = chunk_width(S), nch = (S + W - 1) / W;
+    // symbols in page-locked arenas (seq_create) are copied in place by DMA; otherwise they are gathered
+    // into / scattered from the pinned staging buffer by the host pool
+    size_t ip = 0, rp = 0;
+    uint8_t* idev = nullptr;
+    const uint8_t* ib = arena_run(inf->symbols, k, S, &ip, &idev);
+    uint8_t* rdev = nullptr;
+    uint8_t* rb = const_cast<uint8_t*>(arena_run(rep->symbols, r, S, &rp, &rdev));
+    const size_t P = pad16(S), n = size_t(k) + r, W = chunk_width(S, ib ? im.arena_chunks : kMaxChunks),
+                 nch = (S + W - 1) / W;
+    if (ib && rb && idev && rdev && im.arena_zc && streams_once(*c->enc, S)) {
+        rc = rsg_encode(c, idev, int64_t(n * ip), int64_t(ip), rdev, int64_t(n * rp), int64_t(rp), 1, int64_t(S),
+                        im.stream);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+        HIP_TRY(hipEventSynchronize(im.ev[0]));
+        return 0;
+    }
     if (im.reserve(n * P)) return 1;
     uint8_t *h = im.h_buf, *d = im.d_buf;
     // chunk c: gather k columns -> H2D (2D) -> encode -> D2H (2D); scatter of c - 1 overlaps it
     auto scatter = [&](size_t c) {
+        if (rb) return;
         const size_t off = c * W, w = std::min(W, S - off);
         im.pool->run(r, [&](int p) { std::memcpy(rep->symbols[p]->data + off, h + (k + size_t(p)) * P + off, w); });
     };
     for (size_t ch = 0; ch < nch; ++ch) {
         const size_t off = ch * W, w = std::min(W, S - off);
-        im.pool->run(k, [&](int i) { std::memcpy(h + size_t(i) * P + off, inf->symbols[i]->data + off, w); });
-        HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, k, hipMemcpyHostToDevice, im.stream));
+        if (ib) {
+            HIP_TRY(hipMemcpy2DAsync(d + off, P, ib + off, ip, w, k, hipMemcpyHostToDevice, im.in_stream));
+            HIP_TRY(hipEventRecord(im.ev_in[ch], im.in_stream));
+            HIP_TRY(hipStreamWaitEvent(im.stream, im.ev_in[ch], 0));
+        } else {
+            im.pool->run(k, [&](int i) { std::memcpy(h + size_t(i) * P + off, inf->symbols[i]->data + off, w); });
+            HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, k, hipMemcpyHostToDevice, im.stream));
+        }
         rc = rsg_encode(c, d + off, n * P, P, d + size_t(k) * P + off, n * P, P, 1, w, im.stream);
         if (rc) return rc;
-        HIP_TRY(hipMemcpy2DAsync(h + size_t(k) * P + off, P, d + size_t(k) * P + off, P, w, r, hipMemcpyDeviceToHost,
-                                 im.stream));
+        if (rb && rdev && im.arena_put)
+            HIP_TRY(launch_put_rows(rdev + off, int64_t(rp), d + size_t(k) * P + off, int64_t(P), nullptr, int64_t(r),
+                                    int64_t(ch + 1 == nch ? P - off : w), im.stream));
+        else if (rb)
+            HIP_TRY(hipMemcpy2DAsync(rb + off, rp, d + size_t(k) * P + off, P, w, r, hipMemcpyDeviceToHost, im.stream));
+        else
+            HIP_TRY(hipMemcpy2DAsync(h + size_t(k) * P + off, P, d + size_t(k) * P + off, P, w, r,
+                                     hipMemcpyDeviceToHost, im.stream));
         HIP_TRY(hipEventRecord(im.ev[ch], im.stream));
-        if (ch) {
+        if (ch && !rb) {  // host scatter of chunk c - 1 overlaps chunk c
             HIP_TRY(hipEventSynchronize(im.ev[ch - 1]));
             scatter(ch - 1);
         }
@@ -1959,13 +2229,29 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     DevPlan* dplan = nullptr;
     if ((rc = decode_plan(c, is_erased, t, &dplan, im.stream))) return rc;
     const bool pending = c->m <= 8 && c->jit != 0 && !dplan->xj && !dplan->jit && !dplan->xj_failed && !dplan->jit_failed;
-    const size_t P = pad16(S), W = pending ? S : chunk_width(S), nch = (S + W - 1) / W,
+    size_t sp = 0;
+    uint8_t* sdev = nullptr;
+    uint8_t* sb = const_cast<uint8_t*>(arena_run(rcv->symbols, n, S, &sp, &sdev));
+    if (sb && sdev && im.arena_zc && streams_once(*dplan, S)) {  // in place across PCIe, one launch
+        rc = rsg_decode(c, sdev, n * sp, sp, 1, S, is_erased, t, im.stream);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+        HIP_TRY(hipEventSynchronize(im.ev[0]));
+        return 0;
+    }
+    // a stripe in a page-locked arena (seq_create) is copied in place: all n rows in by one 2D DMA
+    // (erased rows ride along unread), restored rows out by DMA of their span or, when scattered,
+    // written across PCIe by k_put_rows straight into the arena
+    const size_t P = pad16(S), W = pending ? S : chunk_width(S, sb ? im.arena_chunks : kMaxChunks),
+                 nch = (S + W - 1) / W,
                  nl = lost.size();
     // erased slots are neither gathered nor read by the decoder. Only restored rows come back: the span
     // lost[0] .. lost.back() when it is (nearly) contiguous, else the rows packed on the device behind
     // the stripe (k_gather_rows) and copied as one block
     const size_t lo = size_t(lost.front()), rows = size_t(lost.back()) - lo + 1;
     const bool packed = rows > nl + nl / 4;
+    const bool put = sb && packed && sdev;  // restored rows written in place by the device
+    const bool host_scatter = !sb || (packed && !sdev);
     if (im.reserve((n + (packed ? nl : 0)) * P)) return 1;
     uint8_t *h = im.h_buf, *d = im.d_buf;
     if (packed) {
@@ -1984,6 +2270,7 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     }
     uint8_t *hp = h + n * P, *dp = d + n * P;  // packed restored rows (row j = slot lost[j])
     auto scatter = [&](size_t ch) {
+        if (!host_scatter) return;
         const size_t off = ch * W, w = std::min(W, S - off);
         im.pool->run(int(nl), [&](int j) {
             const size_t i = size_t(lost[size_t(j)]);
@@ -1992,14 +2279,29 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     };
     for (size_t ch = 0; ch < nch; ++ch) {
         const size_t off = ch * W, w = std::min(W, S - off);
-        im.pool->run(int(keep.size()), [&](int j) {
-            const size_t i = size_t(keep[size_t(j)]);
-            std::memcpy(h + i * P + off, rcv->symbols[i]->data + off, w);
-        });
-        HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, n, hipMemcpyHostToDevice, im.stream));
+        if (sb) {
+            HIP_TRY(hipMemcpy2DAsync(d + off, P, sb + off, sp, w, n, hipMemcpyHostToDevice, im.in_stream));
+            HIP_TRY(hipEventRecord(im.ev_in[ch], im.in_stream));
+            HIP_TRY(hipStreamWaitEvent(im.stream, im.ev_in[ch], 0));
+        } else {
+            im.pool->run(int(keep.size()), [&](int j) {
+                const size_t i = size_t(keep[size_t(j)]);
+                std::memcpy(h + i * P + off, rcv->symbols[i]->data + off, w);
+            });
+            HIP_TRY(hipMemcpy2DAsync(d + off, P, h + off, P, w, n, hipMemcpyHostToDevice, im.stream));
+        }
         rc = rsg_decode(c, d + off, n * P, P, 1, w, is_erased, t, im.stream);
         if (rc) return rc;
-        if (packed) {
+        if (put) {
+            // chunk widths are multiples of 2048 but the last; it runs to the padded row end, for which
+            // the arena's pitch leaves room
+            const size_t wp = ch + 1 == nch ? P - off : w;
+            HIP_TRY(launch_put_rows(sdev + off, int64_t(sp), d + off, int64_t(P), im.d_rows, int64_t(nl), int64_t(wp),
+                                    im.stream));
+        } else if (sb && !packed) {
+            HIP_TRY(hipMemcpy2DAsync(sb + lo * sp + off, sp, d + lo * P + off, P, w, rows, hipMemcpyDeviceToHost,
+                                     im.stream));
+        } else if (packed) {
             HIP_TRY(launch_gather_rows(dp + off, int64_t(P), d + off, int64_t(P), im.d_rows, int64_t(nl), int64_t(w),
                                        im.stream));
             HIP_TRY(hipMemcpy2DAsync(hp + off, P, dp + off, P, w, nl, hipMemcpyDeviceToHost, im.stream));
@@ -2008,7 +2310,7 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
                                      im.stream));
         }
         HIP_TRY(hipEventRecord(im.ev[ch], im.stream));
-        if (ch) {
+        if (ch && host_scatter) {
             HIP_TRY(hipEventSynchronize(im.ev[ch - 1]));
             scatter(ch - 1);
         }
@@ -2032,7 +2334,7 @@ extern "C" symbol_t* symbol_create(size_t symbol_size) {
 
 extern "C" void symbol_destroy(symbol_t* s) {
     if (!s) return;
-    std::free(s->data);
+    if (!arena_release(s->data)) std::free(s->data);
     std::free(s);
 }
 
@@ -2060,6 +2362,22 @@ extern "C" symbol_seq_t* seq_create(size_t length, size_t symbol_size) {
     if (!q->symbols) {
         std::free(q);
         return nullptr;
+    }
+    // large sequences: one zeroed page-locked arena at stride pad16(S) (see arena_alloc)
+    const size_t P = pad16(symbol_size ? symbol_size : 1);
+    if (uint8_t* blk = symbol_size ? arena_alloc(length, P) : nullptr) {
+        bool ok = true;
+        for (size_t i = 0; i < length && ok; ++i)
+            ok = (q->symbols[i] = static_cast<symbol_t*>(std::calloc(1, sizeof(symbol_t)))) != nullptr;
+        if (!ok) {
+            for (size_t i = 0; i < length; ++i) std::free(q->symbols[i]);
+            for (size_t i = 0; i < length; ++i) arena_release(blk);  // drops the block with its last count
+            std::free(q->symbols);
+            std::free(q);
+            return nullptr;
+        }
+        for (size_t i = 0; i < length; ++i) q->symbols[i]->data = blk + i * P;
+        return q;
     }
     for (size_t i = 0; i < length; ++i) {
         if (!(q->symbols[i] = symbol_create(symbol_size))) {

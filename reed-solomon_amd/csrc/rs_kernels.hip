@@ -1390,6 +1390,28 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
     return hipGetLastError();
 }
 
+// 16-byte stores of whole rows across PCIe into page-locked host memory (posted writes; visible to
+// the host once the stream's completion event has been waited on)
+__global__ void __launch_bounds__(256) k_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
+                                                  const int32_t* rows, int64_t units) {
+    const int64_t u = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (u >= units) return;
+    const int64_t i = rows ? rows[blockIdx.y] : int64_t(blockIdx.y);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<u32x4*>(dst + i * dpitch)[u] = reinterpret_cast<const u32x4*>(src + i * spitch)[u];
+}
+
+hipError_t launch_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                           int64_t nrows, int64_t width, hipStream_t st) {
+    const int64_t units = width / 16;
+    if (nrows <= 0 || units <= 0) return hipSuccess;
+    if ((width & 15) || (dpitch & 15) || (spitch & 15) || (uintptr_t(dst) & 15) || (uintptr_t(src) & 15))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_put_rows, dim3(unsigned((units + 255) / 256), unsigned(nrows)), dim3(256), 0, st, dst, dpitch,
+                       src, spitch, rows, units);
+    return hipGetLastError();
+}
+
 hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
     if (n_sel <= 0) return hipSuccess;
     if (a.n > 256) return hipErrorInvalidValue;

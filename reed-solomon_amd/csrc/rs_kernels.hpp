@@ -94,6 +94,11 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
 // dst row j = src row rows[j] for j < nrows, `width` bytes each (16-byte aligned rows, padded pitch)
 hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
                               int64_t nrows, int64_t width, hipStream_t st);
+// dst row rows[j] = src row rows[j] (same slot, different pitch): the per-call decode writes its
+// restored rows straight into the caller's page-locked stripe (dst a device-visible host address);
+// rows == nullptr: rows 0 .. nrows - 1
+hipError_t launch_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                           int64_t nrows, int64_t width, hipStream_t st);
 
 // m = 16 cyclotomic syndromes (k_cs16, the reference's fft_transform_cycl structure, src/rs/fft.c:39-100):
 // S_j = sum_i X_i^j in_i for the needed j, inputs grouped by cyclotomic coset (16 slots at positions

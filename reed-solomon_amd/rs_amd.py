@@ -70,6 +70,8 @@ def _sig(name, restype, *argtypes):
 
 _sig("rs_create", P)
 _sig("rs_destroy", None, P)
+_sig("seq_create", ctypes.POINTER(SymbolSeqT), ctypes.c_size_t, ctypes.c_size_t)
+_sig("seq_destroy", None, ctypes.POINTER(SymbolSeqT))
 _sig("rs_generate_repair_symbols", ctypes.c_int, P, ctypes.POINTER(SymbolSeqT), ctypes.POINTER(SymbolSeqT))
 _sig("rs_restore_symbols", ctypes.c_int, P, u16, u16, ctypes.POINTER(SymbolSeqT), P, u16)
 _sig("rsg_codec_create", ctypes.c_int, ctypes.c_int, u16, u16, ctypes.POINTER(P))
@@ -202,6 +204,35 @@ class _SeqBuf:
         self.seq = SymbolSeqT(len(arrays), symbol_size, self.ptrs)
 
 
+class Seq:
+    """A library-allocated symbol_seq_t (seq_create, reference include/memory/seq.h). Sequences of
+    1 MiB and more live in one page-locked arena, which rs_generate_repair_symbols /
+    rs_restore_symbols copy in place by DMA. symbols[i] is a numpy view of symbol i."""
+
+    def __init__(self, length, symbol_size):
+        self._p = _lib.seq_create(length, symbol_size)
+        if not self._p:
+            raise MemoryError("seq_create")
+        self.length, self.symbol_size = length, symbol_size
+        q = self._p.contents
+        self.symbols = [np.ctypeslib.as_array(q.symbols[i].contents.data, (symbol_size,)) for i in range(length)]
+
+    def view(self, start, count):
+        """symbol_seq_t over symbols [start, start + count) (shares the symbol pointers)."""
+        q = self._p.contents
+        base = ctypes.cast(q.symbols, ctypes.c_void_p).value + start * ctypes.sizeof(ctypes.c_void_p)
+        return SymbolSeqT(count, self.symbol_size, ctypes.cast(base, ctypes.POINTER(ctypes.POINTER(SymbolT))))
+
+    def close(self):
+        if self._p:
+            self.symbols = []
+            _lib.seq_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.close()
+
+
 class RS:
     """Mirror of the reference context API (reference include/rs/reed_solomon.h:44-74)."""
 
@@ -219,13 +250,22 @@ class RS:
         self.close()
 
     def generate_repair_symbols(self, inf_symbols, rep_symbols):
-        """inf_symbols: k host symbols, rep_symbols: r host symbols (written). Returns the C rc."""
+        """inf_symbols: k host symbols, rep_symbols: r host symbols (written); or a Seq of k + r
+        symbols as inf_symbols with rep_symbols = r. Returns the C rc."""
+        if isinstance(inf_symbols, Seq):
+            q, r = inf_symbols, int(rep_symbols)
+            a, b = q.view(0, q.length - r), q.view(q.length - r, r)
+            return _lib.rs_generate_repair_symbols(self._h, ctypes.byref(a), ctypes.byref(b))
         S = inf_symbols[0].size if len(inf_symbols) else rep_symbols[0].size
         a, b = _SeqBuf(list(inf_symbols), S), _SeqBuf(list(rep_symbols), S)
         return _lib.rs_generate_repair_symbols(self._h, ctypes.byref(a.seq), ctypes.byref(b.seq))
 
     def restore_symbols(self, k, r, rcv_symbols, is_erased, t):
-        """rcv_symbols: k + r host symbols, erased ones zero; restored in place. Returns the C rc."""
+        """rcv_symbols: k + r host symbols (or a Seq), erased ones zero; restored in place. Returns the C rc."""
+        if isinstance(rcv_symbols, Seq):
+            er = np.ascontiguousarray(is_erased, dtype=np.bool_)
+            a = rcv_symbols.view(0, rcv_symbols.length)
+            return _lib.rs_restore_symbols(self._h, k, r, ctypes.byref(a), _np_ptr(er), t)
         S = rcv_symbols[0].size
         a = _SeqBuf(list(rcv_symbols), S)
         er = np.ascontiguousarray(is_erased, dtype=np.bool_)

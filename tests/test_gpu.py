@@ -590,6 +590,58 @@ def test_drop_in_m16_large_symbols():
     rs.close()
 
 
+@pytest.mark.parametrize("k,r,S,pattern", [(128, 32, 65536, "bench"), (128, 32, 65536, "span"),
+                                           (128, 32, 65536, "random"), (300, 64, 8192 + 6, "random"),
+                                           (64, 16, 16384 + 2, "bench")])
+def test_drop_in_pinned_seq(k, r, S, pattern):
+    """seq_create places large sequences in a page-locked arena and the per-call API copies them in
+    place (2D DMA in; restored rows out by DMA of their span or by k_put_rows across PCIe): encode and
+    restore bit-exact vs the oracle, for scattered (bench, random) and contiguous (span) erasures,
+    GF(256) and GF(2^16) codes, symbol sizes that are not multiples of 16 (padded arena pitch); the
+    same calls on pageable symbols (RS_AMD_PINNED_SEQ=0 -> calloc per symbol) give the same bytes."""
+    import os
+    rng = np.random.default_rng(k * 7 + S)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    if pattern == "bench":
+        er = rs_amd.bench_pattern(k, r)
+    elif pattern == "span":
+        er = np.zeros(k + r, bool)
+        er[5:5 + r] = True
+    else:
+        er = np.zeros(k + r, bool)
+        er[rng.choice(k + r, r, replace=False)] = True
+    want = np.zeros((k + r, S), np.uint8)
+    want[:k] = data
+    assert oracle_encode(k, r, want) == 0
+    rs = rs_amd.RS()
+    outs = []
+    for flag in ("1", "0"):
+        os.environ["RS_AMD_PINNED_SEQ"] = flag
+        try:
+            q = rs_amd.Seq(k + r, S)
+        finally:
+            os.environ.pop("RS_AMD_PINNED_SEQ")
+        pitch = q.symbols[1].ctypes.data - q.symbols[0].ctypes.data
+        if flag == "1":
+            assert pitch == _pad(S), "seq_create did not place the sequence in one arena"
+        for i in range(k):
+            q.symbols[i][:] = data[i]
+        for call in range(4):  # decode calls 3+ of a GF(256) pattern run the specialised plan, 4+ zero-copy
+            assert rs.generate_repair_symbols(q, r) == 0
+            got = np.stack(q.symbols)
+            assert np.array_equal(got, want), f"encode pinned={flag} call {call}"
+            for i in np.nonzero(er)[0]:
+                q.symbols[i][:] = 0
+            assert rs.restore_symbols(k, r, q, er, int(er.sum())) == 0
+            got = np.stack(q.symbols)
+            assert np.array_equal(got[:k], data), f"restore pinned={flag} call {call}"
+            assert not got[k:][er[k:]].any()  # erased repair slots are not written
+        outs.append(got)
+        q.close()
+    assert np.array_equal(outs[0], outs[1])
+    rs.close()
+
+
 
 @pytest.mark.parametrize("k,r,S,n,pinned", [(128, 32, 65536, 30, True), (10, 4, 4096 + 24, 300, False),
                                             (300, 70, 2048 + 10, 5, True)])
