@@ -412,15 +412,22 @@ def main():
     # roofline of the dominant kernel (encode and decode move the same algorithmic bytes here)
     dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, kern_enc) if enc_ms >= dec_ms else (dec_ms, dec_bytes, kern_dec)
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
-    traffic = measured_traffic(dom_name, f"k{k}_r{r}_S{S}_n{n}_t{t}")
+    cfg_key = f"k{k}_r{r}_S{S}_n{n}_t{t}"
+    traffic = measured_traffic(dom_name, cfg_key)
     line = base_line(args, world, n, k, r, S, t, elapsed)
     line["config"]["kernel"] = {"encode": kern_enc, "decode": kern_dec}
     line["rccl_world"] = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes}
+                        "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
+                        "traffic_key": cfg_key}
     if codec.subfield == 16:  # compute roofline of the GF(2^16) kernels (issue bound, not HBM)
         line["roofline"]["compute"] = compute_roofline(work_enc, enc_ms, work_dec, dec_ms)
+    # both legs: algorithmic bytes and PMC-measured HBM bytes per launch (null when unmeasured)
+    line["per_launch"] = {"encode": {"kernel": kern_enc, "ms": round(enc_ms, 3), "bytes": enc_bytes,
+                                     "traffic": measured_traffic(kern_enc, cfg_key)},
+                          "decode": {"kernel": kern_dec, "ms": round(dec_ms, 3), "bytes": dec_bytes,
+                                     "traffic": measured_traffic(kern_dec, cfg_key)}}
     line["encode_ms"] = round(enc_ms, 3)
     line["decode_ms"] = round(dec_ms, 3)
     line["per_rank"] = per_rank

@@ -1,6 +1,6 @@
 // rs_xj.cpp -- generator, cache and launcher of the bit-plane XOR kernels (see rs_xj.hpp).
 //
-// Generated kernel `rs_xj` (one per coding matrix and slot lists):
+// Generated kernel `rs_xj_<source hash>` (one per coding matrix and slot lists):
 //   grid (column chunks of 256 B, stripes), block = 64 x roles threads. All waves of a block work on
 //   the same 256-byte column of one stripe; wave w ("role") owns outputs opr*w .. opr*w + opr - 1
 //   (opr = min(16, R) outputs per role by default, XjConfig).
@@ -727,10 +727,26 @@ int xj_pairs(int R) {
     return std::max(1, xj_max_roles(R) / xj_roles(R));
 }
 
+// The kernel's symbol carries the hash of its generated source (rs_xj_<8 hex>), so profiler records
+// (rocprofv3 Kernel_Name) tell the encode and decode kernels of one run apart; the same hash names
+// the kernel in rsg_last_kernel ("rs_xj[RxK:<hash>]").
+static std::string xj_named_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
+                                   const std::vector<int32_t>& out_slots, std::string* fname) {
+    std::string src = xj_source(M, K, R, in_slots, out_slots);
+    char nm[32];
+    std::snprintf(nm, sizeof nm, "rs_xj_%08llx", static_cast<unsigned long long>(jit_hash(src) & 0xffffffff));
+    const std::string key = ") rs_xj(XJArgs a)";
+    const size_t at = src.find(key);
+    if (at != std::string::npos) src.replace(at, key.size(), std::string(") ") + nm + "(XJArgs a)");
+    *fname = nm;
+    return src;
+}
+
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                   const std::vector<int32_t>& out_slots) {
     if (!xj_supported(8, K, R)) return 0;
-    const std::string src = xj_source(M, K, R, in_slots, out_slots);
+    std::string fname;
+    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname);
     std::vector<char> code;
     return jit_code(src, "xj", jit_hash(src), code) ? 3 : 0;
 }
@@ -739,7 +755,8 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
              const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out) {
     out.reset();
     if (!xj_supported(8, K, R)) return 0;
-    const std::string src = xj_source(M, K, R, in_slots, out_slots);
+    std::string fname;
+    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname);
     uint64_t h = 0;
     std::shared_ptr<JitModule> mod;
     if (jit_module(src, "xj", mod, &h)) return 3;
@@ -748,9 +765,9 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     (void)hipGetDevice(&k->device);
     k->roles = xj_roles(R);
     k->pairs = XjConfig(R).lfin ? xj_pairs(R) : 0;
-    if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), "rs_xj") != hipSuccess) return 3;
+    if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), fname.c_str()) != hipSuccess) return 3;
     char nm[64];
-    std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%08llx]", R, K, static_cast<unsigned long long>(h & 0xffffffff));
+    std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%s]", R, K, fname.c_str() + 6);
     k->name = nm;
     out = std::move(k);
     return 0;
