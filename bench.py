@@ -241,9 +241,11 @@ VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions / s: 256 CUs x 4 SIM
 
 
 def compute_roofline(work_enc, enc_ms, work_dec, dec_ms):
-    """Issue rate of the hand-scheduled GF(2^16) kernels (their generated steps' VALU + SALU counts,
-    rsg_last_work) against the chip's VALU issue peak. gpr-indexed VALU (the table lookups) issue at half
-    rate on gfx950 (profiles/r1_issue_bench.log), so frac ~0.5 is the practical ceiling of these kernels."""
+    """Issue rate of the generated kernels (their asm's VALU + SALU counts per launch, rsg_last_work:
+    XOR kernels per 256-byte column, GF(2^16) steps per step) against the chip's VALU issue peak
+    (2 cycles per wave64 op per SIMD at 2.4 GHz). The chip holds ~1.4-1.5 GHz under these loads, and
+    gpr-indexed VALU (the GF(2^16) table lookups) issue at half rate on gfx950
+    (profiles/r1_issue_bench.log), so frac ~0.6 (XOR kernels) / ~0.5 (GF(2^16)) are practical ceilings."""
     v = work_enc[0] + work_dec[0]
     sa = work_enc[1] + work_dec[1]
     t = (enc_ms + dec_ms) / 1e3
@@ -421,7 +423,7 @@ def main():
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
                         "traffic_key": cfg_key}
-    if codec.subfield == 16:  # compute roofline of the GF(2^16) kernels (issue bound, not HBM)
+    if work_enc[0] + work_dec[0] > 0:  # compute roofline (the kernels are VALU-issue bound)
         line["roofline"]["compute"] = compute_roofline(work_enc, enc_ms, work_dec, dec_ms)
     # both legs: algorithmic bytes and PMC-measured HBM bytes per launch (null when unmeasured)
     line["per_launch"] = {"encode": {"kernel": kern_enc, "ms": round(enc_ms, 3), "bytes": enc_bytes,

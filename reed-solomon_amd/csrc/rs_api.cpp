@@ -1249,6 +1249,9 @@ static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t
         // 256-byte column chunks up to the last full 2 KiB boundary; the rest by the generic tail kernel
         int rc = xj_launch(*p.xj, x, int64_t(n_stripes), (a.nbytes / 2048) * (2048 / kXjChunk), st);
         if (rc) return rc;
+        const uint64_t cols = n_stripes * uint64_t(a.nbytes / 2048) * (2048 / kXjChunk);
+        c->work_valu += cols * p.xj->valu_per_col;
+        c->work_salu += cols * p.xj->salu_per_col;
         launch_m8_tail(a, int64_t(n_stripes), unsigned(nt32), st);
         HIP_TRY(hipGetLastError());
         return 0;

@@ -18,6 +18,7 @@
 //   buffer addressing, spread loads, Horner in alpha, LDS-table finish (persistent grid), LDS table
 //   sharing between roles.
 #include "rs_xj.hpp"
+#include <cstring>
 
 #include <algorithm>
 #include <cstdio>
@@ -639,6 +640,41 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
 
 }  // namespace
 
+// Static instruction counts of one column (see XjKernel::valu_per_col): VALU = "v_" lines; SALU = "s_"
+// lines other than program-flow / wait / message (SOPP) and scalar memory ops.
+static void count_insts(const std::vector<std::string>& L, uint64_t mult, uint64_t* valu, uint64_t* salu) {
+    static const char* kNotSalu[] = {"s_waitcnt", "s_nop", "s_barrier", "s_branch", "s_cbranch", "s_setprio",
+                                     "s_sleep", "s_endpgm", "s_load", "s_buffer_load", "s_store", "s_dcache",
+                                     "s_set_gpr_idx_on", "s_set_gpr_idx_off"};
+    for (const std::string& ln : L) {
+        size_t i = ln.find_first_not_of(" \t");
+        if (i == std::string::npos) continue;
+        if (ln.compare(i, 2, "v_") == 0) {
+            *valu += mult;
+        } else if (ln.compare(i, 2, "s_") == 0) {
+            bool flow = false;
+            for (const char* f : kNotSalu) flow = flow || ln.compare(i, std::strlen(f), f) == 0;
+            if (!flow) *salu += mult;
+        }
+    }
+}
+
+static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
+               const std::vector<int32_t>& out_slots, uint64_t* valu, uint64_t* salu) {
+    const XjConfig C(R);
+    const XjBasis& B = xj_basis(C.horner);
+    std::vector<uint8_t> cb(M.size());
+    for (size_t e = 0; e < M.size(); ++e) cb[e] = C.lfin ? gamma8().coord(M[e]) : B.bits(M[e]);
+    const int roles = (R + C.opr - 1) / C.opr;
+    *valu = *salu = 0;
+    std::vector<std::string> fin = finish_block(C);
+    if (!fin.empty()) fin.erase(fin.begin(), fin.begin() + 2);  // the branch around the block and its label
+    for (int w = 0; w < roles; ++w) {
+        count_insts(role_block(C, w, cb, K, R, in_slots, out_slots), 1, valu, salu);
+        if (!(C.ablate & 1)) count_insts(fin, 1, valu, salu);
+    }
+}
+
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots) {
     const XjConfig C(R);
@@ -769,6 +805,7 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%s]", R, K, fname.c_str() + 6);
     k->name = nm;
+    xj_counts(M, K, R, in_slots, out_slots, &k->valu_per_col, &k->salu_per_col);
     out = std::move(k);
     return 0;
 }

@@ -45,6 +45,10 @@ struct XjKernel {
     int roles = 0;  // waves per column (opr outputs each)
     int pairs = 0;  // > 0: persistent kernel (LDS finish), columns per workgroup in flight, grid <= CUs
     std::string name;
+    // wave instructions per 256-byte column, all role waves together, counted in the generated asm
+    // (the XOR network, the finish once per role, loads / stores / addressing); the compiler's few
+    // prologue instructions are not included
+    uint64_t valu_per_col = 0, salu_per_col = 0;
 };
 
 constexpr int kXjMaxRoles = 16;     // 1024-thread blocks
