@@ -167,7 +167,16 @@ int pool_dev_acquire(size_t bytes, int device, void** out, size_t* cap) {
         for (auto it = range.first; it != range.second; ++it) {
             if (it->second.device != device) continue;
             if (it->second.guard) {
-                if (hipEventQuery(it->second.guard) != hipSuccess) continue;  // still in use (or unknown)
+                const hipError_t q = hipEventQuery(it->second.guard);
+                (void)hipGetLastError();  // an ignored status must not surface at the next launch check
+                if (q == hipErrorNotReady) continue;  // still in use
+                if (q != hipSuccess) {  // unexpected: wait for the last launch the hard way
+                    static bool once = false;
+                    if (!once) std::fprintf(stderr, "librs_amd: plan pool: event query: %s\n", hipGetErrorString(q));
+                    once = true;
+                    (void)hipEventSynchronize(it->second.guard);
+                    (void)hipGetLastError();
+                }
                 (void)hipEventDestroy(it->second.guard);
             }
             *out = it->second.p;
@@ -199,6 +208,7 @@ void pool_dev_release(void* p, size_t cap, int device, hipEvent_t guard) {
         (void)hipEventDestroy(guard);
     }
     (void)hipFree(p);
+    (void)hipGetLastError();
 }
 
 int pool_host_acquire(size_t bytes, void** out, size_t* cap) {
@@ -232,6 +242,7 @@ void pool_host_release(void* p, size_t cap) {  // the copies reading p have comp
         }
     }
     (void)hipHostFree(p);
+    (void)hipGetLastError();
 }
 
 // A coding matrix resident on one device, packed for the kernels.
@@ -291,7 +302,9 @@ struct DevPlan {
     // once the build is complete
     int order_after_build(hipStream_t st) {
         if (!ready) return 0;
-        if (hipEventQuery(ready) == hipSuccess) {
+        const hipError_t q = hipEventQuery(ready);
+        (void)hipGetLastError();  // NotReady is a status, not an error of the next launch
+        if (q == hipSuccess) {
             (void)hipEventDestroy(ready);
             ready = nullptr;
             pool_host_release(h_stage, stage_cap);
@@ -310,7 +323,14 @@ struct DevPlan {
             (void)hipEventDestroy(ready);
         }
         pool_host_release(h_stage, stage_cap);
+        if (used && hipEventQuery(used) == hipSuccess) {  // last launch done: no guard to carry
+            (void)hipEventDestroy(used);
+            used = nullptr;
+        }
+        (void)hipGetLastError();
         if (blob && !multi_stream) {
+            // a guard may outlive its stream (a drop-in context's streams die after its codecs): the
+            // pool then sees an odd query status and waits on the event before reusing the buffer
             pool_dev_release(blob, blob_cap, device, used);
             used = nullptr;
         } else if (blob) {
@@ -323,6 +343,7 @@ struct DevPlan {
         }
         if (used) (void)hipEventDestroy(used);
         (void)hipSetDevice(cur);
+        (void)hipGetLastError();  // teardown statuses are not the next launch's error
     }
 };
 
@@ -1976,6 +1997,7 @@ bool arena_release(const uint8_t* p) {
     if (uintptr_t(p) >= it->first + it->second.bytes) return false;
     if (--it->second.live == 0) {
         (void)hipHostFree(reinterpret_cast<void*>(it->first));
+        (void)hipGetLastError();
         r.blocks.erase(it);
     }
     return true;

@@ -3,7 +3,9 @@ symbol sizes with and without tail columns, stripe counts and erasure patterns, 
 path: matrix-specialised XOR kernels (jit=1), generic GF(256) kernels (jit=0), GF(2^16) codes
 (hand-scheduled kernel, split-K on small grids, device-built plans), and rsg_decode_batch with a
 pattern per stripe (device-built plans; for GF(2^16) codes, "batch16", one plan rebuilt on the stream
-per pattern). Prints one JSON line per case and a summary."""
+per pattern), the GF(2^16) syndrome route ("route": k_cs16 + k_bs16 / second stage) and the per-call
+drop-in API on seq_create arenas ("dropin"). Prints one JSON line per case and a summary.
+usage: fuzz_parity.py [seed] [seconds] [family,family,...]"""
 import json
 import os
 import sys
@@ -25,24 +27,68 @@ counts = {}
 fails = 0
 
 
+def one_dropin():
+    """Reference per-call API on library-allocated (seq_create) stripes: page-locked arenas, DMA in
+    place, zero-copy XOR-kernel launches once a plan is specialised; 4 restores of one pattern."""
+    if rng.integers(0, 2):
+        k = int(rng.integers(20, 200))
+        r = int(rng.integers(1, min(255 - k, 64) + 1))
+    else:
+        k = int(rng.integers(200, 700))
+        r = int(rng.integers(max(1, 256 - k), 200))
+    S = 2 * int(rng.integers(max(1024, (1 << 20) // (2 * (k + r))), 16384))
+    q = rs_amd.Seq(k + r, S)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    for i in range(k):
+        q.symbols[i][:] = data[i]
+    rs = rs_amd.RS()
+    want = np.zeros((k + r, S), np.uint8)
+    want[:k] = data
+    assert oracle_encode(k, r, want) == 0
+    ok = True
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    for call in range(4):
+        assert rs.generate_repair_symbols(q, r) == 0
+        ok = ok and bool(np.array_equal(np.stack(q.symbols), want))
+        for i in np.nonzero(er)[0]:
+            q.symbols[i][:] = 0
+        assert rs.restore_symbols(k, r, q, er, int(er.sum())) == 0
+        got = np.stack(q.symbols)
+        ok = ok and bool(np.array_equal(got[:k], data)) and not got[k:][er[k:]].any()
+    pitch = q.symbols[1].ctypes.data - q.symbols[0].ctypes.data if k + r > 1 else 0
+    q.close()
+    rs.close()
+    return dict(family="dropin", k=k, r=r, S=S, stripes=1, t=int(er.sum()), arena=pitch == (S + 15) // 16 * 16, ok=ok)
+
+
 def one(family):
+    if family == "dropin":
+        return one_dropin()
     if family in ("xj", "generic", "batch"):
         k = int(rng.integers(1, 200))
         r = int(rng.integers(1, min(255 - k, 80) + 1))
     elif family == "m16":
         k = int(rng.integers(200, 1500))
         r = int(rng.integers(max(1, 256 - k), 300))
+    elif family == "route":  # GF(2^16) syndrome route: K, R >= 64, whole 1 KiB column chunks
+        k = int(rng.integers(200, 1200))
+        r = int(rng.integers(max(64, 256 - k), 300))
     else:  # batch16: GF(2^16) codes, small enough for the oracle to check every stripe quickly
         k = int(rng.integers(150, 500))
         r = int(rng.integers(max(1, 256 - k), 160))
     S = int(rng.choice([2048, 4096, 8192, 1024])) + 8 * int(rng.integers(0, 64)) * int(rng.integers(0, 2))
     if family in ("m16", "batch16"):
         S = min(S, 4096 if family == "m16" else 2048)
+    if family == "route":
+        S = 1024 * int(rng.integers(1, 4))
     n = int(rng.integers(1, 5)) if family not in ("batch", "batch16") else int(rng.integers(20, 60))
+    if family == "route":
+        n = int(rng.integers(1, 3))
     host = np.zeros((n, k + r, S), np.uint8)
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
-    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "batch": dict(batch_plans=1),
+    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "route": {}, "batch": dict(batch_plans=1),
           "batch16": dict(batch_plans=1)}[family]
     codec = rs_amd.Codec(k, r, **kw)
     codec.encode(dev)
@@ -63,7 +109,8 @@ def one(family):
         assert codec.decode_batch(dev, pats) == 0
     else:
         er = np.zeros(k + r, bool)
-        er[rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+        lo = 64 if family == "route" and rng.integers(0, 2) else 1  # t >= 64: the decode route too
+        er[rng.choice(k + r, int(rng.integers(min(lo, r), r + 1)), replace=False)] = True
         pats = np.broadcast_to(er, (n, k + r))
         poisoned = got.copy()
         poisoned[:, er] = 0
@@ -80,7 +127,8 @@ def one(family):
     return dict(family=family, k=k, r=r, S=S, stripes=n, encode=enc_kernel, decode=dec_kernel, ok=ok)
 
 
-families = ["xj", "generic", "m16", "batch", "batch16"]
+families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "batch", "batch16",
+                                                             "dropin"]
 i = 0
 while time.time() < t_end:
     fam = families[i % len(families)]
