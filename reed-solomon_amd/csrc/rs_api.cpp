@@ -276,6 +276,11 @@ struct DevPlan {
     };
     std::unique_ptr<Cs> cs;
     std::unique_ptr<DevPlan> second, dense;
+    // decode plans of route-eligible GF(2^16) patterns start dense: `route` is built once route_bytes
+    // (bytes moved by this plan's launches) reaches the codec's route_min_bytes
+    bool route_ok = false;
+    uint64_t route_bytes = 0;
+    std::unique_ptr<DevPlan> route;
     std::vector<uint8_t> erased;  // the pattern (empty: encode), to build `dense`
     int64_t uses = 0;                // launches of this plan (JIT policy)
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
@@ -560,6 +565,10 @@ struct rsg_codec {
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
     int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
+    // a decode pattern starts on the dense device-built plan and moves to the syndrome route once its
+    // launches have moved this many bytes ((K + R) * S per stripe): the route's host build (~16 ms at
+    // C5) pays only over a few hundred stripes; 0 = route at once (option m16_route_min_bytes)
+    int64_t route_min_bytes = int64_t(1) << 30;
     // wave-instructions issued by the hand-scheduled GF(2^16) kernels of the last rsg_encode / rsg_decode
     // (their generated steps' VALU / SALU counts times the steps run; rsg_last_work)
     uint64_t work_valu = 0, work_salu = 0;
@@ -943,7 +952,13 @@ static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan
     std::vector<int32_t> in, outs;
     codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
     const int K = int(in.size()), R = int(outs.size());
-    if (cs_route_eligible(c, K, R, int(targets.size()))) return make_plan_cs(c, erased, out, st);
+    if (cs_route_eligible(c, K, R, int(targets.size()))) {
+        if (!erased || c->route_min_bytes == 0) return make_plan_cs(c, erased, out, st);
+        if (int rc = make_plan_dense(c, erased, out, st)) return rc;
+        out->route_ok = true;
+        out->erased.assign(erased, erased + size_t(c->k) + c->r);
+        return 0;
+    }
     return make_plan_dense(c, erased, out, st);
 }
 
@@ -1063,6 +1078,13 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "m16_route_min_bytes")) {
+        if (value < 0) return RS_ERR_INVALID;
+        c->route_min_bytes = value;
+        c->dec.clear();
+        c->dec_lru.clear();
+        return 0;
+    }
     if (!std::strcmp(name, "syn_route")) {
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->syn_route = int(value);
@@ -1172,6 +1194,23 @@ static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t
                          uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
                          hipStream_t st, const int32_t* d_ids, bool dst_local) {
     if (int rc = p.order_after_build(st)) return rc;
+    if (p.route_ok && !d_ids && !dst_local && S % 1024 == 0 && int64_t(S) < (int64_t(1) << 31)) {
+        int64_t max_in = 0;  // the route's 31-bit offsets (run_plan_body's p.cs branch)
+        for (int32_t v : p.in_slots) max_in = std::max<int64_t>(max_in, v);
+        const int64_t D = int64_t(std::count(p.erased.begin(), p.erased.end(), uint8_t(1)));
+        const bool fits = max_in * src_sym + int64_t(S) < (int64_t(1) << 31) && D * int64_t(S) < (int64_t(1) << 31);
+        if (fits && !p.route) {
+            p.route_bytes += n_stripes * uint64_t(p.K + p.R) * S;
+            if (p.route_bytes >= uint64_t(c->route_min_bytes)) {
+                std::unique_ptr<bool[]> er(new bool[p.erased.size()]);
+                for (size_t i = 0; i < p.erased.size(); ++i) er[i] = p.erased[i] != 0;
+                if (int rc = make_plan_cs(c, er.get(), p.route, st)) return rc;
+            }
+        }
+        if (fits && p.route)
+            return run_plan(c, *p.route, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st, d_ids,
+                            dst_local);
+    }
     if (p.cs) {
         HIP_TRY(hipSetDevice(c->device));
         // both stages index their inputs with 31-bit byte offsets (the second stage reads D syndrome rows)

@@ -91,6 +91,8 @@ def one(family):
     kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "route": {}, "batch": dict(batch_plans=1),
           "batch16": dict(batch_plans=1)}[family]
     codec = rs_amd.Codec(k, r, **kw)
+    if family == "route":
+        codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route at once
     codec.encode(dev)
     torch.cuda.synchronize()
     enc_kernel = codec.last_kernel

@@ -538,6 +538,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r)
     codec.set_option("m16_route", route)
+    codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route from their first launch
     assert codec.subfield == 16
     codec.encode(dev)
     torch.cuda.synchronize()
@@ -561,6 +562,38 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
         ref = poisoned[s].copy()
         assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
         assert np.array_equal(out[s], ref)
+
+
+def test_m16_decode_moves_to_route():
+    """A GF(2^16) decode pattern starts on the dense device-built plan and moves to the syndrome route
+    once its launches have moved m16_route_min_bytes: the first launch runs k_apply_m16_v1, the second
+    k_cs16 + its second stage; both bit-exact vs the oracle."""
+    k, r, S, n = 600, 100, 2048, 2
+    rng = np.random.default_rng(77)
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route_min_bytes", int(1.5 * n * (k + r) * S))
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k, 80, replace=False)] = True
+    er[k + 3] = True
+    poisoned = got.copy()
+    poisoned[:, er] = 0
+    want = poisoned.copy()
+    for s in range(n):
+        assert oracle_decode(k, r, want[s], er, int(er.sum())) == 0
+    kernels = []
+    for call in range(3):
+        dev.copy_(torch.from_numpy(poisoned))
+        codec.decode(dev, er)
+        torch.cuda.synchronize()
+        kernels.append(codec.last_kernel)
+        assert np.array_equal(dev.cpu().numpy(), want), f"call {call} ({codec.last_kernel})"
+    assert kernels[0] == "apply_m16_v1" and kernels[1].startswith("cs16+") and kernels[2] == kernels[1], kernels
 
 
 def test_drop_in_m16_large_symbols():
