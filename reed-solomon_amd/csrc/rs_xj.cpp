@@ -152,6 +152,8 @@ struct XjConfig {
     int kreg = 1;      // finish step constants: 1 = in VGPRs (4-byte VOP2 forms), 0 = literals
     int lfin = 0;      // finish: 0 = VALU Horner over z (above); 1 = Horner in gamma through a 128 KiB LDS
                        // table T[w] = gamma * w (persistent kernel, one workgroup per CU)
+    int xcd = 0;       // 1: workgroup -> column remap so each XCD walks contiguous 1/8 spans of every stripe
+                       // (dispatch puts workgroup i on XCD i % 8); 0: consecutive columns round-robin
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
@@ -169,6 +171,7 @@ struct XjConfig {
         env("RS_XJ_FIN", lfin);
         env("RS_XJ_SHARE", share);
         env("RS_XJ_KREG", kreg);
+        env("RS_XJ_XCD", xcd);
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
@@ -192,7 +195,7 @@ struct XjConfig {
         char b[128];
         std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
-        return b;
+        return xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
     }
 };
 
@@ -714,9 +717,12 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
         o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds["
           << (C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
-          << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
-             "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n"
-             "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
+          << (C.xcd ? "  const uint32_t xl = blockIdx.x + blockIdx.y * gridDim.x, xw = gridDim.x >> 3, xk = xl >> 3;\n"
+                      "  const uint32_t by = xk / xw, bx = (xl & 7u) * xw + xk % xw;\n"
+                    : "  const uint32_t bx = blockIdx.x, by = blockIdx.y;\n")
+          << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[by] : (uint64_t)by;\n"
+             "  const uint64_t dstripe = a.dst_local ? (uint64_t)by : stripe;\n"
+             "  const uint32_t col = bx * 256u + (threadIdx.x & 63u) * 4u;\n"
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
              "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
           << (C.share ? 0 : C.lds * 2048) << "u;\n"
