@@ -232,3 +232,17 @@ def test_header_layouts_match_reference(tmp_path):
         subprocess.check_call(["gcc", "-std=c11", "-w", f"-I{inc}", "-o", str(exe), str(src)])
         outs.append(subprocess.check_output([str(exe)], text=True))
     assert outs[0] == outs[1], outs
+
+
+def test_seq_create_without_gpu_falls_back_to_heap():
+    """seq_create of a large sequence tries a page-locked arena; with no GPU (this container) it falls
+    back to zeroed heap symbols, and seq_destroy / symbol_destroy free either kind."""
+    q = rs_amd.Seq(160, 65536 + 2)
+    assert all(s.size == 65538 and not s.any() for s in q.symbols)
+    q.symbols[3][:] = 7
+    v = q.view(128, 32)
+    assert v.length == 32 and v.symbol_size == 65538
+    q.close()
+    small = rs_amd.Seq(4, 16)  # below the arena threshold: always heap
+    assert len(small.symbols) == 4
+    small.close()
