@@ -2303,20 +2303,6 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
         HIP_TRY(hipEventSynchronize(im.ev[0]));
         return 0;
     }
-    // a GF(256) pattern not specialised yet (its first calls): the codec's pattern-independent syndrome
-    // kernel streams the arena across PCIe into device scratch, then the pattern's t-input solve is
-    // built and applied on the device (rsg_decode_batch's syndrome route), writing the restored rows
-    // back across PCIe -- instead of the generic kernel over the whole stripe, whose few workgroups
-    // leave the chip idle. The call still counts toward the pattern's specialisation.
-    if (sb && sdev && im.arena_zc && pending && dplan->uses + 1 < c->dec_jit_uses && S % 2048 == 0 &&
-        syn_prepare(c, S, int64_t(sp))) {
-        rc = decode_batch_device_plans(c, sdev, int64_t(n * sp), int64_t(sp), 1, S, is_erased, im.stream);
-        if (rc) return rc;
-        if (uint64_t(dplan->K + dplan->R) * S >= kJitMinBytes) ++dplan->uses;
-        HIP_TRY(hipEventRecord(im.ev[0], im.stream));
-        HIP_TRY(hipEventSynchronize(im.ev[0]));
-        return 0;
-    }
     // a stripe in a page-locked arena (seq_create) is copied in place: all n rows in by one 2D DMA
     // (erased rows ride along unread), restored rows out by DMA of their span or, when scattered,
     // written across PCIe by k_put_rows straight into the arena
