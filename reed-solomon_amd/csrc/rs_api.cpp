@@ -1984,46 +1984,103 @@ inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
 // instead of H2D DMA + launch + D2H DMA and their stream hand-offs. Kernels that re-read inputs per
 // output tile (m = 16 tiles, the syndrome route) stay on the DMA path.
 bool streams_once(const DevPlan& p, size_t S) { return p.m == 8 && p.xj && !p.xj_failed && S >= 2048; }
+// Stripes up to this many bytes are latency-bound on any path: every kernel runs on them across PCIe
+// (one launch, no copies), whatever its re-reads.
+constexpr uint64_t kZcSmallBytes = uint64_t(1) << 20;
 
-// Page-locked symbol arenas. seq_create of a sequence of at least kArenaMin bytes places its symbols
-// in one hipHostMalloc block at stride pad16(S), so rs_generate_repair_symbols / rs_restore_symbols
-// DMA straight between the caller's symbols and HBM (no host gather / scatter, no staging copy). The
+// Page-locked symbol arenas. seq_create places a sequence's symbols in one page-locked block at stride
+// pad16(S) (its own hipHostMalloc block from kArenaMin bytes on, a share of a slab below), so
+// rs_generate_repair_symbols / rs_restore_symbols run kernels on the caller's symbols across PCIe or
+// DMA straight between them and HBM (no host gather / scatter, no staging copy). The
 // registry maps a block's start to its size, device-visible address and live symbol count;
 // symbol_destroy returns a block when its last symbol goes. RS_AMD_PINNED_SEQ=0 turns it off (plain
 // calloc per symbol, as before).
 constexpr size_t kArenaMin = size_t(1) << 20;
+// Smaller sequences share page-locked slabs (bump-allocated, 256-byte aligned): pinning memory per
+// small sequence would cost more than the call it serves. A slab's space is reused once every
+// sequence in it is destroyed; past kMaxSlabs slabs small sequences go to the heap.
+constexpr size_t kSlabBytes = size_t(8) << 20;
+constexpr size_t kMaxSlabs = 64;
+struct Slab {
+    uint8_t* base;
+    uint8_t* dev;
+    size_t used = 0, live = 0;
+};
 struct Arena {
     size_t bytes;
     uint8_t* dev;  // device-visible address of the block start (nullptr: DMA only)
     size_t live;
+    Slab* slab = nullptr;  // the slab the block lives in (nullptr: its own hipHostMalloc block)
 };
 struct ArenaRegistry {
     std::mutex mu;
     std::map<uintptr_t, Arena> blocks;
+    std::vector<Slab*> slabs;
+    bool no_pinning = false;  // page-locked allocation failed once (no GPU): heap from then on
 };
 ArenaRegistry& arenas() {
     static ArenaRegistry* r = new ArenaRegistry;  // never destroyed: symbols may outlive static destructors
     return *r;
 }
 
-uint8_t* arena_alloc(size_t length, size_t P) {
-    const char* e = std::getenv("RS_AMD_PINNED_SEQ");
-    if ((e && e[0] == '0') || length * P < kArenaMin) return nullptr;
+// a zeroed, mapped page-locked block and its device-visible address (nullptr if none)
+static uint8_t* pinned_block(size_t bytes, uint8_t** dev) {
     void* h = nullptr;
-    if (hipHostMalloc(&h, length * P, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc(&h, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    std::memset(h, 0, length * P);
+    std::memset(h, 0, bytes);
     void* dv = nullptr;
     if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess) {
         (void)hipGetLastError();
         dv = nullptr;
     }
+    *dev = static_cast<uint8_t*>(dv);
+    return static_cast<uint8_t*>(h);
+}
+
+uint8_t* arena_alloc(size_t length, size_t P) {
+    const char* e = std::getenv("RS_AMD_PINNED_SEQ");
+    const size_t bytes = length * P;
+    if ((e && e[0] == '0') || bytes == 0) return nullptr;
     ArenaRegistry& r = arenas();
     std::lock_guard<std::mutex> lk(r.mu);
-    r.blocks[uintptr_t(h)] = Arena{length * P, static_cast<uint8_t*>(dv), length};
-    return static_cast<uint8_t*>(h);
+    if (r.no_pinning) return nullptr;
+    if (bytes >= kArenaMin) {
+        uint8_t* dv = nullptr;
+        uint8_t* h = pinned_block(bytes, &dv);
+        if (!h) {
+            r.no_pinning = true;
+            return nullptr;
+        }
+        r.blocks[uintptr_t(h)] = Arena{bytes, dv, length};
+        return h;
+    }
+    const size_t need = (bytes + 255) & ~size_t(255);
+    Slab* sl = nullptr;
+    for (Slab* x : r.slabs)
+        if (x->used + need <= kSlabBytes) {
+            sl = x;
+            break;
+        }
+    if (!sl) {
+        if (r.slabs.size() >= kMaxSlabs) return nullptr;
+        uint8_t* dv = nullptr;
+        uint8_t* h = pinned_block(kSlabBytes, &dv);
+        if (!h) {
+            r.no_pinning = true;
+            return nullptr;
+        }
+        sl = new Slab{h, dv};
+        r.slabs.push_back(sl);
+    }
+    uint8_t* blk = sl->base + sl->used;
+    std::memset(blk, 0, need);  // a reused slab holds old data
+    r.blocks[uintptr_t(blk)] = Arena{bytes, sl->dev ? sl->dev + sl->used : nullptr, length, sl};
+    sl->used += need;
+    ++sl->live;
+    return blk;
 }
 
 // true (and the block released when it was the last) when p lies in an arena
@@ -2035,8 +2092,12 @@ bool arena_release(const uint8_t* p) {
     --it;
     if (uintptr_t(p) >= it->first + it->second.bytes) return false;
     if (--it->second.live == 0) {
-        (void)hipHostFree(reinterpret_cast<void*>(it->first));
-        (void)hipGetLastError();
+        if (Slab* sl = it->second.slab) {
+            if (--sl->live == 0) sl->used = 0;  // every sequence of the slab is gone: reuse its space
+        } else {
+            (void)hipHostFree(reinterpret_cast<void*>(it->first));
+            (void)hipGetLastError();
+        }
         r.blocks.erase(it);
     }
     return true;
@@ -2214,7 +2275,7 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
     uint8_t* rb = const_cast<uint8_t*>(arena_run(rep->symbols, r, S, &rp, &rdev));
     const size_t P = pad16(S), n = size_t(k) + r, W = chunk_width(S, ib ? im.arena_chunks : kMaxChunks),
                  nch = (S + W - 1) / W;
-    if (ib && rb && idev && rdev && im.arena_zc && streams_once(*c->enc, S)) {
+    if (ib && rb && idev && rdev && im.arena_zc && (streams_once(*c->enc, S) || uint64_t(n) * S <= kZcSmallBytes)) {
         rc = rsg_encode(c, idev, int64_t(n * ip), int64_t(ip), rdev, int64_t(n * rp), int64_t(rp), 1, int64_t(S),
                         im.stream);
         if (rc) return rc;
@@ -2296,7 +2357,7 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     size_t sp = 0;
     uint8_t* sdev = nullptr;
     uint8_t* sb = const_cast<uint8_t*>(arena_run(rcv->symbols, n, S, &sp, &sdev));
-    if (sb && sdev && im.arena_zc && streams_once(*dplan, S)) {  // in place across PCIe, one launch
+    if (sb && sdev && im.arena_zc && (streams_once(*dplan, S) || uint64_t(n) * S <= kZcSmallBytes)) {  // in place, one launch
         rc = rsg_decode(c, sdev, n * sp, sp, 1, S, is_erased, t, im.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(im.ev[0], im.stream));
@@ -2427,7 +2488,7 @@ extern "C" symbol_seq_t* seq_create(size_t length, size_t symbol_size) {
         std::free(q);
         return nullptr;
     }
-    // large sequences: one zeroed page-locked arena at stride pad16(S) (see arena_alloc)
+    // one zeroed page-locked block (or a slab share for small sequences) at stride pad16(S), see arena_alloc
     const size_t P = pad16(symbol_size ? symbol_size : 1);
     if (uint8_t* blk = symbol_size ? arena_alloc(length, P) : nullptr) {
         bool ok = true;

@@ -7,7 +7,7 @@ export PYTHONPATH=$PWD/reed-solomon_amd:$PWD/tests
 timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread \
     -k "drop_in or dropin" > gpurun_out/dropin_tests.log 2>&1 || { tail -30 gpurun_out/dropin_tests.log; exit 1; }
 tail -2 gpurun_out/dropin_tests.log
-for shape in "128 32 65536 32" "4096 1024 4096 8"; do
+for shape in "128 32 65536 32" "4096 1024 4096 8" "4 2 256 512" "10 4 4096 512"; do
     timeout -k 10 120 ./scripts/bench_dropin $shape | tee -a gpurun_out/dropin_bench.log || exit 1
     RS_AMD_PINNED_SEQ=0 timeout -k 10 120 ./scripts/bench_dropin $shape | tee -a gpurun_out/dropin_bench.log || exit 1
 done

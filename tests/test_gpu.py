@@ -625,13 +625,17 @@ def test_drop_in_m16_large_symbols():
 
 @pytest.mark.parametrize("k,r,S,pattern", [(128, 32, 65536, "bench"), (128, 32, 65536, "span"),
                                            (128, 32, 65536, "random"), (300, 64, 8192 + 6, "random"),
-                                           (64, 16, 16384 + 2, "bench")])
+                                           (64, 16, 16384 + 2, "bench"), (4, 2, 256, "random"),
+                                           (10, 4, 4096, "bench"), (200, 55, 66, "random"),
+                                           (300, 64, 64, "random")])
 def test_drop_in_pinned_seq(k, r, S, pattern):
-    """seq_create places large sequences in a page-locked arena and the per-call API copies them in
-    place (2D DMA in; restored rows out by DMA of their span or by k_put_rows across PCIe): encode and
-    restore bit-exact vs the oracle, for scattered (bench, random) and contiguous (span) erasures,
-    GF(256) and GF(2^16) codes, symbol sizes that are not multiples of 16 (padded arena pitch); the
-    same calls on pageable symbols (RS_AMD_PINNED_SEQ=0 -> calloc per symbol) give the same bytes."""
+    """seq_create places sequences in page-locked memory (own block from 1 MiB, slab share below) and
+    the per-call API works on them in place: zero-copy launches (specialised XOR kernels; any kernel on
+    stripes up to 1 MiB), else 2D DMA in and restored rows out by DMA of their span or k_put_rows.
+    Encode and restore bit-exact vs the oracle for scattered (bench, random) and contiguous (span)
+    erasures, GF(16) / GF(256) / GF(2^16) codes, symbol sizes that are not multiples of 16 (padded
+    pitch); the same calls on pageable symbols (RS_AMD_PINNED_SEQ=0 -> calloc per symbol) give the same
+    bytes."""
     import os
     rng = np.random.default_rng(k * 7 + S)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
