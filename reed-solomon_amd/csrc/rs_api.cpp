@@ -1285,9 +1285,10 @@ static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
-    if (p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) {  // split-K scratch for small m = 16 grids
+    const bool m8_generic = p.m == 8 && p.d_idx && a.mode == 18 && !(xj_ok && p.xj) && !(jit_ok && p.jit);
+    if ((p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) || m8_generic) {  // split-K scratch for small grids
         int64_t need = 0;
-        if (m16_kslices(a, int64_t(n_stripes), &need) > 1) {
+        if ((m8_generic ? m8_kslices(a, int64_t(n_stripes), &need) : m16_kslices(a, int64_t(n_stripes), &need)) > 1) {
             if (int rc = scratch_acquire(c, st)) return rc;
             if (int rc = grow(&c->d_partial, c->partial_cap, size_t(need))) return rc;
             a.scratch = static_cast<uint32_t*>(c->d_partial);

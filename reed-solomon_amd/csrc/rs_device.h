@@ -133,6 +133,16 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     const int32_t* in_idx = a.in_idx;
     const int32_t* out_idx = a.out_idx;
     const uint32_t* idxb = a.idx;
+    // split-K (small grids, one plan for all stripes): this workgroup takes inputs [i0, i0 + K) of the
+    // list and leaves its partial outputs for k_xor_slices
+    const int slice = blockIdx.z;
+    const int kfull = a.K;
+    int i0 = 0;
+    if (a.kslices > 1 && !a.ps_kr) {
+        i0 = int(int64_t(a.K) * slice / a.kslices);
+        K = int(int64_t(a.K) * (slice + 1) / a.kslices) - i0;
+        in_idx += i0;
+    }
     if (a.ps_kr) {  // this stripe's own plan
         K = sload(a.ps_kr + 2 * local);
         R = sload(a.ps_kr + 2 * local + 1);
@@ -177,13 +187,21 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 4 * b + j;
-            if (i < K) step(y[j], i, tile, a0, a1, idxb + (size_t(tile) * K + i) * 64);
+            if (i < K) step(y[j], i, tile, a0, a1, idxb + (size_t(tile) * (a.ps_kr ? K : kfull) + i0 + i) * 64);
         }
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
     }
-    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
     const int rows = min(32, R - tile * 32);
+    if (a.kslices > 1 && !a.ps_kr) {  // partial products (L^-1 is GF(2)-linear: XOR of converted partials)
+        const int64_t nloc = gridDim.x / a.nchunks, rpad = int64_t(gridDim.y) * 32, cw = a.nchunks * 256;
+        uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 32) * cw + (chunk0 >> 2) + threadIdx.x;
+#pragma unroll
+        for (int p = 0; p < 32; ++p)
+            if (p < rows) part[p * cw] = lds_lookup4(lt + 1024, p < 16 ? a0[p & 15] : a1[p & 15]);
+        return;
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
 #pragma unroll
     for (int p = 0; p < 32; ++p) {
         if (p < rows) {

@@ -924,14 +924,21 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
         if (a.mode == 18 || a.mode == 19) {  // V = 1 kernel (19: without gpr-index mode, timing only)
             const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
             if (full > 0) {
-                const V1Args v = v1_args(a, full, nullptr);
-                dim3 g(unsigned(n_stripes * full), grid.y);
+                V1Args v = v1_args(a, full, nullptr);
+                v.kslices = a.mode == 18 ? m8_kslices(a, n_stripes, nullptr) : 1;
+                v.partial = a.scratch;
+                dim3 g(unsigned(n_stripes * full), grid.y, unsigned(v.kslices));
 #ifdef RS_AMD_DIAG
                 if (a.mode == 19)
                     hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
                 else
 #endif
                     hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
+                if (v.kslices > 1) {
+                    const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
+                    hipLaunchKernelGGL(k_xor_slices, dim3(unsigned((rows + 255) / 256), unsigned(n_stripes)), dim3(256),
+                                       0, st, v, int64_t(n_stripes), int64_t(grid.y) * 32, cw);
+                }
             }
             launch_m8_tail(a, n_stripes, grid.y, st);
         } else if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15) || a.mode == 17) {
@@ -1036,6 +1043,21 @@ int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes) {
     if (blocks <= 0 || blocks >= 256) return 1;
     int64_t s = std::min<int64_t>({(16 * cap + blocks - 1) / blocks, int64_t(a.K) / 64, cap});
     const int64_t per = n_stripes * tiles * 64 * full * 1024;  // partial bytes per slice
+    if (!scratch_bytes) s = std::min<int64_t>(s, per > 0 ? a.scratch_bytes / per : 0);
+    if (s < 2) return 1;
+    if (scratch_bytes) *scratch_bytes = s * per;
+    return int(s);
+}
+
+int m8_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes) {
+    // the generic V = 1 kernel on small grids (e.g. one 64 KiB stripe of a per-call decode before its
+    // pattern is specialised: 64 workgroups each walking all K inputs): up to 16 input slices of >= 16
+    // inputs, aiming for >= 512 workgroups, within the scratch
+    const int64_t full = (a.nbytes / 2048) * 2, tiles = (a.R + 31) / 32;
+    const int64_t blocks = n_stripes * full * tiles;
+    if (blocks <= 0 || blocks >= 256 || a.ids) return 1;
+    int64_t s = std::min<int64_t>({(512 + blocks - 1) / blocks, int64_t(a.K) / 16, 16});
+    const int64_t per = n_stripes * tiles * 32 * full * 1024;  // partial bytes per slice
     if (!scratch_bytes) s = std::min<int64_t>(s, per > 0 ? a.scratch_bytes / per : 0);
     if (s < 2) return 1;
     if (scratch_bytes) *scratch_bytes = s * per;

@@ -34,6 +34,8 @@ struct ApplyArgs {
 };
 // input slices of the split-K m = 16 launch over n_stripes (1 = no split) and the scratch it needs
 int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes);
+// the same for the generic GF(256) V = 1 kernel (m8 mode 18, 32-row tiles)
+int m8_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes);
 
 // Per-stripe decode plans (k_plan_m8): one per selected stripe, from its erasure mask.
 struct PlanArgs {
