@@ -1979,12 +1979,15 @@ constexpr int kMaxChunks = 4;
 
 inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
 
-// Zero-copy eligibility of a per-call launch on arena-resident symbols: the plan runs as the
-// bit-plane XOR kernel (already specialised), which reads each input column once and writes each
-// output once, so it can stream the caller's page-locked symbols across PCIe itself -- one launch
-// instead of H2D DMA + launch + D2H DMA and their stream hand-offs. Kernels that re-read inputs per
-// output tile (m = 16 tiles, the syndrome route) stay on the DMA path.
-bool streams_once(const DevPlan& p, size_t S) { return p.m == 8 && p.xj && !p.xj_failed && S >= 2048; }
+// Zero-copy eligibility of a per-call launch on arena-resident symbols: the plan's kernel reads each
+// input column once and writes each output once -- the bit-plane XOR kernel, or any GF(256) kernel
+// with a single 32-row tile (R <= 32; the generic one splits K on small grids) -- so it can stream the
+// caller's page-locked symbols across PCIe itself: one launch instead of H2D DMA + launch + D2H DMA and
+// their stream hand-offs. Kernels that re-read inputs per output tile (m = 16 tiles, the syndrome
+// route) stay on the DMA path.
+bool streams_once(const DevPlan& p, size_t S) {
+    return p.m == 8 && ((p.xj && !p.xj_failed && S >= 2048) || p.R <= 32);
+}
 // Stripes up to this many bytes are latency-bound on any path: every kernel runs on them across PCIe
 // (one launch, no copies), whatever its re-reads.
 constexpr uint64_t kZcSmallBytes = uint64_t(1) << 20;

@@ -39,7 +39,8 @@ def one_dropin():
     if rng.integers(0, 2):  # slab-allocated small stripe: zero-copy launches of any kernel
         S = 2 * int(rng.integers(1, max(2, (1 << 19) // (k + r))))
     else:
-        S = 2 * int(rng.integers(max(1024, (1 << 20) // (2 * (k + r))), 16384))
+        lo = max(1024, (1 << 20) // (2 * (k + r)))
+        S = 2 * int(rng.integers(lo, max(16384, lo + 1024)))
     q = rs_amd.Seq(k + r, S)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
     for i in range(k):
