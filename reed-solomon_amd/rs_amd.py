@@ -11,7 +11,9 @@ Two layers, both thin wrappers over the C ABI (include/rs/reed_solomon.h, includ
 There is no CPU fallback: if librs_amd.so is missing this module raises on import, and a codec
 cannot be created without a GPU.
 """
+import atexit
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -204,15 +206,28 @@ class _SeqBuf:
         self.seq = SymbolSeqT(len(arrays), symbol_size, self.ptrs)
 
 
+_live_seqs = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_seqs():
+    # page-locked sequences must be released while the HIP runtime is still up (before its static
+    # destructors run at process exit), not whenever the garbage collector reaches them
+    for q in list(_live_seqs):
+        q.close()
+
+
 class Seq:
-    """A library-allocated symbol_seq_t (seq_create, reference include/memory/seq.h). Sequences of
-    1 MiB and more live in one page-locked arena, which rs_generate_repair_symbols /
-    rs_restore_symbols copy in place by DMA. symbols[i] is a numpy view of symbol i."""
+    """A library-allocated symbol_seq_t (seq_create, reference include/memory/seq.h). The symbols
+    live in page-locked memory (own block from 1 MiB, slab share below), which
+    rs_generate_repair_symbols / rs_restore_symbols use in place (zero-copy launches or DMA).
+    symbols[i] is a numpy view of symbol i."""
 
     def __init__(self, length, symbol_size):
         self._p = _lib.seq_create(length, symbol_size)
         if not self._p:
             raise MemoryError("seq_create")
+        _live_seqs.add(self)
         self.length, self.symbol_size = length, symbol_size
         q = self._p.contents
         self.symbols = [np.ctypeslib.as_array(q.symbols[i].contents.data, (symbol_size,)) for i in range(length)]

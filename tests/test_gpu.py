@@ -596,6 +596,53 @@ def test_m16_decode_moves_to_route():
     assert kernels[0] == "apply_m16_v1" and kernels[1].startswith("cs16+") and kernels[2] == kernels[1], kernels
 
 
+def test_drop_in_arena_mixed_layouts():
+    """Per-call calls on seq_create memory in layouts other than one strided sequence: information and
+    repair symbols in two different sequences (zero-copy with two bases), and a sequence whose symbol
+    pointers were permuted (no longer one strided run: the gather / scatter path for that side) --
+    bit-exact vs the oracle."""
+    k, r, S = 128, 32, 65536
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    want = np.zeros((k + r, S), np.uint8)
+    want[:k] = data
+    assert oracle_encode(k, r, want) == 0
+    rs = rs_amd.RS()
+    qa, qb = rs_amd.Seq(k, S), rs_amd.Seq(r, S)
+    for i in range(k):
+        qa.symbols[i][:] = data[i]
+    for call in range(3):  # first call: DMA; then the specialised XOR kernel zero-copy
+        va, vb = qa.view(0, k), qb.view(0, r)
+        assert rs_amd._lib.rs_generate_repair_symbols(rs._h, ctypes.byref(va), ctypes.byref(vb)) == 0
+        assert np.array_equal(np.stack(qb.symbols), want[k:]), f"two sequences, call {call}"
+    qa.close()
+    qb.close()
+    q = rs_amd.Seq(k + r, S)
+    for i in range(k):
+        q.symbols[i][:] = data[i]
+    ptrs = q._p.contents.symbols
+    sym_p = ctypes.POINTER(rs_amd.SymbolT)
+    a0, a1 = (ctypes.cast(ptrs[i], ctypes.c_void_p).value for i in (0, 1))  # addresses, not views of the slots
+    ptrs[0], ptrs[1] = ctypes.cast(a1, sym_p), ctypes.cast(a0, sym_p)  # logical symbol 0 = second block row
+    ref = np.zeros_like(want)
+    ref[:k] = want[:k]
+    ref[[0, 1]] = ref[[1, 0]]
+    assert oracle_encode(k, r, ref) == 0
+    er = rs_amd.bench_pattern(k, r)
+    for call in range(4):
+        assert rs.generate_repair_symbols(q, r) == 0
+        got = np.stack([np.ctypeslib.as_array(ptrs[i].contents.data, (S,)) for i in range(k + r)])
+        assert np.array_equal(got, ref), f"permuted, encode call {call}"
+        for i in np.nonzero(er)[0]:
+            np.ctypeslib.as_array(ptrs[i].contents.data, (S,))[:] = 0
+        assert rs.restore_symbols(k, r, q, er, int(er.sum())) == 0
+        got = np.stack([np.ctypeslib.as_array(ptrs[i].contents.data, (S,)) for i in range(k + r)])
+        assert np.array_equal(got[:k], ref[:k]), f"permuted, restore call {call}"
+    ptrs[0], ptrs[1] = ctypes.cast(a0, sym_p), ctypes.cast(a1, sym_p)
+    q.close()
+    rs.close()
+
+
 def test_drop_in_m16_large_symbols():
     """Reference per-call API on a GF(2^16) code with 64 KiB symbols: the call is pipelined in column
     chunks on one stream and each chunk's small grid runs split-K; encode + restore bit-exact vs the
