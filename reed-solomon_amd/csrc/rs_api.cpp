@@ -2004,7 +2004,7 @@ constexpr size_t kArenaMin = size_t(1) << 20;
 // small sequence would cost more than the call it serves. A slab's space is reused once every
 // sequence in it is destroyed; past kMaxSlabs slabs small sequences go to the heap.
 constexpr size_t kSlabBytes = size_t(8) << 20;
-constexpr size_t kMaxSlabs = 64;
+constexpr size_t kMaxSlabs = 16;  // at most 128 MiB of page-locked slabs
 struct Slab {
     uint8_t* base;
     uint8_t* dev;

@@ -674,7 +674,7 @@ def test_drop_in_m16_large_symbols():
                                            (128, 32, 65536, "random"), (300, 64, 8192 + 6, "random"),
                                            (64, 16, 16384 + 2, "bench"), (4, 2, 256, "random"),
                                            (10, 4, 4096, "bench"), (200, 55, 66, "random"),
-                                           (300, 64, 64, "random")])
+                                           (300, 64, 64, "random"), (300, 70, 1024, "random")])
 def test_drop_in_pinned_seq(k, r, S, pattern):
     """seq_create places sequences in page-locked memory (own block from 1 MiB, slab share below) and
     the per-call API works on them in place: zero-copy launches (specialised XOR kernels; any kernel on
