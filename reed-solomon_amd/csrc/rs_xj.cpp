@@ -172,6 +172,7 @@ struct XjConfig {
         env("RS_XJ_SHARE", share);
         env("RS_XJ_KREG", kreg);
         env("RS_XJ_XCD", xcd);
+
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
         lds = lds ? std::max(2, std::min(8, lds)) : 0;
@@ -719,10 +720,13 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
           << (C.xcd ? "  const uint32_t xl = blockIdx.x + blockIdx.y * gridDim.x, xw = gridDim.x >> 3, xk = xl >> 3;\n"
                       "  const uint32_t by = xk / xw, bx = (xl & 7u) * xw + xk % xw;\n"
-                    : "  const uint32_t bx = blockIdx.x, by = blockIdx.y;\n")
-          << "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[by] : (uint64_t)by;\n"
-             "  const uint64_t dstripe = a.dst_local ? (uint64_t)by : stripe;\n"
-             "  const uint32_t col = bx * 256u + (threadIdx.x & 63u) * 4u;\n"
+                      "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[by] : (uint64_t)by;\n"
+                      "  const uint64_t dstripe = a.dst_local ? (uint64_t)by : stripe;\n"
+                      "  const uint32_t col = bx * 256u + (threadIdx.x & 63u) * 4u;\n"
+                    : "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
+                      "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n"
+                      "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n")
+          << ""
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
              "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
           << (C.share ? 0 : C.lds * 2048) << "u;\n"
