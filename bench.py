@@ -332,7 +332,7 @@ def main():
         print(f"bench.py: WORLD_SIZE {world} exceeds the {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
         sys.exit(2)
     import rs_amd  # raises if librs_amd.so is missing: no fallback
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:  # launched as ranks (torchrun or --gpus N): RCCL process group, even at N=1
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -439,7 +439,7 @@ def main():
         line["scatter"] = scatter
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     if "MISMATCH" in parity:
         sys.exit(1)
