@@ -24,7 +24,12 @@ typedef struct {
     symbol_t** symbols;
 } symbol_seq_t;
 
-/* reference seq.h:45 -- `length` zero-filled symbols, NULL on allocation failure */
+/* reference seq.h:45 -- `length` zero-filled symbols, NULL on allocation failure.
+ * With a GPU present the symbols' data are page-locked, one block per sequence at a stride of
+ * symbol_size rounded up to 16 bytes (own block from 1 MiB, a shared slab below), so
+ * rs_generate_repair_symbols / rs_restore_symbols work on them in place (zero-copy kernels or DMA).
+ * Free them only through symbol_destroy / seq_destroy (as the reference's callers do). The
+ * environment variable RS_AMD_PINNED_SEQ=0 restores one heap allocation per symbol. */
 symbol_seq_t* seq_create(size_t length, size_t symbol_size);
 /* reference seq.h:52 */
 void seq_destroy(symbol_seq_t* seq);
