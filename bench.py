@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--r", type=int, default=32)
     ap.add_argument("--symbol", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=8192, help="stripes per GPU")
+    ap.add_argument("--t", type=int, default=0,
+                    help="decode erasures (information symbols at i * (k // t)); 0 = r, the bench pattern")
     ap.add_argument("--kernel", default="auto", choices=["auto", "jit", "v1jit", "v1", "idx", "table", "mask", "m16c"],
                     help="auto = library default policy (matrix-specialised kernels, generic fallback)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -283,7 +285,7 @@ def base_line(args, world, n, k, r, S, t, elapsed):
         "dtype": "u16 (GF(2^16) words)",
         "data": "synthetic (counter-based splitmix64 stripes generated in HBM)",
         "config": {"workload": f"k={k} r={r} symbol={S}B stripes/gpu={n} decode t={t} (info erasures "
-                               f"at i*{max(k // max(r, 1), 1)})", "stripes_total": n * world,
+                               f"at i*{max(k // max(t, 1), 1)})", "stripes_total": n * world,
                    "parallelism": f"stripes x{world}"},
     }
 
@@ -340,6 +342,8 @@ def main():
 
     k, r, S, n = args.k, args.r, args.symbol, args.stripes
     erased = rs_amd.bench_pattern(k, r)
+    if args.t:  # t information erasures at i * (k // t), no repair erasure
+        erased = np.concatenate([rs_amd.bench_pattern(k, args.t)[:k], np.zeros(r, np.bool_)])
     t = int(erased.sum())
     opts = {"auto": {}, "jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(jit=0, m8_mode=18),
             "idx": dict(jit=0, m8_mode=2), "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1),

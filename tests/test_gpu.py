@@ -529,7 +529,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
     1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle. Two
     stripes make small grids, so every case also runs split-K (k=2000: 31 input slices). Route 0: the
-    dense kernel; route 1: the syndrome route where it applies (R, K >= 64, whole 1 KiB chunks; other
+    dense kernel; route 1: the syndrome route where it applies (K >= 64, whole 1 KiB chunks; other
     launches of a route plan fall back to its dense plan)."""
     rng = np.random.default_rng(k + 7 * r + S)
     n = 2
@@ -542,8 +542,9 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     assert codec.subfield == 16
     codec.encode(dev)
     torch.cuda.synchronize()
-    routed = route == 1 and k >= 64 and r >= 64 and S % 1024 == 0
-    assert codec.last_kernel == ("cs16+bs16" if routed else "apply_m16_v1"), codec.last_kernel
+    routed = route == 1 and k >= 64 and S % 1024 == 0
+    dense = "apply_m16_v1" if r > 32 else f"apply_m16_rt{16 if r <= 16 else 32}"
+    assert codec.last_kernel == ("cs16+bs16" if routed else dense), codec.last_kernel
     got = dev.cpu().numpy()
     want = host.copy()
     for s in range(n):
