@@ -564,10 +564,11 @@ struct rsg_codec {
     int m8_mode = 18;
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
-    int m16_route = 1;  // m = 16 matrices with R, K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense apply
-    // a decode pattern starts on the dense device-built plan and moves to the syndrome route once its
-    // launches have moved this many bytes ((K + R) * S per stripe): the route's host build (~16 ms at
-    // C5) pays only over a few hundred stripes; 0 = route at once (option m16_route_min_bytes)
+    int m16_route = 1;  // m = 16 matrices with K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense, 2 all
+    // a decode pattern with t > 64 erasures starts on the dense device-built plan and moves to the
+    // syndrome route once its launches have moved this many bytes ((K + R) * S per stripe): that route
+    // plan's host build (~16 ms at C5, t = 1024) pays only over a few hundred stripes; 0 = route at once
+    // (option m16_route_min_bytes). Patterns with t <= 64 take the route at once (cheap build).
     int64_t route_min_bytes = int64_t(1) << 30;
     // wave-instructions issued by the hand-scheduled GF(2^16) kernels of the last rsg_encode / rsg_decode
     // (their generated steps' VALU / SALU counts times the steps run; rsg_last_work)
@@ -956,7 +957,8 @@ static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan
     codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
     const int K = int(in.size()), R = int(outs.size());
     if (cs_route_eligible(c, K, R, int(targets.size()))) {
-        if (!erased || c->route_min_bytes == 0) return make_plan_cs(c, erased, out, st);
+        // small t: the route's plan (a few syndrome cosets, a t x t second stage) is cheap to build
+        if (!erased || c->route_min_bytes == 0 || targets.size() <= 64) return make_plan_cs(c, erased, out, st);
         if (int rc = make_plan_dense(c, erased, out, st)) return rc;
         out->route_ok = true;
         out->erased.assign(erased, erased + size_t(c->k) + c->r);
