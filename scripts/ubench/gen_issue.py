@@ -64,7 +64,9 @@ def body(kind):
             raise ValueError(kind)
     return L
 
-KINDS = ["b3_rmw0", "b3_rmw2", "b3_new", "xor_rmw", "xor_c0", "idx_noswitch", "xor", "bitop3_v"] if "--rmw" in sys.argv else ["dep1x", "dep2x", "dep3x", "dep4x", "dep6x", "dep8x", "dep1a", "dep2a", "dep4a", "xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
+OCC = "--occ" in sys.argv  # occupancy sweep: 1..8 waves per SIMD (two workgroups per CU above 4)
+KINDS = ["idx_noswitch", "idx_sw4", "xor", "bitop3_v", "b3_rmw0"] if OCC else \
+    ["b3_rmw0", "b3_rmw2", "b3_new", "xor_rmw", "xor_c0", "idx_noswitch", "xor", "bitop3_v"] if "--rmw" in sys.argv else ["dep1x", "dep2x", "dep3x", "dep4x", "dep6x", "dep8x", "dep1a", "dep2a", "dep4a", "xor", "xor_sgpr", "xor_e64", "and_lit", "and_sgpr", "lshl_imm", "lshr_imm", "lshl_v", "add_u32", "pk_lshl16",
          "lshl_add", "lshl_or", "and_or", "or3", "bfi", "bfe", "perm_v", "perm_s", "alignbit", "pk_mul", "pk_mul_v",
          "mul_u24", "bitop3_s", "bitop3_v", "cndmask", "mov", "xor_sdwa", "idx_noswitch", "idx_sw2",
          "idx_sw4", "nop_sw2", "sadd_2"]
@@ -90,6 +92,7 @@ for n, k in enumerate(KINDS):
     if ((threadIdx.x & 63) == 0) out[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)] = t1 - t0;
 }}
 static const int nvalu{n} = {nv}, ninst{n} = {len(pre) + len(b) + len(post) + 3};''')
+out.append(f'#define WMAX {6 if OCC else 3}')
 out.append('typedef void (*kfn)(unsigned long long*, int);')
 out.append('static kfn fns[] = {' + ", ".join(f"k{n}" for n in range(len(KINDS))) + '};')
 out.append('static const int nvalu[] = {' + ", ".join(f"nvalu{n}" for n in range(len(KINDS))) + '};')
@@ -97,12 +100,14 @@ out.append('static const int ninst[] = {' + ", ".join(f"ninst{n}" for n in range
 out.append(r'''int main() {
     int cus = 0; hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 500;
-    unsigned long long* d; hipMalloc(&d, sizeof(unsigned long long) * cus * 16);
-    std::vector<unsigned long long> h(cus * 16);
+    unsigned long long* d; hipMalloc(&d, sizeof(unsigned long long) * cus * 32);
+    std::vector<unsigned long long> h(cus * 32);
     for (int k = 0; k < (int)(sizeof(fns) / sizeof(fns[0])); ++k)
-        for (int w = 1; w <= 3; ++w) {
-            hipMemset(d, 0, sizeof(unsigned long long) * cus * 16); hipLaunchKernelGGL(fns[k], dim3(cus), dim3(256 * w), 0, 0, d, iters);  // warm
-            hipLaunchKernelGGL(fns[k], dim3(cus), dim3(256 * w), 0, 0, d, iters);
+        for (int w = 1; w <= WMAX; ++w) {
+            if (w > 4 && (w & 1)) continue;  // above 4: two equal workgroups per CU
+            const int nb = w > 4 ? 2 : 1, bs = 256 * w / nb;
+            hipMemset(d, 0, sizeof(unsigned long long) * cus * 32); hipLaunchKernelGGL(fns[k], dim3(cus * nb), dim3(bs), 0, 0, d, iters);  // warm
+            hipLaunchKernelGGL(fns[k], dim3(cus * nb), dim3(bs), 0, 0, d, iters);
             if (hipDeviceSynchronize() != hipSuccess) { printf("{\"error\": \"%s\"}\n", kinds[k]); return 1; }
             hipMemcpy(h.data(), d, sizeof(unsigned long long) * cus * 4 * w, hipMemcpyDeviceToHost);
             std::sort(h.begin(), h.begin() + cus * 4 * w);
