@@ -273,9 +273,19 @@ struct DevPlan {
         int32_t* fin = nullptr;
         int32_t* fin_off = nullptr;
         uint32_t nblog[16] = {};
+        std::vector<int32_t> h_groups;  // host copy of `groups` (re-encode plans mask it)
     };
     std::unique_ptr<Cs> cs;
     std::unique_ptr<DevPlan> second, dense;
+    // Decode by re-encoding (no repair symbol erased, t close to r): with U the surviving information
+    // slots, e = D_Rep (y + G_U u) -- G_U u is the codec's encode route (k_cs16 + k_bs16) over U only
+    // (`groups` = the encode plan's groups with the erased slots masked), y the received repair symbols,
+    // D_Rep the decode matrix's repair columns (t x r, dense). Exact: D_U = D_Rep G_U over GF(2^16).
+    struct Reenc {
+        int32_t* groups = nullptr;  // in this plan's blob
+        std::unique_ptr<DevPlan> drep;
+    };
+    std::unique_ptr<Reenc> reenc;
     // decode plans of route-eligible GF(2^16) patterns start dense: `route` is built once route_bytes
     // (bytes moved by this plan's launches) reaches the codec's route_min_bytes
     bool route_ok = false;
@@ -574,6 +584,9 @@ struct rsg_codec {
     // (their generated steps' VALU / SALU counts times the steps run; rsg_last_work)
     uint64_t work_valu = 0, work_salu = 0;
     void* d_cs = nullptr;  // syndrome route scratch: [chunk][D][S]
+    void* d_reenc = nullptr;  // re-encode decode scratch: [chunk][r][S] (G_U u + y)
+    size_t reenc_cap = 0;
+    int m16_reenc = 1;  // option m16_reenc: 0 keeps full-pattern decodes on the plain route
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
     size_t goff_cap[2] = {0, 0};
@@ -628,7 +641,7 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_goff[0], d_goff[1]})
+                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_reenc, d_goff[0], d_goff[1]})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -817,6 +830,7 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
     cs->ntiles = h.ntiles;
     cs->fin_stride = h.fin_stride;
     cs->groups = PlanBlob::at<int32_t>(p, o_g);
+    cs->h_groups = h.groups;
     cs->rec = PlanBlob::at<uint32_t>(p, o_r);
     cs->fin = PlanBlob::at<int32_t>(p, o_f);
     cs->fin_off = PlanBlob::at<int32_t>(p, o_fo);
@@ -950,6 +964,63 @@ static int make_plan_cs(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevP
     return 0;
 }
 
+// Re-encode decode eligibility: the codec's encode plan is the route with the k_bs16 second stage, no
+// repair slot is erased, and t is close to r (the re-encode pays for all r syndromes of the encode
+// route whatever t is; the plain route's syndrome pass shrinks with t: measured cross-over near 0.9 r).
+static bool reenc_eligible(const rsg_codec_t* c, const bool* erased) {
+    if (!c->m16_reenc || c->m <= 8 || !erased || !c->enc || !c->enc->cs || c->enc->cs->kind != 0 || !c->enc->second ||
+        !c->enc->second->cs || c->enc->second->cs->kind != 1 || c->enc->cs->h_groups.empty())
+        return false;
+    int t = 0;
+    for (int i = 0; i < c->k; ++i) t += erased[i] ? 1 : 0;
+    for (int i = c->k; i < c->k + c->r; ++i)
+        if (erased[i]) return false;
+    return t >= 1 && 10 * t >= 9 * c->r && c->k - t >= 64;
+}
+
+static int make_plan_reenc(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
+    const DevPlan& E = *c->enc;
+    const size_t k = c->k, r = c->r;
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in_u, outs;
+    for (size_t i = 0; i < k; ++i) {
+        if (erased[i]) {
+            emit.push_back(int(targets.size()));
+            targets.push_back(c->positions[i]);
+            outs.push_back(int32_t(i));
+        } else {
+            in_u.push_back(int32_t(i));
+        }
+    }
+    for (size_t p = 0; p < r; ++p) sources.push_back(c->positions[k + p]);
+    std::vector<int32_t> groups = E.cs->h_groups;  // the encode route's input groups, erased slots masked
+    for (int32_t& g : groups)
+        if (g >= 0 && erased[g]) g = -1;
+    auto p = std::make_unique<DevPlan>();
+    p->device = c->device;
+    p->m = 16;
+    p->K = int(in_u.size() + r);  // survivors read: U and the r repair symbols
+    p->R = int(outs.size());
+    p->in_slots = in_u;
+    for (size_t q = 0; q < r; ++q) p->in_slots.push_back(int32_t(k + q));
+    p->out_slots = outs;
+    p->erased.assign(erased, erased + k + r);
+    PlanBlob blob;
+    const size_t o_g = blob.add(groups.data(), groups.size() * 4);
+    if (int rc = blob.upload(*p, st)) return rc;
+    if (int rc = PlanBlob::finish(*p)) return rc;
+    p->reenc = std::make_unique<DevPlan::Reenc>();
+    p->reenc->groups = PlanBlob::at<int32_t>(*p, o_g);
+    std::vector<int32_t> rows(r);
+    for (size_t q = 0; q < r; ++q) rows[q] = int32_t(q);  // scratch rows y + G_U u
+    if (int rc = build_plan_m16_device(c->device, targets, emit, sources, std::move(rows), std::move(outs),
+                                       p->reenc->drep, st))
+        return rc;
+    out = std::move(p);
+    return 0;
+}
+
 static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
     std::vector<uint16_t> targets, sources;
     std::vector<int> emit;
@@ -957,8 +1028,10 @@ static int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan
     codec_lists(c->positions, c->k, c->r, erased, targets, emit, sources, in, outs);
     const int K = int(in.size()), R = int(outs.size());
     if (cs_route_eligible(c, K, R, int(targets.size()))) {
-        // small t: the route's plan (a few syndrome cosets, a t x t second stage) is cheap to build
-        if (!erased || c->route_min_bytes == 0 || targets.size() <= 64) return make_plan_cs(c, erased, out, st);
+        // small t: the route's plan (a few syndrome cosets, a t x t second stage) is cheap to build. Larger
+        // patterns start dense and move to the route (or the re-encode decode) at the first launch past
+        // route_min_bytes (0: the first launch the route covers); the dense plan serves the rest.
+        if (!erased || targets.size() <= 64) return make_plan_cs(c, erased, out, st);
         if (int rc = make_plan_dense(c, erased, out, st)) return rc;
         out->route_ok = true;
         out->erased.assign(erased, erased + size_t(c->k) + c->r);
@@ -1083,6 +1156,13 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "m16_reenc")) {  // decode patterns built from now on
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->m16_reenc = int(value);
+        c->dec.clear();
+        c->dec_lru.clear();
+        return 0;
+    }
     if (!std::strcmp(name, "m16_route_min_bytes")) {
         if (value < 0) return RS_ERR_INVALID;
         c->route_min_bytes = value;
@@ -1117,7 +1197,8 @@ static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_
                     const int32_t* d_ids = nullptr, bool dst_local = false);
 
 static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
-                  int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st) {
+                  int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
+                  const int32_t* groups = nullptr) {
     const DevPlan::Cs& cs = *p.cs;
     if ((uintptr_t(src) | uintptr_t(dst) | uint64_t(src_stripe) | uint64_t(src_sym) | uint64_t(dst_stripe) |
          uint64_t(dst_sym)) % 4)
@@ -1127,7 +1208,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
     const int ngo = (cs.ngroups + 3) * 16;
     if (int rc = grow(&c->d_goff[cs.kind], c->goff_cap[cs.kind], size_t(ngo) * 4)) return rc;
-    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
+    HIP_TRY(launch_cs16_goff(groups ? groups : cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
     Cs16Args a{};
     a.src_stripe = src_stripe;
     a.src_sym = src_sym;
@@ -1181,6 +1262,31 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     return scratch_release(c, st);
 }
 
+// The re-encode decode (DevPlan::Reenc) over a chunk loop: the encode route over U into scratch rows
+// (G_U u), + the received repair rows, then D_Rep from scratch into the erased information slots.
+static int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_stride, int64_t sym,
+                     uint64_t n_stripes, uint64_t S, hipStream_t st) {
+    DevPlan& E = *c->enc;
+    const int64_t k = c->k, r = c->r, per = r * int64_t(S);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({int64_t(n_stripes), (int64_t(1) << 30) / per, 65535}));
+    if (int rc = scratch_acquire(c, st)) return rc;
+    if (int rc = grow(&c->d_reenc, c->reenc_cap, size_t(chunk * per))) return rc;
+    uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
+    std::string k2;
+    for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
+        const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
+        uint8_t* b = base + c0 * stripe_stride;
+        if (int rc = run_cs(c, E, b, stripe_stride, sym, y, per, int64_t(S), uint64_t(cn), S, st, p.reenc->groups))
+            return rc;
+        HIP_TRY(launch_xor_rows(y, per, int64_t(S), b + k * sym, stripe_stride, sym, r, int64_t(S), cn, st));
+        if (int rc = run_plan(c, *p.reenc->drep, y, per, int64_t(S), b, stripe_stride, sym, uint64_t(cn), S, st))
+            return rc;
+        k2 = c->last_kernel;
+    }
+    c->last_kernel = "cs16+bs16+xor+" + k2;
+    return scratch_release(c, st);
+}
+
 static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym,
                          uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
                          hipStream_t st, const int32_t* d_ids, bool dst_local);
@@ -1199,6 +1305,10 @@ static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t
                          uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
                          hipStream_t st, const int32_t* d_ids, bool dst_local) {
     if (int rc = p.order_after_build(st)) return rc;
+    if (p.reenc) {  // in place: src == dst is the stripe (rsg_decode); the parent checked the launch fits
+        if (src != dst || src_stripe != dst_stripe || src_sym != dst_sym || d_ids || dst_local) return RS_ERR_INVALID;
+        return run_reenc(c, p, dst, dst_stripe, dst_sym, n_stripes, S, st);
+    }
     if (p.route_ok && !d_ids && !dst_local && S % 1024 == 0 && int64_t(S) < (int64_t(1) << 31)) {
         int64_t max_in = 0;  // the route's 31-bit offsets (run_plan_body's p.cs branch)
         for (int32_t v : p.in_slots) max_in = std::max<int64_t>(max_in, v);
@@ -1209,7 +1319,11 @@ static int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t
             if (p.route_bytes >= uint64_t(c->route_min_bytes)) {
                 std::unique_ptr<bool[]> er(new bool[p.erased.size()]);
                 for (size_t i = 0; i < p.erased.size(); ++i) er[i] = p.erased[i] != 0;
-                if (int rc = make_plan_cs(c, er.get(), p.route, st)) return rc;
+                const bool re = reenc_eligible(c, er.get()) && src == dst && src_stripe == dst_stripe &&
+                                src_sym == dst_sym && (c->k + c->r) * src_sym < (int64_t(1) << 31) &&
+                                int64_t(c->r) * int64_t(S) < (int64_t(1) << 31);
+                if (int rc = re ? make_plan_reenc(c, er.get(), p.route, st) : make_plan_cs(c, er.get(), p.route, st))
+                    return rc;
             }
         }
         if (fits && p.route)

@@ -1412,6 +1412,29 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
     return hipGetLastError();
 }
 
+// Re-encode decode (rs_api.cpp run_reenc): row p of stripe s of dst ^= row p of stripe s of src, S bytes
+// as 4-byte words (blockIdx.y = row, blockIdx.z = stripe).
+__global__ void __launch_bounds__(256) k_xor_rows(uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, const uint8_t* src,
+                                                  int64_t src_stripe, int64_t src_sym, int64_t words) {
+    const int64_t w = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (w >= words) return;
+    const int64_t p = blockIdx.y, s = blockIdx.z;
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst + s * dst_stripe + p * dst_sym) + w;
+    *d ^= reinterpret_cast<const uint32_t*>(src + s * src_stripe + p * src_sym)[w];
+}
+
+hipError_t launch_xor_rows(uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, const uint8_t* src, int64_t src_stripe,
+                           int64_t src_sym, int64_t nrows, int64_t S, int64_t n_stripes, hipStream_t st) {
+    if (nrows <= 0 || n_stripes <= 0 || S <= 0) return hipSuccess;
+    if ((S | dst_stripe | dst_sym | src_stripe | src_sym) % 4 || (uintptr_t(dst) | uintptr_t(src)) % 4 ||
+        nrows > 65535 || n_stripes > 65535)
+        return hipErrorInvalidValue;
+    const int64_t words = S / 4;
+    hipLaunchKernelGGL(k_xor_rows, dim3(unsigned((words + 255) / 256), unsigned(nrows), unsigned(n_stripes)), dim3(256),
+                       0, st, dst, dst_stripe, dst_sym, src, src_stripe, src_sym, words);
+    return hipGetLastError();
+}
+
 // 16-byte stores of whole rows across PCIe into page-locked host memory (posted writes; visible to
 // the host once the stream's completion event has been waited on)
 __global__ void __launch_bounds__(256) k_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,

@@ -101,6 +101,9 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
 // rows == nullptr: rows 0 .. nrows - 1
 hipError_t launch_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
                            int64_t nrows, int64_t width, hipStream_t st);
+// row p of stripe s of dst ^= the same row of src (p < nrows, S bytes, 4-byte aligned; the re-encode decode)
+hipError_t launch_xor_rows(uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, const uint8_t* src, int64_t src_stripe,
+                           int64_t src_sym, int64_t nrows, int64_t S, int64_t n_stripes, hipStream_t st);
 
 // m = 16 cyclotomic syndromes (k_cs16, the reference's fft_transform_cycl structure, src/rs/fft.c:39-100):
 // S_j = sum_i X_i^j in_i for the needed j, inputs grouped by cyclotomic coset (16 slots at positions

@@ -78,24 +78,27 @@ def one(family):
     elif family == "route":  # GF(2^16) syndrome route: K, R >= 64, whole 1 KiB column chunks
         k = int(rng.integers(200, 1200))
         r = int(rng.integers(max(64, 256 - k), 300))
+    elif family == "reenc":  # re-encode decode: information erasures only, t >= 0.9 r
+        k = int(rng.integers(300, 1500))
+        r = int(rng.integers(max(64, 256 - k), 300))
     else:  # batch16: GF(2^16) codes, small enough for the oracle to check every stripe quickly
         k = int(rng.integers(150, 500))
         r = int(rng.integers(max(1, 256 - k), 160))
     S = int(rng.choice([2048, 4096, 8192, 1024])) + 8 * int(rng.integers(0, 64)) * int(rng.integers(0, 2))
     if family in ("m16", "batch16"):
         S = min(S, 4096 if family == "m16" else 2048)
-    if family == "route":
+    if family in ("route", "reenc"):
         S = 1024 * int(rng.integers(1, 4))
     n = int(rng.integers(1, 5)) if family not in ("batch", "batch16") else int(rng.integers(20, 60))
-    if family == "route":
+    if family in ("route", "reenc"):
         n = int(rng.integers(1, 3))
     host = np.zeros((n, k + r, S), np.uint8)
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
-    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "route": {}, "batch": dict(batch_plans=1),
+    kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "route": {}, "reenc": {}, "batch": dict(batch_plans=1),
           "batch16": dict(batch_plans=1)}[family]
     codec = rs_amd.Codec(k, r, **kw)
-    if family == "route":
+    if family in ("route", "reenc"):
         codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route at once
     codec.encode(dev)
     torch.cuda.synchronize()
@@ -115,8 +118,11 @@ def one(family):
         assert codec.decode_batch(dev, pats) == 0
     else:
         er = np.zeros(k + r, bool)
-        lo = 64 if family == "route" and rng.integers(0, 2) else 1  # t >= 64: the decode route too
-        er[rng.choice(k + r, int(rng.integers(min(lo, r), r + 1)), replace=False)] = True
+        if family == "reenc":
+            er[rng.choice(k, int(rng.integers((9 * r + 9) // 10, r + 1)), replace=False)] = True
+        else:
+            lo = 64 if family == "route" and rng.integers(0, 2) else 1  # t >= 64: the decode route too
+            er[rng.choice(k + r, int(rng.integers(min(lo, r), r + 1)), replace=False)] = True
         pats = np.broadcast_to(er, (n, k + r))
         poisoned = got.copy()
         poisoned[:, er] = 0
@@ -133,8 +139,8 @@ def one(family):
     return dict(family=family, k=k, r=r, S=S, stripes=n, encode=enc_kernel, decode=dec_kernel, ok=ok)
 
 
-families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "batch", "batch16",
-                                                             "dropin"]
+families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "reenc", "batch",
+                                                             "batch16", "dropin"]
 i = 0
 while time.time() < t_end:
     fam = families[i % len(families)]

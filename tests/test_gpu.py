@@ -597,6 +597,42 @@ def test_m16_decode_moves_to_route():
     assert kernels[0] == "apply_m16_v1" and kernels[1].startswith("cs16+") and kernels[2] == kernels[1], kernels
 
 
+@pytest.mark.parametrize("k,r,t,S", [(1000, 200, 200, 2048), (700, 96, 90, 1024), (4096, 1024, 1024, 1024)])
+def test_m16_reenc_decode(k, r, t, S):
+    """GF(2^16) decode by re-encoding (information erasures only, t >= 0.9 r): the encode route over the
+    surviving information symbols, + the received repair symbols, then the decode matrix's repair
+    columns -- bit-exact vs the oracle (C5 shape included), and the same bytes as the plain route."""
+    rng = np.random.default_rng(k + r + t)
+    n = 2
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route_min_bytes", 0)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k, t, replace=False)] = True
+    poisoned = got.copy()
+    poisoned[:, er] = 0
+    outs = []
+    for reenc in (1, 0):
+        codec.set_option("m16_reenc", reenc)
+        dev.copy_(torch.from_numpy(poisoned))
+        codec.decode(dev, er)
+        torch.cuda.synchronize()
+        assert codec.last_kernel.startswith("cs16+bs16+xor+" if reenc else "cs16+apply"), codec.last_kernel
+        outs.append(dev.cpu().numpy())
+    assert np.array_equal(outs[0][:, :k], got[:, :k])
+    assert np.array_equal(outs[0], outs[1])
+    if k + r <= 1500:
+        for s in range(n):
+            ref = poisoned[s].copy()
+            assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
+            assert np.array_equal(outs[0][s], ref)
+
+
 def test_drop_in_arena_mixed_layouts():
     """Per-call calls on seq_create memory in layouts other than one strided sequence: information and
     repair symbols in two different sequences (zero-copy with two bases), and a sequence whose symbol
