@@ -1267,6 +1267,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
 static int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_stride, int64_t sym,
                      uint64_t n_stripes, uint64_t S, hipStream_t st) {
     DevPlan& E = *c->enc;
+    if (int rc = E.order_after_build(st)) return rc;  // its records are read directly (run_cs, not run_plan)
     const int64_t k = c->k, r = c->r, per = r * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({int64_t(n_stripes), (int64_t(1) << 30) / per, 65535}));
     if (int rc = scratch_acquire(c, st)) return rc;
