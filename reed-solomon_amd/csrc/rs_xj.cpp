@@ -154,6 +154,10 @@ struct XjConfig {
                        // table T[w] = gamma * w (persistent kernel, one workgroup per CU)
     int xcd = 0;       // 1: workgroup -> column remap so each XCD walks contiguous 1/8 spans of every stripe
                        // (dispatch puts workgroup i on XCD i % 8); 0: consecutive columns round-robin
+    int cpb = 1;       // columns per block: > 1 loops each role over cpb consecutive 256-byte columns of a
+                       // stripe; the next column's first input pair is loaded during the current column's
+                       // last pair and finish (its ring slot stays clear of the finish registers), so only
+                       // the block's first column waits for a cold load. Needs an even pair count (set_k).
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
@@ -172,6 +176,7 @@ struct XjConfig {
         env("RS_XJ_SHARE", share);
         env("RS_XJ_KREG", kreg);
         env("RS_XJ_XCD", xcd);
+        env("RS_XJ_CPB", cpb);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -182,21 +187,30 @@ struct XjConfig {
         share = (share && !lds && !lfin && R > 0 && (R + opr - 1) / opr == 2) ? 1 : 0;
         ring = std::max(2, std::min(6, ring));
         horner = horner ? 1 : 0;
+        cpb = std::max(1, std::min(64, cpb));
+        if (lfin || lds || share || spread || xcd || buffer || ring != 2) cpb = 1;
+    }
+    // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
+    void set_k(int K) {
+        if (((K + 7) / 8) % 2) cpb = 1;
     }
     // register map (the column offset is the compiler's %[col] operand register, outside this range)
     int acc(int q, int t) const { return 1 + 8 * q + t; }
     int ring_base() const { return 1 + 8 * opr; }
     int tab(int h) const { return ring_base() + 8 * ring + 11 * h; }
     int max_vgpr() const { return tab(2) - 1; }
-    // after the XOR network: result of output q, and per-chain temporaries (chains run in batches of 8)
-    int fin(int q) const { return ring_base() + q; }
-    int tmp(int q, int k) const { return ring_base() + opr + 2 * (q % 8) + k; }
-    int cst() const { return ring_base() + opr + 16; }  // cst .. cst + 2 <= max_vgpr: opr <= 8 ring + 3
+    // after the XOR network: result of output q, and per-chain temporaries (chains run in batches of 8).
+    // Column loop (cpb > 1): results and temporaries above ring slot 0 (slot 1 + the tables), one batch of
+    // 8 results at a time, each batch stored before the next is computed.
+    int fin(int q) const { return cpb > 1 ? ring_base() + 8 + q % 8 : ring_base() + q; }
+    int tmp(int q, int k) const { return (cpb > 1 ? ring_base() + 16 : ring_base() + opr) + 2 * (q % 8) + k; }
+    int cst() const { return cpb > 1 ? ring_base() + 32 : ring_base() + opr + 16; }  // cst + 2 <= max_vgpr
     std::string tag() const {
         char b[128];
         std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
-        return xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
+        std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
+        return cpb > 1 ? s + " cpb" + std::to_string(cpb) : s;
     }
 };
 
@@ -238,15 +252,24 @@ std::vector<std::string> finish_block(const XjConfig& C) {
     const XjBasis& B = xj_basis(C.horner);
     std::vector<std::string> L;
     L.push_back("s_branch L_xj_fin_end");
-    L.push_back("L_xj_fin:");
-    if (C.horner) {
-        L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0x2d002d");
-    } else if (C.kreg) {  // step constants in VGPRs: 4-byte VOP2 forms issue faster than literal ones (bank_bench)
-        L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0xfffeffff");
-        L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 1) + ", 0x10001");
-        L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 2) + ", 0x8016");
+    auto consts = [&]() {
+        if (C.horner) {
+            L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0x2d002d");
+        } else if (C.kreg) {  // step constants in VGPRs: 4-byte VOP2 forms issue faster than literal ones (bank_bench)
+            L.push_back("v_mov_b32 v" + std::to_string(C.cst()) + ", 0xfffeffff");
+            L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 1) + ", 0x10001");
+            L.push_back("v_mov_b32 v" + std::to_string(C.cst() + 2) + ", 0x8016");
+        }
+    };
+    if (C.cpb == 1) {
+        L.push_back("L_xj_fin:");
+        consts();
     }
     for (int q0 = 0; q0 < C.opr; q0 += 8) {
+        if (C.cpb > 1) {  // column loop: one entry per batch of 8 outputs (L_xj_fin0, L_xj_fin1)
+            L.push_back("L_xj_fin" + std::to_string(q0 / 8) + ":");
+            consts();
+        }
         const int nc = std::min(8, C.opr - q0);
         std::vector<std::vector<std::string>> chains(static_cast<size_t>(nc));
         for (int c = 0; c < nc; ++c) {
@@ -317,8 +340,9 @@ std::vector<std::string> finish_block(const XjConfig& C) {
         const size_t n = chains[0].size();
         for (size_t i = 0; i < n; ++i)
             for (int c = 0; c < nc; ++c) L.push_back(chains[size_t(c)][i]);
+        if (C.cpb > 1) L.push_back("s_setpc_b64 s[58:59]");
     }
-    L.push_back("s_setpc_b64 s[58:59]");
+    if (C.cpb == 1) L.push_back("s_setpc_b64 s[58:59]");
     L.push_back("L_xj_fin_end:");
     return L;
 }
@@ -415,9 +439,12 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.e("s_mov_b32 s55, 0x20000");
     }
     const int ngp = (K + 7) / 8;
+    const bool loop = C.cpb > 1;  // column loop (s39 = columns left, %[col] advances by 256 per column)
+    if (loop) E.e("s_mov_b32 s39, %[nc]");
     auto nload = [&](int g) { return g < ngp ? std::min(8, K - 8 * g) : 0; };
-    // instruction lists of the loads of pair g (address arithmetic first, then the loads)
-    auto load_ops = [&](int g) {
+    // instruction lists of the loads of pair g (address arithmetic first, then the loads); `next_col`:
+    // the same pair of the following column (immediate offset 256)
+    auto load_ops = [&](int g, bool next_col = false) {
         std::vector<std::string> ops;
         const int n = nload(g);
         for (int j = 0; j < n; ++j) {
@@ -430,8 +457,8 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 ops.push_back(E.fmt("s_mul_i32 s62, s34, %d", slot));
                 ops.push_back(E.fmt("s_add_u32 s%d, s32, s62", 40 + 2 * j));
                 ops.push_back(E.fmt("s_addc_u32 s%d, s33, 0", 41 + 2 * j));
-                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
-                                    (C.nt & 1) ? " nt" : ""));
+                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
+                                    next_col ? " offset:256" : "", (C.nt & 1) ? " nt" : ""));
             }
         }
         return ops;
@@ -471,6 +498,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         for (int g = 0; g < ahead; ++g)
             for (auto& op : load_ops(g)) E.e(op);
     }
+    if (loop) {  // the first column's pair 0 is the block's only cold wait
+        E.e("s_waitcnt vmcnt(0)");
+        E.f("L_xj_col%d:", w);
+    }
     for (int g = 0; g < ngp; ++g) {
         std::vector<std::string> next, mid;
         if (D) {
@@ -492,7 +523,16 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 for (auto& op : next) E.e(op);
                 pending += nload(g + ahead);
             }
+            // column loop: the previous column's stores were issued after this pair 0 and before the
+            // loads above (vmcnt retires in issue order)
+            if (loop && g == 0) pending += nq;
             E.f("s_waitcnt vmcnt(%d)", pending);
+            if (loop && g == ngp - 1) {  // the next column's pair 0 into ring slot 0 (free: pair ngp-2 is done)
+                E.e("s_cmp_gt_u32 s39, 1");
+                E.f("s_cbranch_scc0 L_xj_npf%d", w);
+                for (auto& op : load_ops(0, true)) E.e(op);
+                E.f("L_xj_npf%d:", w);
+            }
         }
         // patterns of this role's rows over the pair's two groups
         int pat[16][8][2];
@@ -607,6 +647,33 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
     for (int q = 0; q < nq; ++q)
         for (int t = 0; t < 8; ++t)
             if (!init[q][t]) E.f("v_mov_b32 v%d, 0", C.acc(q, t));
+    if (loop) {  // per batch of 8 outputs: its finish entry, then its stores (no wait: operands are read at issue)
+        for (int q0 = 0; q0 < nq; q0 += 8) {
+            const int nb = std::min(8, nq - q0);
+            if (!(C.ablate & 1)) {
+                E.e("s_getpc_b64 s[56:57]");
+                E.f("s_add_u32 s56, s56, L_xj_fin%d-.", q0 / 8);
+                E.e("s_addc_u32 s57, s57, -1");
+                E.e("s_swappc_b64 s[58:59], s[56:57]");
+            } else {
+                for (int j = 0; j < nb; ++j) E.f("v_mov_b32 v%d, v%d", C.fin(q0 + j), C.acc(q0 + j, 0));
+            }
+            for (int j = 0; j < nb; ++j) {
+                E.f("s_mul_i32 s62, s38, %d", out_slots[size_t(p0 + q0 + j)]);
+                E.f("s_add_u32 s%d, s36, s62", 40 + 2 * j);
+                E.f("s_addc_u32 s%d, s37, 0", 41 + 2 * j);
+            }
+            for (int j = 0; j < nb; ++j)
+                E.f("global_store_dword %s, v%d, s[%d:%d]%s", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j,
+                    (C.nt & 2) ? " nt" : "");
+        }
+        E.f("v_add_u32 %s, 0x100, %s", COL, COL);
+        E.e("s_sub_u32 s39, s39, 1");
+        E.e("s_cmp_lg_u32 s39, 0");
+        E.f("s_cbranch_scc1 L_xj_col%d", w);
+        E.e("s_waitcnt vmcnt(0)");
+        return E.L;
+    }
     // finish (shared block; returns through s[58:59]); L_xj_fin precedes every role block
     if (!(C.ablate & 1)) {
         E.e("s_getpc_b64 s[56:57]");
@@ -665,7 +732,8 @@ static void count_insts(const std::vector<std::string>& L, uint64_t mult, uint64
 
 static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                const std::vector<int32_t>& out_slots, uint64_t* valu, uint64_t* salu) {
-    const XjConfig C(R);
+    XjConfig C(R);
+    C.set_k(K);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
     for (size_t e = 0; e < M.size(); ++e) cb[e] = C.lfin ? gamma8().coord(M[e]) : B.bits(M[e]);
@@ -681,7 +749,8 @@ static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::v
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
                       const std::vector<int32_t>& out_slots) {
-    const XjConfig C(R);
+    XjConfig C(R);
+    C.set_k(K);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
     for (size_t e = 0; e < M.size(); ++e) cb[e] = C.lfin ? gamma8().coord(M[e]) : B.bits(M[e]);
@@ -724,8 +793,12 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
                       "  const uint64_t dstripe = a.dst_local ? (uint64_t)by : stripe;\n"
                       "  const uint32_t col = bx * 256u + (threadIdx.x & 63u) * 4u;\n"
                     : "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
-                      "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n"
-                      "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n")
+                      "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n")
+          << (C.cpb > 1 ? "  const uint32_t c0 = blockIdx.x * " + std::to_string(C.cpb) + "u;\n"
+                          "  const uint32_t nc = a.nchunks - c0 < " + std::to_string(C.cpb) + "u ? a.nchunks - c0 : " +
+                              std::to_string(C.cpb) + "u;\n"
+                          "  uint32_t col = c0 * 256u + (threadIdx.x & 63u) * 4u;\n"
+                        : std::string(C.xcd ? "" : "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"))
           << ""
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
              "  const uint32_t lb = (uint32_t)(unsigned long)xj_lds + (uint32_t)role * "
@@ -744,7 +817,9 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
     for (int w = 0; w < roles; ++w) {
         o << "  case " << w << ": asm volatile(\n"
           << as_string_literals(role_block(C, w, cb, K, R, in_slots, out_slots))
-          << "  : : [col] \"v\"(col), [la] \"v\"(la), [sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
+          << (C.cpb > 1 ? "  : [col] \"+v\"(col) : [la] \"v\"(la), [nc] \"s\"(nc), "
+                        : "  : : [col] \"v\"(col), [la] \"v\"(la), ")
+          << "[sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
              " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)\n  : "
           << clob << ");\n    break;\n";
     }
@@ -811,6 +886,11 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     (void)hipGetDevice(&k->device);
     k->roles = xj_roles(R);
     k->pairs = XjConfig(R).lfin ? xj_pairs(R) : 0;
+    {
+        XjConfig C(R);
+        C.set_k(K);
+        k->cpb = C.cpb;
+    }
     if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), fname.c_str()) != hipSuccess) return 3;
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%s]", R, K, fname.c_str() + 6);
@@ -891,9 +971,10 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
         a.src_stripe = 0;
         a.dst_stripe = 0;
         void* args[] = {&a};
+        a.nchunks = uint32_t(nchunks);
         const unsigned ny = unsigned(std::min<int64_t>(65535, n_stripes));
-        hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(nchunks), ny, 1, unsigned(64 * k.roles), 1, 1, 0, st, args,
-                                             nullptr);
+        hipError_t e = hipModuleLaunchKernel(k.fn, unsigned((nchunks + k.cpb - 1) / k.cpb), ny, 1,
+                                             unsigned(64 * k.roles), 1, 1, 0, st, args, nullptr);
         return e == hipSuccess ? 0 : 3;
     }
     for (int64_t s0 = 0; s0 < n_stripes; s0 += 65535) {  // grid.y limit
@@ -905,10 +986,11 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
             a.src += s0 * a.src_stripe;
             a.dst += s0 * a.dst_stripe;
         }
+        a.nchunks = uint32_t(nchunks);
         const unsigned ny = unsigned(std::min<int64_t>(65535, n_stripes - s0));
         void* args[] = {&a};
-        hipError_t e = hipModuleLaunchKernel(k.fn, unsigned(nchunks), ny, 1, unsigned(64 * k.roles), 1, 1, 0, st, args,
-                                             nullptr);
+        hipError_t e = hipModuleLaunchKernel(k.fn, unsigned((nchunks + k.cpb - 1) / k.cpb), ny, 1,
+                                             unsigned(64 * k.roles), 1, 1, 0, st, args, nullptr);
         if (e != hipSuccess) {
             std::fprintf(stderr, "librs_amd: xj launch: %s\n", hipGetErrorString(e));
             return 3;

@@ -34,7 +34,7 @@ struct XJArgs {
     int32_t src_sym, dst_sym;  // symbol strides (slot * stride < 2^31)
     const int32_t* ids;        // optional [n_stripes] stripe indices; null = 0..n-1
     const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch)
-    uint32_t nchunks, ncols;   // persistent form: chunks per stripe, chunks in the launch (set by xj_launch)
+    uint32_t nchunks, ncols;   // chunks per stripe (set by xj_launch); persistent form: chunks in the launch
     uint32_t dst_local;        // 1: dst indexed by the launch-local stripe (ids only select the source)
 };
 
@@ -44,6 +44,7 @@ struct XjKernel {
     int device = 0;
     int roles = 0;  // waves per column (opr outputs each)
     int pairs = 0;  // > 0: persistent kernel (LDS finish), columns per workgroup in flight, grid <= CUs
+    int cpb = 1;    // consecutive 256-byte columns per workgroup (column loop), grid.x = chunks / cpb
     std::string name;
     // wave instructions per 256-byte column, all role waves together, counted in the generated asm
     // (the XOR network, the finish once per role, loads / stores / addressing); the compiler's few

@@ -147,3 +147,40 @@ def test_xj_generation_knobs_match_oracle(k, r, knobs, monkeypatch):
     mem.b[:k * S] = want[:k].reshape(-1)
     run_block(xj_source(k, r), mem, 0, S, k * S, S)
     assert np.array_equal(mem.b.reshape(k + r, S)[k:], want[k:])
+
+
+@pytest.mark.parametrize("cpb,ncols", [(2, 4), (4, 4), (4, 3), (8, 1)])
+@pytest.mark.parametrize("k,r,kind", [(128, 32, "enc"), (128, 32, "bench"), (30, 17, "enc"), (16, 4, "enc"),
+                                      (24, 8, "enc")])
+def test_xj_column_loop_matches_oracle(k, r, kind, cpb, ncols, monkeypatch):
+    """RS_XJ_CPB (a block loops over cpb consecutive 256-byte columns; the next column's first input pair
+    is loaded under the current column's last pair and finish, results stored per batch of 8): every
+    column of the block is bit-exact vs the oracle, including a block with fewer columns than cpb and
+    pair counts the loop does not take (K = 24: three pairs -> one column per block)."""
+    monkeypatch.setenv("RS_XJ_CPB", str(cpb))
+    S4 = 256 * ncols
+    rng = np.random.default_rng(k * 31 + r + cpb)
+    full = np.zeros((k + r, S4), np.uint8)
+    full[:k] = rng.integers(0, 256, (k, S4), dtype=np.uint8)
+    assert oracle_encode(k, r, full) == 0
+    looped = ((k + 7) // 8) % 2 == 0
+    if kind == "enc":
+        src = xj_source(k, r)
+        assert ("cpb%d" % cpb in src) == looped and ("L_xj_col0" in src) == looped
+        mem = Memory((k + r) * S4)
+        mem.b[:k * S4] = full[:k].reshape(-1)
+        for c0 in range(0, ncols, cpb if looped else 1):
+            run_block(src, mem, 0, S4, k * S4, S4, chunk=c0, ncols=min(cpb, ncols - c0) if looped else 1)
+        assert np.array_equal(mem.b.reshape(k + r, S4)[k:], full[k:])
+    else:
+        er = np.zeros(k + r, bool)
+        er[bench_pattern(k, r)] = True
+        rcv = full.copy()
+        rcv[er] = 0
+        mem = Memory((k + r) * S4)
+        mem.b[:] = rcv.reshape(-1)
+        src = xj_source(k, r, er)
+        assert "cpb%d" % cpb in src
+        for c0 in range(0, ncols, cpb):
+            run_block(src, mem, 0, S4, 0, S4, chunk=c0, ncols=min(cpb, ncols - c0))
+        assert np.array_equal(mem.b.reshape(k + r, S4)[:k], full[:k])

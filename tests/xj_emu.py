@@ -61,6 +61,9 @@ class Wave:
         self.s[int(tok[1:])] = np.uint64(x & 0xFFFFFFFF)
 
     def vset(self, tok, x):
+        if tok.startswith("%["):  # a read-write VGPR operand ("+v"), e.g. the column offset of the loop
+            self.ops[tok[2:-1]] = np.asarray(x, dtype=np.uint64).astype(np.uint32)
+            return
         self.v[_vreg(tok)] = np.asarray(x, dtype=np.uint64).astype(np.uint32) if np.ndim(x) else np.uint32(x)
 
     def pair(self, tok):
@@ -73,13 +76,38 @@ class Wave:
         lo = int(m.group(1))
         return int(self.s[lo]) | ((int(self.s[lo + 1]) & 0xFFFF) << 32)
 
-    def run(self, lines, finish):
-        for ln in lines:
+    def run(self, lines, finish, entry=None):
+        """Executes `lines` from label `entry` (or the top) until its end or an s_setpc_b64 (the finish
+        blocks' return); labels, s_branch / s_cbranch_scc0/1 jumps within `lines`."""
+        labels = {ln[:-1]: i for i, ln in enumerate(lines) if ln.endswith(":")}
+        pc = labels[entry] if entry else 0
+        while pc < len(lines):
+            ln = lines[pc]
+            pc += 1
             if ln.endswith(":"):
                 continue
             op, _, rest = ln.partition(" ")
             a = [x.strip() for x in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
-            if op in ("s_nop", "s_waitcnt", "s_branch", "s_getpc_b64", "s_setpc_b64", "s_barrier"):
+            if op == "s_setpc_b64":
+                return
+            if op == "s_branch":
+                if entry is None and a[0] in labels:  # the role code's own jumps (the finish is entered by call)
+                    pc = labels[a[0]]
+                continue
+            if op in ("s_cbranch_scc0", "s_cbranch_scc1"):
+                if (self.scc != 0) == (op == "s_cbranch_scc1"):
+                    pc = labels[a[0]]
+                continue
+            if op in ("s_cmp_gt_u32", "s_cmp_lg_u32"):
+                x, y = self.val(a[0]), self.val(a[1])
+                self.scc = int(x > y) if op == "s_cmp_gt_u32" else int(x != y)
+                continue
+            if op == "s_sub_u32":
+                t = self.val(a[1]) - self.val(a[2])
+                self.scc = int(t < 0)
+                self.sset(a[0], t)
+                continue
+            if op in ("s_nop", "s_waitcnt", "s_getpc_b64", "s_barrier"):
                 continue
             # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
             if op == "s_set_gpr_idx_on":
@@ -108,7 +136,7 @@ class Wave:
                 self.vset(a[0], (self.val(a[1]).astype(np.int64) - self.val(a[2])) & 0xFFFFFFFF)
                 continue
             if op == "s_swappc_b64":
-                self.run(finish, finish)
+                self.run(finish, finish, self.call)
             elif op == "s_mov_b32":
                 self.sset(a[0], self.val(a[1]))
             elif op == "s_lshr_b64":
@@ -123,7 +151,8 @@ class Wave:
                 self.sset(a[0], self.val(a[1]) * self.val(a[2]))
             elif op == "s_add_u32":
                 if "L_" in a[2]:
-                    continue  # call-target arithmetic
+                    self.call = a[2].split("-")[0]  # call-target arithmetic: the finish entry label
+                    continue
                 t = self.val(a[1]) + self.val(a[2])
                 self.scc = t >> 32
                 self.sset(a[0], t)
@@ -183,7 +212,9 @@ class Wave:
                 hi = ((x >> 16).astype(np.uint16).view(np.int16) >> sh).view(np.uint16).astype(np.uint32)
                 self.vset(a[0], lo | (hi << np.uint32(16)))
             elif op == "global_load_dword":
-                addr = self.pair(a[2].split()[0]) + self.val(a[1]).astype(np.uint64)
+                mods = a[2].split()[1:]
+                off = sum(int(m.split(":")[1], 0) for m in mods if m.startswith("offset:"))
+                addr = self.pair(a[2].split()[0]) + self.val(a[1]).astype(np.uint64) + np.uint64(off)
                 self.vset(a[0], self.mem.load32(addr))
             elif op == "global_store_dword":
                 addr = self.pair(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
@@ -265,9 +296,10 @@ class Memory:
         self.b[idx.reshape(-1)] = np.ascontiguousarray(val, dtype="<u4").view(np.uint8)
 
 
-def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
+def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1):
     """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`
-    (LDS base address 0; each role's ring region at role * region bytes)."""
+    (LDS base address 0; each role's ring region at role * region bytes). Column-loop kernels (cpb > 1)
+    process `ncols` consecutive columns from `chunk`."""
     finish, roles = split_source(src)
     m = re.search(r"\(uint32_t\)role \* (\d+)u", src)
     region = int(m.group(1)) if m else 0
@@ -281,8 +313,9 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0):
     for w, lines in enumerate(roles):
         lb = w * region
         ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF,
-                   dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb,
+                   dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb, nc=ncols,
                    la=(lb + np.arange(64) * 4).astype(np.uint32))
+        ops["col"] = col.copy()
         wave = Wave(mem, ops)
         wave.lds = lds
         waves.append(wave)
