@@ -158,6 +158,7 @@ struct XjConfig {
                        // stripe; the next column's first input pair is loaded during the current column's
                        // last pair and finish (its ring slot stays clear of the finish registers), so only
                        // the block's first column waits for a cold load. Needs an even pair count (set_k).
+    int cpb_sync = 1;  // column loop: s_barrier per column
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
@@ -177,6 +178,7 @@ struct XjConfig {
         env("RS_XJ_KREG", kreg);
         env("RS_XJ_XCD", xcd);
         env("RS_XJ_CPB", cpb);
+        env("RS_XJ_CPB_SYNC", cpb_sync);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -210,7 +212,7 @@ struct XjConfig {
         std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
         std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
-        return cpb > 1 ? s + " cpb" + std::to_string(cpb) : s;
+        return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
 
@@ -439,11 +441,18 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.e("s_mov_b32 s55, 0x20000");
     }
     const int ngp = (K + 7) / 8;
-    const bool loop = C.cpb > 1;  // column loop (s39 = columns left, %[col] advances by 256 per column)
-    if (loop) E.e("s_mov_b32 s39, %[nc]");
+    // column loop: s39 = columns left; the block's columns are gridDim.x apart (s63 = that stride in bytes),
+    // so the blocks in flight still read neighbouring columns together; s[60:61] = source base + stride
+    const bool loop = C.cpb > 1;
+    if (loop) {
+        E.e("s_mov_b32 s39, %[nc]");
+        E.e("s_mov_b32 s63, %[cs]");
+        E.e("s_add_u32 s60, s32, s63");
+        E.e("s_addc_u32 s61, s33, 0");
+    }
     auto nload = [&](int g) { return g < ngp ? std::min(8, K - 8 * g) : 0; };
     // instruction lists of the loads of pair g (address arithmetic first, then the loads); `next_col`:
-    // the same pair of the following column (immediate offset 256)
+    // the same pair of the block's next column (base s[60:61])
     auto load_ops = [&](int g, bool next_col = false) {
         std::vector<std::string> ops;
         const int n = nload(g);
@@ -455,10 +464,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 ops.push_back(E.fmt("buffer_load_dword v%d, %s, s[48:51], s%d offen", dst, COL, 40 + j));
             } else {
                 ops.push_back(E.fmt("s_mul_i32 s62, s34, %d", slot));
-                ops.push_back(E.fmt("s_add_u32 s%d, s32, s62", 40 + 2 * j));
-                ops.push_back(E.fmt("s_addc_u32 s%d, s33, 0", 41 + 2 * j));
-                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
-                                    next_col ? " offset:256" : "", (C.nt & 1) ? " nt" : ""));
+                ops.push_back(E.fmt("s_add_u32 s%d, s%d, s62", 40 + 2 * j, next_col ? 60 : 32));
+                ops.push_back(E.fmt("s_addc_u32 s%d, s%d, 0", 41 + 2 * j, next_col ? 61 : 33));
+                ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
+                                    (C.nt & 1) ? " nt" : ""));
             }
         }
         return ops;
@@ -501,6 +510,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
     if (loop) {  // the first column's pair 0 is the block's only cold wait
         E.e("s_waitcnt vmcnt(0)");
         E.f("L_xj_col%d:", w);
+        if (C.cpb_sync) E.e("s_barrier");  // the roles of a column stay together (their loads share L1)
     }
     for (int g = 0; g < ngp; ++g) {
         std::vector<std::string> next, mid;
@@ -667,7 +677,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 E.f("global_store_dword %s, v%d, s[%d:%d]%s", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j,
                     (C.nt & 2) ? " nt" : "");
         }
-        E.f("v_add_u32 %s, 0x100, %s", COL, COL);
+        E.f("v_add_u32 %s, s63, %s", COL, COL);
         E.e("s_sub_u32 s39, s39, 1");
         E.e("s_cmp_lg_u32 s39, 0");
         E.f("s_cbranch_scc1 L_xj_col%d", w);
@@ -794,10 +804,10 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
                       "  const uint32_t col = bx * 256u + (threadIdx.x & 63u) * 4u;\n"
                     : "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[blockIdx.y] : (uint64_t)blockIdx.y;\n"
                       "  const uint64_t dstripe = a.dst_local ? (uint64_t)blockIdx.y : stripe;\n")
-          << (C.cpb > 1 ? "  const uint32_t c0 = blockIdx.x * " + std::to_string(C.cpb) + "u;\n"
-                          "  const uint32_t nc = a.nchunks - c0 < " + std::to_string(C.cpb) + "u ? a.nchunks - c0 : " +
-                              std::to_string(C.cpb) + "u;\n"
-                          "  uint32_t col = c0 * 256u + (threadIdx.x & 63u) * 4u;\n"
+          << (C.cpb > 1 ? "  const uint32_t nc0 = (a.nchunks - blockIdx.x + gridDim.x - 1) / gridDim.x;\n"
+                          "  const uint32_t nc = nc0 < " + std::to_string(C.cpb) + "u ? nc0 : " + std::to_string(C.cpb) + "u;\n"
+                          "  const uint32_t cs = gridDim.x * 256u;\n"
+                          "  uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"
                         : std::string(C.xcd ? "" : "  const uint32_t col = blockIdx.x * 256u + (threadIdx.x & 63u) * 4u;\n"))
           << ""
              "  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));\n"
@@ -817,7 +827,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
     for (int w = 0; w < roles; ++w) {
         o << "  case " << w << ": asm volatile(\n"
           << as_string_literals(role_block(C, w, cb, K, R, in_slots, out_slots))
-          << (C.cpb > 1 ? "  : [col] \"+v\"(col) : [la] \"v\"(la), [nc] \"s\"(nc), "
+          << (C.cpb > 1 ? "  : [col] \"+v\"(col) : [nc] \"s\"(nc), [cs] \"s\"(cs), "  // no LDS address: one VGPR fewer (3 waves/SIMD)
                         : "  : : [col] \"v\"(col), [la] \"v\"(la), ")
           << "[sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
              " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)\n  : "

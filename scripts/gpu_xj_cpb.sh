@@ -5,7 +5,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/cpb
-for i in 1 2; do for v in default 2 4 8 16; do
+for i in 1 2; do for v in default 2 4 16; do
   if [ "$v" = default ]; then E="-u RS_XJ_CPB"; else E="RS_XJ_CPB=$v"; fi
   env $E timeout -k 10 300 python -u bench.py --steps 20 --warmup 2 --no-cpu > gpurun_out/cpb/c3_${v}_${i}.log 2>&1 || exit 1
   echo "CPB=$v run=$i $(python3 -c "import json; l=[json.loads(x) for x in open('gpurun_out/cpb/c3_${v}_${i}.log') if x.startswith('{')][-1]; print(l['value'], l['encode_ms'], l['decode_ms'], l['parity'], l['roofline']['frac'])")" | tee -a gpurun_out/cpb/sweep.log

@@ -149,11 +149,18 @@ def test_xj_generation_knobs_match_oracle(k, r, knobs, monkeypatch):
     assert np.array_equal(mem.b.reshape(k + r, S)[k:], want[k:])
 
 
-@pytest.mark.parametrize("cpb,ncols", [(2, 4), (4, 4), (4, 3), (8, 1)])
+def _run_grid(src, mem, S4, dst_base, ncols, cpb):
+    """Every block of one stripe's grid: gx = ceil(ncols / cpb) blocks, block b walks columns b, b + gx, ..."""
+    gx = -(-ncols // cpb)
+    for b in range(gx):
+        run_block(src, mem, 0, S4, dst_base, S4, chunk=b, ncols=min(cpb, -(-(ncols - b) // gx)), gx=gx)
+
+
+@pytest.mark.parametrize("cpb,ncols", [(2, 4), (4, 4), (4, 3), (8, 1), (2, 5), (4, 6)])
 @pytest.mark.parametrize("k,r,kind", [(128, 32, "enc"), (128, 32, "bench"), (30, 17, "enc"), (16, 4, "enc"),
                                       (24, 8, "enc")])
 def test_xj_column_loop_matches_oracle(k, r, kind, cpb, ncols, monkeypatch):
-    """RS_XJ_CPB (a block loops over cpb consecutive 256-byte columns; the next column's first input pair
+    """RS_XJ_CPB (a block loops over cpb 256-byte columns gridDim.x apart; the next column's first input pair
     is loaded under the current column's last pair and finish, results stored per batch of 8): every
     column of the block is bit-exact vs the oracle, including a block with fewer columns than cpb and
     pair counts the loop does not take (K = 24: three pairs -> one column per block)."""
@@ -169,8 +176,7 @@ def test_xj_column_loop_matches_oracle(k, r, kind, cpb, ncols, monkeypatch):
         assert ("cpb%d" % cpb in src) == looped and ("L_xj_col0" in src) == looped
         mem = Memory((k + r) * S4)
         mem.b[:k * S4] = full[:k].reshape(-1)
-        for c0 in range(0, ncols, cpb if looped else 1):
-            run_block(src, mem, 0, S4, k * S4, S4, chunk=c0, ncols=min(cpb, ncols - c0) if looped else 1)
+        _run_grid(src, mem, S4, k * S4, ncols, cpb if looped else 1)
         assert np.array_equal(mem.b.reshape(k + r, S4)[k:], full[k:])
     else:
         er = np.zeros(k + r, bool)
@@ -181,6 +187,5 @@ def test_xj_column_loop_matches_oracle(k, r, kind, cpb, ncols, monkeypatch):
         mem.b[:] = rcv.reshape(-1)
         src = xj_source(k, r, er)
         assert "cpb%d" % cpb in src
-        for c0 in range(0, ncols, cpb):
-            run_block(src, mem, 0, S4, 0, S4, chunk=c0, ncols=min(cpb, ncols - c0))
+        _run_grid(src, mem, S4, 0, ncols, cpb)
         assert np.array_equal(mem.b.reshape(k + r, S4)[:k], full[:k])

@@ -296,10 +296,10 @@ class Memory:
         self.b[idx.reshape(-1)] = np.ascontiguousarray(val, dtype="<u4").view(np.uint8)
 
 
-def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1):
+def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, gx=1):
     """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`
     (LDS base address 0; each role's ring region at role * region bytes). Column-loop kernels (cpb > 1)
-    process `ncols` consecutive columns from `chunk`."""
+    process `ncols` columns from `chunk`, `gx` (the grid's x size) columns apart."""
     finish, roles = split_source(src)
     m = re.search(r"\(uint32_t\)role \* (\d+)u", src)
     region = int(m.group(1)) if m else 0
@@ -313,7 +313,7 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1):
     for w, lines in enumerate(roles):
         lb = w * region
         ops = dict(col=col, sl=src_base & 0xFFFFFFFF, sh=src_base >> 32, dl=dst_base & 0xFFFFFFFF,
-                   dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb, nc=ncols,
+                   dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb, nc=ncols, cs=gx * 256,
                    la=(lb + np.arange(64) * 4).astype(np.uint32))
         ops["col"] = col.copy()
         wave = Wave(mem, ops)
@@ -321,7 +321,7 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1):
         waves.append(wave)
         seg = [[]]  # the block's waves run in lockstep between s_barriers
         for ln in lines:
-            if ln == "s_barrier":
+            if ln == "s_barrier" and "L_xj_col" not in src:  # column-loop roles share nothing: barrier = no-op
                 seg.append([])
             else:
                 seg[-1].append(ln)
