@@ -587,6 +587,7 @@ struct rsg_codec {
     void* d_reenc = nullptr;  // re-encode decode scratch: [chunk][r][S] (G_U u + y)
     size_t reenc_cap = 0;
     int m16_reenc = 1;  // option m16_reenc: 0 keeps full-pattern decodes on the plain route
+    int m16_cs_col = 1024;  // option m16_cs_col: column width of the route kernels' blocks (1024 or 256 bytes)
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
     size_t goff_cap[2] = {0, 0};
@@ -1156,6 +1157,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "m16_cs_col")) {  // k_cs16 / k_bs16 block layout (results identical)
+        if (value != 256 && value != 1024) return RS_ERR_INVALID;
+        c->m16_cs_col = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "m16_reenc")) {  // decode patterns built from now on
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->m16_reenc = int(value);
@@ -1224,7 +1230,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
     a.ngroups = cs.ngroups;
     a.ntiles = cs.ntiles;
-    a.nchunks = int64_t(S) / 1024;
+    a.colw = c->m16_cs_col == 1024 ? 1024 : 256;
+    a.nchunks = int64_t(S) / a.colw;
+    const uint64_t waves_per_unit = uint64_t(a.colw / 256);  // per tile
     if (cs.kind == 1) {  // straight into the outputs
         a.src = src;
         a.dst = dst;
@@ -1232,7 +1240,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst_sym = dst_sym;
         a.units = int64_t(n_stripes) * a.nchunks;
         HIP_TRY(launch_bs16(a, st));
-        const uint64_t steps = uint64_t(a.units) * 4 * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
         c->work_valu += steps * kValu_bs16;
         c->work_salu += steps * kSalu_bs16;
         c->last_kernel = "bs16";
@@ -1250,7 +1258,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst_stripe = per;
         a.units = cn * a.nchunks;
         HIP_TRY(launch_cs16(a, st));
-        const uint64_t steps = uint64_t(a.units) * 4 * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
         c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
         c->work_salu += steps * kSalu_cs16a;
         if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,

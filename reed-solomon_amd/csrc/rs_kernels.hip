@@ -736,14 +736,37 @@ __device__ __forceinline__ void cs16_finish(const Cs16Args& a, const u32x16& u, 
     }
 }
 
+// Block -> (tile, launch-local stripe, lane's column byte) of k_cs16 / k_bs16; false: nothing to do.
+// XCD-aware: consecutive slots on one XCD (workgroup b runs on XCD b % 8) walk the tiles of one unit.
+// colw 1024: block = 4 waves on the four 256-byte quarters of a 1 KiB unit, one tile per block.
+// colw 256: block = 4 waves on one 256-byte unit, tiles 4 (b / 8 % ntb) + wave: a unit's tiles are
+// ntb = ceil(ntiles / 4) consecutive slots, few enough to be resident together, so they sweep the
+// unit's input groups in step and the XCD's L2 serves the repeats (HBM traffic near the inputs' size).
+__device__ __forceinline__ bool cs16_unit(const Cs16Args& a, int& tile, int64_t& local, uint32_t& col) {
+    const int64_t slot = blockIdx.x >> 3;
+    int64_t unit;
+    if (a.colw == 1024) {
+        tile = int(slot % a.ntiles);
+        unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
+        col = uint32_t(threadIdx.x * 4u);
+    } else {
+        const int ntb = (a.ntiles + 3) >> 2;
+        tile = int(slot % ntb) * 4 + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+        unit = (slot / ntb) * 8 + (blockIdx.x & 7);
+        col = uint32_t((threadIdx.x & 63u) * 4u);
+    }
+    if (unit >= a.units || tile >= a.ntiles) return false;
+    local = unit / a.nchunks;
+    col += uint32_t((unit - local * a.nchunks) * a.colw);
+    return true;
+}
+
 __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
-    const int64_t slot = blockIdx.x >> 3;  // XCD-aware: the tiles of one unit run back to back on one XCD
-    const int tile = int(slot % a.ntiles);
-    const int64_t unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
-    if (unit >= a.units) return;
-    const int64_t local = unit / a.nchunks;
+    int tile;
+    int64_t local;
+    uint32_t col;
+    if (!cs16_unit(a, tile, local, col)) return;
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const uint32_t col = uint32_t((unit - local * a.nchunks) * 1024) + threadIdx.x * 4u;
     const uint64_t base = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
     // raw buffer V#: base, stride 0, num_records = the inputs' byte range, 32-bit data format
     const u32x4s rsrc = {uint32_t(base), uint32_t(base >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
@@ -796,13 +819,11 @@ __device__ __forceinline__ void bs16_step(const uint32_t* cp, const uint32_t* gp
 }
 
 __global__ void __launch_bounds__(256) k_bs16(Cs16Args a) {
-    const int64_t slot = blockIdx.x >> 3;
-    const int tile = int(slot % a.ntiles);
-    const int64_t unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
-    if (unit >= a.units) return;
-    const int64_t local = unit / a.nchunks;
+    int tile;
+    int64_t local;
+    uint32_t col;
+    if (!cs16_unit(a, tile, local, col)) return;
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const uint32_t col = uint32_t((unit - local * a.nchunks) * 1024) + threadIdx.x * 4u;
     const uint64_t base = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
     const u32x4s rsrc = {uint32_t(base), uint32_t(base >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
     const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 64;  // [tile][ngroups + 2][4][16]
@@ -833,7 +854,7 @@ __global__ void __launch_bounds__(256) k_bs16(Cs16Args a) {
 
 hipError_t launch_bs16(const Cs16Args& a, hipStream_t st) {
     if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
-    const int64_t blocks = (a.units + 7) / 8 * 8 * a.ntiles;
+    const int64_t blocks = (a.units + 7) / 8 * 8 * (a.colw == 1024 ? a.ntiles : (a.ntiles + 3) / 4);
     if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -852,7 +873,7 @@ hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t
 
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st) {
     if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
-    const int64_t blocks = (a.units + 7) / 8 * 8 * a.ntiles;
+    const int64_t blocks = (a.units + 7) / 8 * 8 * (a.colw == 1024 ? a.ntiles : (a.ntiles + 3) / 4);
     if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_cs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
     return hipGetLastError();

@@ -124,8 +124,10 @@ struct Cs16Args {
     const uint16_t* expt;     // [65536] alpha^e, e < 65535
     uint32_t nblog[16];       // log of the GF(2^16) normal basis elements nb_t
     int32_t ngroups, ntiles;  // ngroups even (padded with empty groups)
-    int64_t nchunks;          // 1 KiB column chunks per symbol
+    int64_t nchunks;          // columns (colw bytes) per symbol
     int64_t units;            // n_stripes * nchunks
+    int32_t colw;             // 1024: block = 4 waves on one 1 KiB column, one tile; 256: block = 4 waves on
+                              // one 256-byte column, 4 consecutive tiles (the tiles of a column run together)
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);

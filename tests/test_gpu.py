@@ -524,13 +524,14 @@ def test_xor_kernel_shapes_vs_oracle(k, r):
 
 @pytest.mark.parametrize("k,r,S", [(250, 33, 1024), (300, 64, 2048 + 40), (200, 65, 1024 + 1000), (1000, 100, 2048),
                                    (400, 129, 3072 + 4), (2000, 100, 1024)])
-@pytest.mark.parametrize("route", [0, 1])
-def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
+@pytest.mark.parametrize("route,col", [(0, 1024), (1, 1024), (1, 256)])
+def test_m16_kernel_shapes_vs_oracle(k, r, S, route, col):
     """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
     1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle. Two
     stripes make small grids, so every case also runs split-K (k=2000: 31 input slices). Route 0: the
     dense kernel; route 1: the syndrome route where it applies (K >= 64, whole 1 KiB chunks; other
-    launches of a route plan fall back to its dense plan)."""
+    launches of a route plan fall back to its dense plan); col: the route kernels' block layout
+    (option m16_cs_col, 1 KiB column per tile or 4 tiles per 256-byte column)."""
     rng = np.random.default_rng(k + 7 * r + S)
     n = 2
     host = np.zeros((n, k + r, S), np.uint8)
@@ -539,6 +540,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route):
     codec = rs_amd.Codec(k, r)
     codec.set_option("m16_route", route)
     codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route from their first launch
+    codec.set_option("m16_cs_col", col)
     assert codec.subfield == 16
     codec.encode(dev)
     torch.cuda.synchronize()
