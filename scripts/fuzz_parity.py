@@ -100,6 +100,7 @@ def one(family):
     codec = rs_amd.Codec(k, r, **kw)
     if family in ("route", "reenc"):
         codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route at once
+        codec.set_option("m16_cs_col", int(rng.choice([256, 1024])))  # route kernels' block layout
     codec.encode(dev)
     torch.cuda.synchronize()
     enc_kernel = codec.last_kernel
