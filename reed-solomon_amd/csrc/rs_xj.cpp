@@ -159,6 +159,8 @@ struct XjConfig {
                        // last pair and finish (its ring slot stays clear of the finish registers), so only
                        // the block's first column waits for a cold load. Needs an even pair count (set_k).
     int cpb_sync = 1;  // column loop: s_barrier per column
+    int early = 0;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
+                       // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {
             if (const char* e = std::getenv(n)) v = std::atoi(e);
@@ -179,6 +181,7 @@ struct XjConfig {
         env("RS_XJ_XCD", xcd);
         env("RS_XJ_CPB", cpb);
         env("RS_XJ_CPB_SYNC", cpb_sync);
+        env("RS_XJ_EARLY", early);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -191,6 +194,7 @@ struct XjConfig {
         horner = horner ? 1 : 0;
         cpb = std::max(1, std::min(64, cpb));
         if (lfin || lds || share || spread || xcd || buffer || ring != 2) cpb = 1;
+        early = (early && !lds && !share && !spread && ring == 2 && cpb == 1) ? 1 : 0;
     }
     // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
     void set_k(int K) {
@@ -212,6 +216,7 @@ struct XjConfig {
         std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
         std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
+        if (early) s += " early";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -504,7 +509,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.f("s_waitcnt vmcnt(%d)", pend);
         for (auto& op : ds_ops(0)) E.e(op);
     } else {
-        for (int g = 0; g < ahead; ++g)
+        for (int g = 0; g < ahead + C.early; ++g)
             for (auto& op : load_ops(g)) E.e(op);
     }
     if (loop) {  // the first column's pair 0 is the block's only cold wait
@@ -525,11 +530,12 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
             if (g + D < ngp)  // into the slot pair g has left (its ds_reads completed above)
                 for (auto& op : dma_ops(g + D)) mid.push_back(op);
         } else {
-            // loads issued so far beyond pair g: pairs g+1 .. g+ahead-1 (g+ahead is issued below)
+            // loads issued so far beyond pair g: pairs g+1 .. g+ahead-1 (g+ahead is issued below); early:
+            // pair g+1 was issued inside pair g-1, pair g+2 goes out inside this pair's rows
             int pending = 0;
-            for (int x = g + 1; x < g + ahead; ++x) pending += nload(x);
-            next = load_ops(g + ahead);
-            if (!C.spread) {
+            for (int x = g + 1; x < g + ahead + C.early; ++x) pending += nload(x);
+            if (!C.early) next = load_ops(g + ahead);
+            if (!C.spread && !C.early) {
                 for (auto& op : next) E.e(op);
                 pending += nload(g + ahead);
             }
@@ -623,22 +629,29 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         if (C.ablate & 4) body.clear();
         for (auto& op : mid) body.push_back(op);  // LDS ring: next pair's reads + refills after the tables
         const size_t nbuild = body.size();
+        std::vector<std::string> rest;  // early: rows that read only built entries, after the next loads
         for (int t = 0; t < 8; ++t)
             for (int q = 0; q < nq; ++q) {
                 const int a = pat[q][t][0], b = pat[q][t][1], acc = C.acc(q, t);
                 if ((!a && !b) || (C.ablate & 2)) continue;
+                const bool raw = __builtin_popcount(a) == 1 || __builtin_popcount(b) == 1;
+                std::vector<std::string>& dst = (C.early && !raw) ? rest : body;
                 if (!init[q][t]) {
                     if (a && b)
-                        body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, reg(0, a), reg(1, b)));
+                        dst.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, reg(0, a), reg(1, b)));
                     else
-                        body.push_back(E.fmt("v_mov_b32 v%d, v%d", acc, a ? reg(0, a) : reg(1, b)));
+                        dst.push_back(E.fmt("v_mov_b32 v%d, v%d", acc, a ? reg(0, a) : reg(1, b)));
                     init[q][t] = true;
                 } else if (a && b) {
-                    body.push_back(E.fmt("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", acc, acc, reg(0, a), reg(1, b)));
+                    dst.push_back(E.fmt("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", acc, acc, reg(0, a), reg(1, b)));
                 } else {
-                    body.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, a ? reg(0, a) : reg(1, b), acc));
+                    dst.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, a ? reg(0, a) : reg(1, b), acc));
                 }
             }
+        if (C.early) {  // this pair's raw inputs are dead now: pair g+2 into their ring slot, then the rest
+            for (auto& op : load_ops(g + 2)) body.push_back(op);
+            for (auto& op : rest) body.push_back(op);
+        }
         if (C.spread && !next.empty()) {
             // the next pair's loads go into this pair's row stream (after the table build: their ring
             // slot was last read by the previous pair), one every few rows

@@ -39,6 +39,10 @@ class Wave:
         self.scc = 0
         self.m0 = 0
         self.lds = None  # np.uint8 array shared by the block's waves
+        # vector-memory counter model: loads land in their VGPRs only when an s_waitcnt vmcnt(N) retires
+        # them (in issue order, stores counted too); touching a VGPR whose load has not been retired is
+        # a missing or too-loose wait and raises
+        self.vm = []  # [(vgpr or None, data)]
         self.mem = mem
         self.ops = operands  # name -> int or np.ndarray (VGPR operand)
 
@@ -76,6 +80,21 @@ class Wave:
         lo = int(m.group(1))
         return int(self.s[lo]) | ((int(self.s[lo + 1]) & 0xFFFF) << 32)
 
+    def retire(self, n):
+        """s_waitcnt vmcnt(n): retire the oldest vector-memory operations until at most n are left."""
+        while len(self.vm) > n:
+            r, data = self.vm.pop(0)
+            if isinstance(r, tuple):  # LDS DMA
+                self.lds[r[1]] = data
+            elif r is not None:
+                self.v[r] = data
+
+    def check_vgprs(self, ln):
+        busy = {r for r, _ in self.vm if isinstance(r, int)}
+        if busy:
+            for tok in re.findall(r"\bv(\d+)\b", ln):
+                assert int(tok) not in busy, f"v{tok} used before its load was waited for: {ln}"
+
     def run(self, lines, finish, entry=None):
         """Executes `lines` from label `entry` (or the top) until its end or an s_setpc_b64 (the finish
         blocks' return); labels, s_branch / s_cbranch_scc0/1 jumps within `lines`."""
@@ -88,6 +107,12 @@ class Wave:
                 continue
             op, _, rest = ln.partition(" ")
             a = [x.strip() for x in re.split(r",\s*(?![^\[]*\])", rest)] if rest else []
+            if op == "s_waitcnt":
+                m = re.search(r"vmcnt\((\d+)\)", rest)
+                if m:
+                    self.retire(int(m.group(1)))
+                continue
+            self.check_vgprs(ln)
             if op == "s_setpc_b64":
                 return
             if op == "s_branch":
@@ -107,7 +132,7 @@ class Wave:
                 self.scc = int(t < 0)
                 self.sset(a[0], t)
                 continue
-            if op in ("s_nop", "s_waitcnt", "s_getpc_b64", "s_barrier"):
+            if op in ("s_nop", "s_getpc_b64", "s_barrier"):
                 continue
             # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
             if op == "s_set_gpr_idx_on":
@@ -215,17 +240,18 @@ class Wave:
                 mods = a[2].split()[1:]
                 off = sum(int(m.split(":")[1], 0) for m in mods if m.startswith("offset:"))
                 addr = self.pair(a[2].split()[0]) + self.val(a[1]).astype(np.uint64) + np.uint64(off)
-                self.vset(a[0], self.mem.load32(addr))
+                self.vm.append((_vreg(a[0]), self.mem.load32(addr)))
             elif op == "global_store_dword":
                 addr = self.pair(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
                 self.mem.store32(addr, self.val(a[1]))
+                self.vm.append((None, None))
             elif op == "buffer_load_dword" and ln.endswith(" lds"):
                 # LDS DMA: a[0] = voffset, a[1] = V#, a[2] = "soffset offen lds"
                 addr = self.vsharp(a[1]) + self.val(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
                 data = self.mem.load32(addr)
                 dst = self.m0 + 4 * np.arange(64)
                 idx = dst[:, None] + np.arange(4)[None, :]
-                self.lds[idx.reshape(-1)] = data.astype("<u4").view(np.uint8)
+                self.vm.append((("lds", idx.reshape(-1)), data.astype("<u4").view(np.uint8)))  # lands at retire
             elif op == "ds_write_b32":
                 base, off = a[0], 0
                 if " " in a[1]:
@@ -255,10 +281,11 @@ class Wave:
                 nrec = int(self.s[int(re.match(r"s\[(\d+):", a[2]).group(1)) + 2])
                 inb = voff < np.uint64(nrec)
                 data = self.mem.load32(np.where(inb, addr, np.uint64(0)))
-                self.vset(a[0], np.where(inb, data, np.uint32(0)))
+                self.vm.append((_vreg(a[0]), np.where(inb, data, np.uint32(0)).astype(np.uint32)))
             elif op == "buffer_store_dword":
                 addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + self.val(a[1]).astype(np.uint64)
                 self.mem.store32(addr, self.val(a[0]))
+                self.vm.append((None, None))
             else:
                 raise NotImplementedError(ln)
 
