@@ -159,7 +159,7 @@ struct XjConfig {
                        // last pair and finish (its ring slot stays clear of the finish registers), so only
                        // the block's first column waits for a cold load. Needs an even pair count (set_k).
     int cpb_sync = 1;  // column loop: s_barrier per column
-    int early = 0;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
+    int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
         auto env = [](const char* n, int& v) {

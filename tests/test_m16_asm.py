@@ -60,6 +60,7 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     w.v[72:136] = acc0
     w.s[90], w.s[91] = 1024, 0
     w.run(["s_load_dwordx16 s[40:55], s[90:91], 0x0"] + text.splitlines(), [])  # the kernel's first-plane load
+    w.retire(0)  # the next step (or the kernel) waits for these loads before use
     lo, hi = x & 0xFFFF, x >> 16
     for p in range(64):
         want = (gf_mul(lo, coef[p]) | (gf_mul(hi, coef[p]) << 16)) ^ acc0[p]
@@ -106,6 +107,7 @@ def test_m8_v1_step_matches_gf256_multiply(tmp_path):
     w.v[40:72] = acc0
     w.s[90], w.s[91] = 1024, 0
     w.run(text.splitlines(), [])
+    w.retire(0)  # the next step (or the kernel) waits for these loads before use
     for p in range(32):
         assert np.array_equal(w.v[40 + p], gf256_mul_bytes(y, coef[p]) ^ acc0[p]), p
 
@@ -158,6 +160,7 @@ def test_cs16_step_circulant_xor(tmp_path, variant):
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
         w.s[76:92] = offs.astype(np.uint64)
         w.run([f"s_load_dwordx16 s[{cur}:{cur + 15}], s[100:101], 0x0"] + text.splitlines(), [])
+        w.retire(0)  # the next step (or the kernel) waits for these loads before use
         for c in range(4):
             for t in range(16):
                 want = acc0[16 * c + t].copy()
@@ -212,6 +215,7 @@ def test_bs16_step_binary_accumulation(tmp_path):
     w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
     w.s[76:92] = offs.astype(np.uint64)
     w.run(["s_load_dwordx16 s[40:55], s[100:101], 0x0"] + text.splitlines(), [])
+    w.retire(0)  # the next step (or the kernel) waits for these loads before use
     for c in range(4):
         for t in range(16):
             want = acc0[16 * c + t].copy()
