@@ -301,16 +301,25 @@ struct DevPlan {
     hipStream_t built_on = nullptr;
     void* h_stage = nullptr;
     size_t stage_cap = 0;
-    // the last launch: `used` recorded on `used_on` after it. A plan launched on more than one stream
-    // is released with hipFree (device-synchronous) instead of to the pool
+    // the guard that keeps the memory from being reused before the last launch is done: `used`, recorded
+    // on the launch stream after the first 16 launches and then after every 64th (a record costs
+    // microseconds of host time, which small launches would feel every call; recording at release
+    // instead is unsafe, as the caller's stream may be gone by then). A plan released with launches
+    // after its last record waits for the device; one launched on more than one stream is released
+    // with hipFree (device-synchronous) instead of to the pool.
     hipEvent_t used = nullptr;
     hipStream_t used_on = nullptr;
-    bool multi_stream = false;
+    bool launched = false, multi_stream = false;
+    int64_t launches = 0, recorded = 0;  // launches so far / covered by `used`
     int note_use(hipStream_t st) {
-        if (used_on && used_on != st) multi_stream = true;
+        if (launched && used_on != st) multi_stream = true;
         used_on = st;
-        if (!used) HIP_TRY(hipEventCreateWithFlags(&used, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(used, st));
+        launched = true;
+        if (++launches <= 16 || launches % 64 == 0) {
+            if (!used) HIP_TRY(hipEventCreateWithFlags(&used, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(used, st));
+            recorded = launches;
+        }
         return 0;
     }
     // called before a launch on stream st: orders it after the build, releases the build's resources
@@ -338,7 +347,11 @@ struct DevPlan {
             (void)hipEventDestroy(ready);
         }
         pool_host_release(h_stage, stage_cap);
-        if (used && hipEventQuery(used) == hipSuccess) {  // last launch done: no guard to carry
+        if (blob && !multi_stream && recorded != launches) {  // launches past the guard: wait for them
+            (void)hipDeviceSynchronize();
+            if (used) (void)hipEventDestroy(used);
+            used = nullptr;
+        } else if (used && hipEventQuery(used) == hipSuccess) {  // last launch done: no guard to carry
             (void)hipEventDestroy(used);
             used = nullptr;
         }
