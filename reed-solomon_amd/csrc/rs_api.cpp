@@ -315,12 +315,19 @@ struct DevPlan {
         if (launched && used_on != st) multi_stream = true;
         used_on = st;
         launched = true;
-        if (++launches <= 16 || launches % 64 == 0) {
-            if (!used) HIP_TRY(hipEventCreateWithFlags(&used, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(used, st));
-            recorded = launches;
-        }
+        if (++launches <= 16 || launches % 64 == 0) return record_guard(st);
         return 0;
+    }
+    int record_guard(hipStream_t st) {
+        if (!used) HIP_TRY(hipEventCreateWithFlags(&used, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(used, st));
+        recorded = launches;
+        return 0;
+    }
+    // before a release from a call on stream st (cache eviction): a plan whose launches all ran on st
+    // gets its guard there -- st is alive, and it orders after them -- instead of a device wait
+    void guard_before_release(hipStream_t st) {
+        if (launched && !multi_stream && recorded != launches && used_on == st) (void)record_guard(st);
     }
     // called before a launch on stream st: orders it after the build, releases the build's resources
     // once the build is complete
@@ -1513,7 +1520,11 @@ static int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPla
         std::unique_ptr<DevPlan> p;
         if (int rc = make_plan(c, is_erased, p, st)) return rc;
         if (c->dec_lru.size() >= 16) {
-            c->dec.erase(c->dec_lru.front());
+            auto old = c->dec.find(c->dec_lru.front());
+            if (old != c->dec.end()) {
+                old->second->guard_before_release(st);
+                c->dec.erase(old);
+            }
             c->dec_lru.erase(c->dec_lru.begin());
         }
         c->dec_lru.push_back(key);
