@@ -60,8 +60,8 @@ def measured_traffic(kernel, cfg):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=150,
-                    help="timed steps (default 150: ~6.6 s of back-to-back GPU work at C3, so utilisation samplers see it)")
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (default 100: ~4.4 s of back-to-back GPU work at C3, so utilisation samplers see it)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--r", type=int, default=32)
