@@ -14,6 +14,9 @@
 //               s62 scratch, s63 saved m0; the column offset is the compiler's %[col] VGPR
 //   The finish block (Horner in alpha^-1 over the 16 z-coordinates, chains interleaved 8 at a time) is
 //   emitted once at the kernel entry and entered by s_swappc_b64 from every role.
+//   Loads (early issue, the default): pairs 0 and 1 go out first; inside pair g, the rows that read one of
+//   the pair's raw inputs run first, then pair g+2's loads go into the freed ring slot, then the rows that
+//   read only built table entries -- so every wait is for loads issued about 1.5 pairs earlier.
 //   Experimental forms (knobs in XjConfig, measured in DESIGN.md section 5): LDS-DMA input ring,
 //   buffer addressing, spread loads, Horner in alpha, LDS-table finish (persistent grid), LDS table
 //   sharing between roles.
