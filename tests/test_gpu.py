@@ -956,3 +956,37 @@ def test_new_pattern_does_not_stall_other_streams():
     finally:
         hip.hipStreamDestroy(sa)
         hip.hipStreamDestroy(sb)
+
+
+@pytest.mark.parametrize("k,r", [(4, 2), (128, 32), (300, 60)])
+def test_edge_empty_batches_and_no_erasures(k, r):
+    """Edge cases of the batched API: zero stripes (encode / decode return 0 and touch nothing), a decode
+    with no erasure (t = 0: nothing to restore, the stripes stay bit-identical), and a pattern that loses
+    only repair symbols (the reference restores information symbols only, so nothing changes either)."""
+    S = 2048
+    rng = np.random.default_rng(k + r)
+    host = np.zeros((3, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (3, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    assert codec.encode(dev[:0]) == 0
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    enc = dev.cpu().numpy()
+    want = host.copy()
+    for s in range(3):
+        assert oracle_encode(k, r, want[s]) == 0
+    assert np.array_equal(enc, want)
+    none = np.zeros(k + r, bool)
+    assert codec.decode(dev, none) == 0
+    rep_only = none.copy()
+    rep_only[k + rng.choice(r, min(r, 2), replace=False)] = True
+    poisoned = enc.copy()
+    poisoned[:, rep_only] = 0
+    dev.copy_(torch.from_numpy(poisoned))
+    assert codec.decode(dev, rep_only) == 0
+    er = none.copy()
+    er[:min(k, r)] = True
+    assert codec.decode(dev[:0], er) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), poisoned)
