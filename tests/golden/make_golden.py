@@ -76,6 +76,11 @@ def cases():
     add("c5_dec_rand_2k", "decode", 4096, 1024, 2048, 1, 1024, rand_pattern(4096, 1024, 1024, 9))
     add("c5_dec_t32_1k", "decode", 4096, 1024, 1024, 1, 32, rand_pattern(4096, 1024, 32, 10, info_only=True))
     add("c5_dec_noncw_1k", "decode_noncw", 4096, 1024, 1024, 1, 300, rand_pattern(4096, 1024, 300, 11))
+    # the largest codes (k + r = 65535) on whole 1 KiB columns: the GF(2^16) syndrome route and the
+    # re-encode decode at maximum n; sha256 of the outputs
+    add("max_n_route_enc_1k", "encode", 64511, 1024, 1024, 1)
+    add("max_n_route_dec_1k", "decode", 64511, 1024, 1024, 1, 1024,
+        rand_pattern(64511, 1024, 1024, 12, info_only=True))
     # example.c shape: 10-byte symbols (5 words, not a multiple of 16 B)
     add("ex_enc", "encode", 100, 10, 10, 1)
     add("ex_dec", "decode", 100, 10, 10, 1, 10, rand_pattern(100, 10, 10, 4))

@@ -27,7 +27,7 @@ def _pad(S):
     return (S + 15) // 16 * 16
 
 
-def run_case_gpu(c, variant):
+def run_case_gpu(c, variant, options=None):
     k, r, S, n = c["k"], c["r"], c["S"], c["n"]
     P = _pad(S)
     host = np.zeros((n, k + r, P), np.uint8)
@@ -37,6 +37,8 @@ def run_case_gpu(c, variant):
         host[s, :, :S] = buf
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r, **VARIANTS[variant])
+    for name, value in (options or {}).items():
+        codec.set_option(name, value)
     st = torch.cuda.current_stream()
     base = dev.data_ptr()
     stride = (k + r) * P
@@ -71,6 +73,14 @@ def test_golden_batch_api(name, variant):
     assert rc == c["rc"], (rc, kern)
     if name.startswith("c5_") and name.endswith(("_1k", "_2k")):  # full 1 KiB chunks: the production GF(2^16) path
         assert kern in M16_PRODUCTION or kern.startswith("cs16+"), kern
+    if name.startswith("max_n_route"):  # k + r = 65535 on whole 1 KiB columns
+        # encode: the syndrome route; decode: a new pattern's first 64 MiB launch runs the dense plan
+        # (m16_route_min_bytes), so the route is pinned by a second run that takes it at once
+        assert kern.startswith("cs16+") if c["op"] == "encode" else kern in M16_PRODUCTION, kern
+        if c["op"] == "decode":
+            rc2, out2, kern2, _ = run_case_gpu(c, variant, {"m16_route_min_bytes": 0})
+            assert rc2 == c["rc"] and kern2.startswith("cs16+bs16+xor+"), kern2  # the re-encode decode
+            check_golden(c, out2)
     check_golden(c, out)
 
 

@@ -63,7 +63,9 @@ def test_positions_survey_fingerprints():
     assert p[10:].tolist() == [4369, 8738, 17476, 34952]
 
 
-CASES = [c["name"] for c in manifest()["cases"] if c["op"] not in EXTRA_OPS]
+# max_n_route_*: k + r = 65535 at 1 KiB symbols, a minute of CPU per case; pinned by the reference's
+# own outputs (the golden) and checked on the GPU only
+CASES = [c["name"] for c in manifest()["cases"] if c["op"] not in EXTRA_OPS and not c["name"].startswith("max_n_route")]
 EXTRA = [c["name"] for c in manifest()["cases"] if c["op"] in EXTRA_OPS]
 FAST = [n for n in CASES if not n.startswith(("gmat_4096", "c5_", "c3_dec_bench_64k"))]
 SLOW = [n for n in CASES if n not in FAST]
