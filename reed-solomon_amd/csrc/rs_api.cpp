@@ -607,7 +607,7 @@ struct rsg_codec {
     void* d_reenc = nullptr;  // re-encode decode scratch: [chunk][r][S] (G_U u + y)
     size_t reenc_cap = 0;
     int m16_reenc = 1;  // option m16_reenc: 0 keeps full-pattern decodes on the plain route
-    int m16_cs_col = 1024;  // option m16_cs_col: column width of the route kernels' blocks (1024 or 256 bytes)
+    int m16_cs_col = 256;  // option m16_cs_col: the route kernels' block layout (256 or 1024 bytes, rs_kernels.hip)
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
     size_t goff_cap[2] = {0, 0};

@@ -739,9 +739,11 @@ __device__ __forceinline__ void cs16_finish(const Cs16Args& a, const u32x16& u, 
 // Block -> (tile, launch-local stripe, lane's column byte) of k_cs16 / k_bs16; false: nothing to do.
 // XCD-aware: consecutive slots on one XCD (workgroup b runs on XCD b % 8) walk the tiles of one unit.
 // colw 1024: block = 4 waves on the four 256-byte quarters of a 1 KiB unit, one tile per block.
-// colw 256: block = 4 waves on one 256-byte unit, tiles 4 (b / 8 % ntb) + wave: a unit's tiles are
-// ntb = ceil(ntiles / 4) consecutive slots, few enough to be resident together, so they sweep the
-// unit's input groups in step and the XCD's L2 serves the repeats (HBM traffic near the inputs' size).
+// colw 256: every wave is one (256-byte unit, tile) pair of the flattened sequence unit * ntiles +
+// tile, 4 consecutive pairs per block (no idle waves when ntiles % 4 != 0), and XCD x runs the
+// contiguous 1/8 of the blocks [x nb / 8, (x + 1) nb / 8) in order (nb = gridDim.x, a multiple of 8): the
+// ~32 blocks of a unit run together on one XCD and sweep its input groups in step, so the XCD's L2
+// serves the repeats.
 __device__ __forceinline__ bool cs16_unit(const Cs16Args& a, int& tile, int64_t& local, uint32_t& col) {
     const int64_t slot = blockIdx.x >> 3;
     int64_t unit;
@@ -750,9 +752,10 @@ __device__ __forceinline__ bool cs16_unit(const Cs16Args& a, int& tile, int64_t&
         unit = (slot / a.ntiles) * 8 + (blockIdx.x & 7);
         col = uint32_t(threadIdx.x * 4u);
     } else {
-        const int ntb = (a.ntiles + 3) >> 2;
-        tile = int(slot % ntb) * 4 + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-        unit = (slot / ntb) * 8 + (blockIdx.x & 7);
+        const int64_t lb = int64_t(blockIdx.x & 7) * (gridDim.x >> 3) + slot;
+        const int64_t wv = lb * 4 + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+        unit = wv / a.ntiles;
+        tile = int(wv - unit * a.ntiles);
         col = uint32_t((threadIdx.x & 63u) * 4u);
     }
     if (unit >= a.units || tile >= a.ntiles) return false;
@@ -854,7 +857,7 @@ __global__ void __launch_bounds__(256) k_bs16(Cs16Args a) {
 
 hipError_t launch_bs16(const Cs16Args& a, hipStream_t st) {
     if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
-    const int64_t blocks = (a.units + 7) / 8 * 8 * (a.colw == 1024 ? a.ntiles : (a.ntiles + 3) / 4);
+    const int64_t blocks = a.colw == 1024 ? (a.units + 7) / 8 * 8 * a.ntiles : (a.units * a.ntiles + 31) / 32 * 8;
     if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
     return hipGetLastError();
@@ -873,7 +876,7 @@ hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t
 
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st) {
     if (a.units <= 0 || a.ntiles <= 0) return hipSuccess;
-    const int64_t blocks = (a.units + 7) / 8 * 8 * (a.colw == 1024 ? a.ntiles : (a.ntiles + 3) / 4);
+    const int64_t blocks = a.colw == 1024 ? (a.units + 7) / 8 * 8 * a.ntiles : (a.units * a.ntiles + 31) / 32 * 8;
     if (blocks > int64_t(0x7fffffff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_cs16, dim3(unsigned(blocks)), dim3(256), 0, st, a);
     return hipGetLastError();

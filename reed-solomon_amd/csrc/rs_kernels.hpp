@@ -126,8 +126,8 @@ struct Cs16Args {
     int32_t ngroups, ntiles;  // ngroups even (padded with empty groups)
     int64_t nchunks;          // columns (colw bytes) per symbol
     int64_t units;            // n_stripes * nchunks
-    int32_t colw;             // 1024: block = 4 waves on one 1 KiB column, one tile; 256: block = 4 waves on
-                              // one 256-byte column, 4 consecutive tiles (the tiles of a column run together)
+    int32_t colw;             // 1024: block = 4 waves on one 1 KiB column, one tile; 256: every wave one
+                              // (256-byte column, tile) pair, 4 consecutive pairs per block (rs_kernels.hip)
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);

@@ -12,5 +12,5 @@ for i in 1 2; do for v in 256 1024; do
   timeout -k 10 300 python -u bench.py --k 4096 --r 1024 --symbol 1024 --stripes 1024 --steps 20 --no-cpu --opt m16_cs_col=$v > gpurun_out/c5col/b_${v}_${i}.log 2>&1 || exit 1
   echo "col=$v run=$i $(python3 -c "import json; l=[json.loads(x) for x in open('gpurun_out/c5col/b_${v}_${i}.log') if x.startswith('{')][-1]; print(l['value'], l['encode_ms'], l['decode_ms'], l['parity'])")" | tee -a gpurun_out/c5col/sweep.log
 done; done
-TR=c5tr bash scripts/gpu_traffic.sh --k 4096 --r 1024 --symbol 1024 --stripes 1024 || exit 1
+TR=c5tr bash scripts/gpu_traffic.sh --k 4096 --r 1024 --symbol 1024 --stripes 1024 ${C5_TRAFFIC_OPT:-} || exit 1
 cat gpurun_out/c5traffic.json | grep -E '"leg"|traffic_bytes'
