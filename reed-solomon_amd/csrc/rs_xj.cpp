@@ -197,7 +197,7 @@ struct XjConfig {
         horner = horner ? 1 : 0;
         cpb = std::max(1, std::min(64, cpb));
         if (lfin || lds || share || spread || xcd || buffer || ring != 2) cpb = 1;
-        early = (early && !lds && !share && !spread && ring == 2 && cpb == 1) ? 1 : 0;
+        early = (early && !lds && !share && !spread && ring == 2 && cpb == 1) ? std::min(2, std::max(1, early)) : 0;
     }
     // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
     void set_k(int K) {
@@ -219,7 +219,7 @@ struct XjConfig {
         std::snprintf(b, sizeof b, "opr%d ring%d buf%d spread%d horner%d ablate%d lds%d nt%d fin%d share%d kreg%d",
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
         std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
-        if (early) s += " early";
+        if (early) s += early == 2 ? " early2" : " early";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -461,10 +461,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
     auto nload = [&](int g) { return g < ngp ? std::min(8, K - 8 * g) : 0; };
     // instruction lists of the loads of pair g (address arithmetic first, then the loads); `next_col`:
     // the same pair of the block's next column (base s[60:61])
-    auto load_ops = [&](int g, bool next_col = false) {
+    auto load_ops = [&](int g, bool next_col = false, int j0 = 0, int j1 = 8) {
         std::vector<std::string> ops;
-        const int n = nload(g);
-        for (int j = 0; j < n; ++j) {
+        const int n = std::min(nload(g), j1);
+        for (int j = j0; j < n; ++j) {
             const int dst = C.ring_base() + 8 * (g % C.ring) + j;
             const int slot = in_slots[size_t(8 * g + j)];
             if (C.buffer) {
@@ -512,7 +512,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.f("s_waitcnt vmcnt(%d)", pend);
         for (auto& op : ds_ops(0)) E.e(op);
     } else {
-        for (int g = 0; g < ahead + C.early; ++g)
+        for (int g = 0; g < ahead + (C.early ? 1 : 0); ++g)
             for (auto& op : load_ops(g)) E.e(op);
     }
     if (loop) {  // the first column's pair 0 is the block's only cold wait
@@ -536,7 +536,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
             // loads issued so far beyond pair g: pairs g+1 .. g+ahead-1 (g+ahead is issued below); early:
             // pair g+1 was issued inside pair g-1, pair g+2 goes out inside this pair's rows
             int pending = 0;
-            for (int x = g + 1; x < g + ahead + C.early; ++x) pending += nload(x);
+            for (int x = g + 1; x < g + ahead + (C.early ? 1 : 0); ++x) pending += nload(x);
             if (!C.early) next = load_ops(g + ahead);
             if (!C.spread && !C.early) {
                 for (auto& op : next) E.e(op);
@@ -632,13 +632,16 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         if (C.ablate & 4) body.clear();
         for (auto& op : mid) body.push_back(op);  // LDS ring: next pair's reads + refills after the tables
         const size_t nbuild = body.size();
-        std::vector<std::string> rest;  // early: rows that read only built entries, after the next loads
+        // early: rows that read only built entries go after the next loads; early 2: the rows reading a
+        // raw input of group 1 (and none of group 0) go between group 0's and group 1's loads
+        std::vector<std::string> rest, raw1;
         for (int t = 0; t < 8; ++t)
             for (int q = 0; q < nq; ++q) {
                 const int a = pat[q][t][0], b = pat[q][t][1], acc = C.acc(q, t);
                 if ((!a && !b) || (C.ablate & 2)) continue;
-                const bool raw = __builtin_popcount(a) == 1 || __builtin_popcount(b) == 1;
-                std::vector<std::string>& dst = (C.early && !raw) ? rest : body;
+                const bool r0 = __builtin_popcount(a) == 1, r1 = __builtin_popcount(b) == 1;
+                std::vector<std::string>& dst =
+                    !C.early ? body : r0 ? body : r1 ? (C.early == 2 ? raw1 : body) : rest;
                 if (!init[q][t]) {
                     if (a && b)
                         dst.push_back(E.fmt("v_xor_b32 v%d, v%d, v%d", acc, reg(0, a), reg(1, b)));
@@ -652,7 +655,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 }
             }
         if (C.early) {  // this pair's raw inputs are dead now: pair g+2 into their ring slot, then the rest
-            for (auto& op : load_ops(g + 2)) body.push_back(op);
+            for (auto& op : load_ops(g + 2, false, 0, C.early == 2 ? 4 : 8)) body.push_back(op);
+            for (auto& op : raw1) body.push_back(op);
+            if (C.early == 2)
+                for (auto& op : load_ops(g + 2, false, 4, 8)) body.push_back(op);
             for (auto& op : rest) body.push_back(op);
         }
         if (C.spread && !next.empty()) {
