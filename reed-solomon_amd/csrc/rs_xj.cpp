@@ -162,6 +162,7 @@ struct XjConfig {
                        // last pair and finish (its ring slot stays clear of the finish registers), so only
                        // the block's first column waits for a cold load. Needs an even pair count (set_k).
     int cpb_sync = 1;  // column loop: s_barrier per column
+    int endwait = 0;   // 1: wait for the stores between the two store batches and at the end of the role
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
@@ -185,6 +186,7 @@ struct XjConfig {
         env("RS_XJ_CPB", cpb);
         env("RS_XJ_CPB_SYNC", cpb_sync);
         env("RS_XJ_EARLY", early);
+        env("RS_XJ_ENDWAIT", endwait);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -220,6 +222,7 @@ struct XjConfig {
                       opr, ring, buffer, spread, horner, ablate, lds, nt, lfin, share, kreg);
         std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
         if (early) s += early == 2 ? " early2" : " early";
+        if (!endwait) s += " noendwait";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -734,9 +737,11 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 E.f("global_store_dword %s, v%d, s[%d:%d]%s", COL, C.fin(q0 + j), 40 + 2 * j, 41 + 2 * j,
                     (C.nt & 2) ? " nt" : "");
         }
-        if (q0 + 8 < nq) E.e("s_waitcnt vmcnt(0)");  // address registers are reused by the next batch
+        // endwait 0: no waits -- a store reads its address and data registers at issue, and the wave may
+        // end with stores in flight
+        if (q0 + 8 < nq && C.endwait) E.e("s_waitcnt vmcnt(0)");
     }
-    E.e("s_waitcnt vmcnt(0)");
+    if (C.endwait || D) E.e("s_waitcnt vmcnt(0)");
     if (D) E.e("s_mov_b32 m0, s63");
     return E.L;
 }
