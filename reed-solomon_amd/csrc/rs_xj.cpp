@@ -163,6 +163,7 @@ struct XjConfig {
                        // the block's first column waits for a cold load. Needs an even pair count (set_k).
     int cpb_sync = 1;  // column loop: s_barrier per column
     int endwait = 0;   // 1: wait for the stores between the two store batches and at the end of the role
+    int splitwait = 0; // 1: wait for a pair's first group of four inputs, build its tables, then wait for the rest
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
@@ -187,6 +188,7 @@ struct XjConfig {
         env("RS_XJ_CPB_SYNC", cpb_sync);
         env("RS_XJ_EARLY", early);
         env("RS_XJ_ENDWAIT", endwait);
+        env("RS_XJ_SPLITWAIT", splitwait);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -200,6 +202,7 @@ struct XjConfig {
         cpb = std::max(1, std::min(64, cpb));
         if (lfin || lds || share || spread || xcd || buffer || ring != 2) cpb = 1;
         early = (early && !lds && !share && !spread && ring == 2 && cpb == 1) ? std::min(2, std::max(1, early)) : 0;
+        splitwait = (splitwait && !lds && !share && cpb == 1) ? 1 : 0;
     }
     // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
     void set_k(int K) {
@@ -223,6 +226,7 @@ struct XjConfig {
         std::string s = xcd ? std::string(b) + " xcd" + std::to_string(xcd) : std::string(b);
         if (early) s += early == 2 ? " early2" : " early";
         if (!endwait) s += " noendwait";
+        if (splitwait) s += " splitwait";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -525,6 +529,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
     }
     for (int g = 0; g < ngp; ++g) {
         std::vector<std::string> next, mid;
+        std::string second_wait;  // splitwait: the wait for the pair's group-1 inputs
         if (D) {
             E.e("s_waitcnt lgkmcnt(0)");
             if (g + 1 < ngp) {  // pair g+1 has landed in LDS once only pairs g+2 .. g+D-1 are pending
@@ -548,7 +553,12 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
             // column loop: the previous column's stores were issued after this pair 0 and before the
             // loads above (vmcnt retires in issue order)
             if (loop && g == 0) pending += nq;
-            E.f("s_waitcnt vmcnt(%d)", pending);
+            if (C.splitwait && nload(g) > 4) {  // group 0's four inputs first; group 1's before its tables
+                E.f("s_waitcnt vmcnt(%d)", pending + nload(g) - 4);
+                second_wait = E.fmt("s_waitcnt vmcnt(%d)", pending);
+            } else {
+                E.f("s_waitcnt vmcnt(%d)", pending);
+            }
             if (loop && g == ngp - 1) {  // the next column's pair 0 into ring slot 0 (free: pair ngp-2 is done)
                 E.e("s_cmp_gt_u32 s39, 1");
                 E.f("s_cbranch_scc0 L_xj_npf%d", w);
@@ -584,6 +594,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         };
         std::vector<std::string> body;
         for (int h = 0; h < 2; ++h) {
+            if (h == 1 && !second_wait.empty()) body.push_back(second_wait);
             if (C.share && h != w) continue;  // the partner role builds the other group
             // popcount 2 and 3 straight from the inputs; 15 from a built triple or pair
             bool built[16] = {};
