@@ -164,6 +164,7 @@ struct XjConfig {
     int cpb_sync = 1;  // column loop: s_barrier per column
     int endwait = 0;   // 1: wait for the stores between the two store batches and at the end of the role
     int splitwait = 0; // 1: wait for a pair's first group of four inputs, build its tables, then wait for the rest
+    int inlinefin = 0; // 1: each role carries its own copy of the finish (no s_swappc / s_setpc per column)
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
@@ -189,6 +190,7 @@ struct XjConfig {
         env("RS_XJ_EARLY", early);
         env("RS_XJ_ENDWAIT", endwait);
         env("RS_XJ_SPLITWAIT", splitwait);
+        env("RS_XJ_INLINEFIN", inlinefin);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -203,6 +205,7 @@ struct XjConfig {
         if (lfin || lds || share || spread || xcd || buffer || ring != 2) cpb = 1;
         early = (early && !lds && !share && !spread && ring == 2 && cpb == 1) ? std::min(2, std::max(1, early)) : 0;
         splitwait = (splitwait && !lds && !share && cpb == 1) ? 1 : 0;
+        inlinefin = (inlinefin && !lfin && cpb == 1) ? 1 : 0;
     }
     // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
     void set_k(int K) {
@@ -227,6 +230,7 @@ struct XjConfig {
         if (early) s += early == 2 ? " early2" : " early";
         if (!endwait) s += " noendwait";
         if (splitwait) s += " splitwait";
+        if (inlinefin) s += " inlinefin";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -721,7 +725,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         return E.L;
     }
     // finish (shared block; returns through s[58:59]); L_xj_fin precedes every role block
-    if (!(C.ablate & 1)) {
+    if (!(C.ablate & 1) && C.inlinefin) {  // the block's body in place: no call / return
+        std::vector<std::string> fb = finish_block(C);
+        for (size_t i = 2; i + 2 < fb.size(); ++i) E.e(fb[i]);  // minus branch + label, return + end label
+    } else if (!(C.ablate & 1)) {
         E.e("s_getpc_b64 s[56:57]");
         E.e("s_add_u32 s56, s56, L_xj_fin-.");
         E.e("s_addc_u32 s57, s57, -1");
