@@ -165,6 +165,7 @@ struct XjConfig {
     int endwait = 0;   // 1: wait for the stores between the two store batches and at the end of the role
     int splitwait = 0; // 1: wait for a pair's first group of four inputs, build its tables, then wait for the rest
     int inlinefin = 0; // 1: each role carries its own copy of the finish (no s_swappc / s_setpc per column)
+    int prio = 0;      // 1: s_setprio 1 over the XOR network, 0 over the finish; 2: 2 over the finish only
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
@@ -191,6 +192,7 @@ struct XjConfig {
         env("RS_XJ_ENDWAIT", endwait);
         env("RS_XJ_SPLITWAIT", splitwait);
         env("RS_XJ_INLINEFIN", inlinefin);
+        env("RS_XJ_PRIO", prio);
 
         lfin = lfin ? 1 : 0;
         if (lfin) lds = 0;  // the table takes the LDS
@@ -231,6 +233,7 @@ struct XjConfig {
         if (!endwait) s += " noendwait";
         if (splitwait) s += " splitwait";
         if (inlinefin) s += " inlinefin";
+        if (prio) s += " prio";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -459,6 +462,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.e("s_mov_b32 s54, -1");
         E.e("s_mov_b32 s55, 0x20000");
     }
+    if (C.prio == 1) E.e("s_setprio 1");  // rows (which issue the loads) ahead of other waves' finishes
     const int ngp = (K + 7) / 8;
     // column loop: s39 = columns left; the block's columns are gridDim.x apart (s63 = that stride in bytes),
     // so the blocks in flight still read neighbouring columns together; s[60:61] = source base + stride
@@ -724,6 +728,8 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         E.e("s_waitcnt vmcnt(0)");
         return E.L;
     }
+    // prio 1: the finish issues no loads, the other waves' rows go first; prio 2: the finish first
+    if (C.prio) E.e(C.prio == 1 ? "s_setprio 0" : "s_setprio 2");
     // finish (shared block; returns through s[58:59]); L_xj_fin precedes every role block
     if (!(C.ablate & 1) && C.inlinefin) {  // the block's body in place: no call / return
         std::vector<std::string> fb = finish_block(C);

@@ -132,7 +132,7 @@ class Wave:
                 self.scc = int(t < 0)
                 self.sset(a[0], t)
                 continue
-            if op in ("s_nop", "s_getpc_b64", "s_barrier"):
+            if op in ("s_nop", "s_getpc_b64", "s_barrier", "s_setprio"):
                 continue
             # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
             if op == "s_set_gpr_idx_on":
