@@ -165,7 +165,8 @@ struct XjConfig {
     int endwait = 0;   // 1: wait for the stores between the two store batches and at the end of the role
     int splitwait = 0; // 1: wait for a pair's first group of four inputs, build its tables, then wait for the rest
     int inlinefin = 0; // 1: each role carries its own copy of the finish (no s_swappc / s_setpc per column)
-    int prio = 0;      // 1: s_setprio 1 over the XOR network, 0 over the finish; 2: 2 over the finish only
+    int prio = 0;      // 1: s_setprio 1 over the XOR network, 0 over the finish; 2: 2 over the finish only;
+                       // 3: 1 over each early load burst
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
     explicit XjConfig(int R = 0) {
@@ -677,7 +678,10 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 }
             }
         if (C.early) {  // this pair's raw inputs are dead now: pair g+2 into their ring slot, then the rest
+            const bool pr = C.prio == 3 && nload(g + 2) > 0;  // prio 3: the load burst ahead of other waves
+            if (pr) body.push_back("s_setprio 1");
             for (auto& op : load_ops(g + 2, false, 0, C.early == 2 ? 4 : 8)) body.push_back(op);
+            if (pr) body.push_back("s_setprio 0");
             for (auto& op : raw1) body.push_back(op);
             if (C.early == 2)
                 for (auto& op : load_ops(g + 2, false, 4, 8)) body.push_back(op);
@@ -729,7 +733,7 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
         return E.L;
     }
     // prio 1: the finish issues no loads, the other waves' rows go first; prio 2: the finish first
-    if (C.prio) E.e(C.prio == 1 ? "s_setprio 0" : "s_setprio 2");
+    if (C.prio == 1 || C.prio == 2) E.e(C.prio == 1 ? "s_setprio 0" : "s_setprio 2");
     // finish (shared block; returns through s[58:59]); L_xj_fin precedes every role block
     if (!(C.ablate & 1) && C.inlinefin) {  // the block's body in place: no call / return
         std::vector<std::string> fb = finish_block(C);

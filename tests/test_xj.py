@@ -130,7 +130,7 @@ def test_xj_shared_tables_match_oracle(k, r, kind, monkeypatch):
 
 KNOBS = [{"RS_XJ_OPR": "8"}, {"RS_XJ_OPR": "5"}, {"RS_XJ_RING": "3"}, {"RS_XJ_BUFFER": "1"}, {"RS_XJ_SPREAD": "1"},
          {"RS_XJ_HORNER": "1"}, {"RS_XJ_LDS": "3"}, {"RS_XJ_NT": "3"}, {"RS_XJ_RING": "4", "RS_XJ_SPREAD": "1"},
-         {"RS_XJ_KREG": "0"}, {"RS_XJ_EARLY": "0"}, {"RS_XJ_EARLY": "0", "RS_XJ_OPR": "8"}, {"RS_XJ_EARLY": "2"}, {"RS_XJ_EARLY": "2", "RS_XJ_OPR": "5"}, {"RS_XJ_ENDWAIT": "1"}, {"RS_XJ_SPLITWAIT": "1"}, {"RS_XJ_SPLITWAIT": "1", "RS_XJ_EARLY": "0"}, {"RS_XJ_INLINEFIN": "1"}, {"RS_XJ_PRIO": "1"}, {"RS_XJ_PRIO": "2"}]
+         {"RS_XJ_KREG": "0"}, {"RS_XJ_EARLY": "0"}, {"RS_XJ_EARLY": "0", "RS_XJ_OPR": "8"}, {"RS_XJ_EARLY": "2"}, {"RS_XJ_EARLY": "2", "RS_XJ_OPR": "5"}, {"RS_XJ_ENDWAIT": "1"}, {"RS_XJ_SPLITWAIT": "1"}, {"RS_XJ_SPLITWAIT": "1", "RS_XJ_EARLY": "0"}, {"RS_XJ_INLINEFIN": "1"}, {"RS_XJ_PRIO": "1"}, {"RS_XJ_PRIO": "2"}, {"RS_XJ_PRIO": "3"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda d: ",".join(f"{k[6:]}={v}" for k, v in d.items()))
