@@ -37,24 +37,28 @@ SEED = 0x5EED
 METRIC = "encode+decode GB/s (device-resident) at k/r/symbol_len; % HBM roofline"  # BASELINE.json
 
 
-def measured_traffic(kernel, cfg):
+def measured_traffic(kernel, cfg, with_source=False):
     """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters on this configuration
     (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches: the
     exact kernel name for JIT kernels (content-addressed), name + source hash for compiled ones.
-    traffic.json holds one record per (kernel, config)."""
+    traffic.json holds one record per (kernel, config). The value is a lookup of an EARLIER rocprofv3
+    run of the same kernel bytes, not a counter read in this run; `with_source` also returns where it
+    came from."""
     from srchash import kernel_src_hash
     try:
         with open(TRAFFIC_JSON) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None
+        return (None, None) if with_source else None
     for rec in t.get("records", [t]):
         if rec.get("config") != cfg or rec.get("bench_kernel") != kernel:
             continue
         if "[" not in str(kernel) and rec.get("src_hash") != kernel_src_hash(kernel):
             continue
-        return int(rec["traffic_bytes"])
-    return None
+        src = (f"profiles/traffic.json (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes, "
+               f"{rec.get('measured', 'undated')}; earlier run of this exact kernel, not this run)")
+        return (int(rec["traffic_bytes"]), src) if with_source else int(rec["traffic_bytes"])
+    return (None, None) if with_source else None
 
 
 def parse(argv=None):
@@ -84,7 +88,14 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks run the launch / barrier / max-over-ranks protocol with no coding work "
                          "(tests the multi-rank harness on CPU); the line says dry_run")
-    return ap.parse_args(argv)
+    ap.add_argument("--dry-fail-rank", type=int, default=-1,
+                    help="dry run only: this rank exits with status 3 inside the timed region (launcher tests)")
+    ap.add_argument("--dry-same-device", action="store_true",
+                    help="dry run only: every rank reports the same device (duplicate-device check tests)")
+    a = ap.parse_args(argv)
+    if (a.dry_fail_rank >= 0 or a.dry_same_device) and not a.dry_run:
+        ap.error("--dry-fail-rank / --dry-same-device need --dry-run")
+    return a
 
 
 # ------------------------------------------------------------------------------ rank launcher
@@ -94,39 +105,120 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def visible_gpu_count(environ=None, kfd_nodes="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs a rank process started from here will see, counted WITHOUT loading HIP in this process:
+    the GPU nodes of the KFD topology (nodes whose gpu_id is non-zero; CPU nodes have 0), cut down by
+    ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (comma lists; an empty value
+    hides every device). None when nothing is known (no topology and no visibility variable)."""
+    environ = os.environ if environ is None else environ
+    count = None
+    try:
+        ids = []
+        for node in os.listdir(kfd_nodes):
+            try:
+                with open(os.path.join(kfd_nodes, node, "gpu_id")) as f:
+                    ids.append(int(f.read().strip() or "0"))
+            except (OSError, ValueError):
+                continue
+        count = sum(1 for g in ids if g != 0)
+    except OSError:
+        pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if var in environ:
+            listed = [e for e in environ[var].split(",") if e.strip()]
+            count = len(listed) if count is None else min(count, len(listed))
+    return count
+
+
 def spawn_ranks(args):
     """`--gpus N` outside torchrun: start N rank processes (this script, RANK/LOCAL_RANK/WORLD_SIZE set,
-    rendezvous on 127.0.0.1) and wait for them. This process never touches a GPU (the device count
-    below does not initialise one on this image); rank 0 prints the JSON line. A failing rank stops
-    the others. Returns the exit code."""
+    rendezvous on 127.0.0.1) and wait for them. This process never loads HIP (the device count comes
+    from the KFD topology, `visible_gpu_count`) and never replaces itself: the ranks are fresh child
+    processes, each of which dies with this one (PR_SET_PDEATHSIG). Rank 0 prints the JSON line. A
+    rank that fails stops the others; every child is reaped before this returns. Returns the exit code
+    (the first failing rank's, else 0)."""
+    import signal
     n = args.gpus
     if not args.dry_run:
-        import torch
-        ndev = torch.cuda.device_count()
-        if n > ndev:
+        ndev = visible_gpu_count()
+        if ndev is not None and n > ndev:
             print(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible", file=sys.stderr)
             return 2
     port = _free_port()
+
+    def die_with_parent():  # runs in the child before exec (the parent holds no GPU state)
+        try:
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except (OSError, AttributeError):
+            pass
+
     procs = []
     for rank in range(n):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=die_with_parent))
+        print(f"bench.py: rank {rank} pid {procs[-1].pid}", file=sys.stderr, flush=True)
+
+    def stop(live):
+        for j in live:
+            if procs[j].poll() is None:
+                procs[j].terminate()
+        deadline = time.time() + 20
+        for j in live:
+            try:
+                procs[j].wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                procs[j].kill()
+                procs[j].wait()
+
+    def on_signal(signum, _frame):
+        stop(range(n))
+        sys.exit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
     live = set(range(n))
-    while live:
-        for i in sorted(live):
-            c = procs[i].poll()
-            if c is None:
-                continue
-            live.discard(i)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 1
-                print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
-                for j in live:
-                    procs[j].terminate()
-        time.sleep(0.05)
+    try:
+        while live:
+            for i in sorted(live):
+                c = procs[i].poll()
+                if c is None:
+                    continue
+                live.discard(i)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 1
+                    print(f"bench.py: rank {i} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    stop(sorted(live))
+                    live.clear()
+            time.sleep(0.05)
+    finally:
+        stop(range(n))
+        for s, h in old.items():
+            signal.signal(s, h)
     return rc
+
+
+def device_identity(dev):
+    """PCI address (domain:bus:device) and UUID of the rank's GPU (torch device properties)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    uuid = str(getattr(p, "uuid", ""))
+    return {"pci_bus_id": pci, "uuid": uuid}
+
+
+def check_distinct_devices(idents):
+    """Fatal if two ranks run on the same device (same PCI address): a weak-scaling number would then
+    count one GPU twice. Every rank calls this on the same gathered list, so all of them stop."""
+    seen = {}
+    for rank, ident in enumerate(idents):
+        key = ident["pci_bus_id"]
+        if key in seen:
+            print(f"bench.py: ranks {seen[key]} and {rank} share device {key}", file=sys.stderr, flush=True)
+            return False
+        seen[key] = rank
+    return True
 
 
 # ------------------------------------------------------------------------------ CPU baseline
@@ -153,7 +245,7 @@ def cpu_cores():
 def cpu_baseline(args, erased, gpu_sample):
     """Times encode + decode of `cpu_stripes` resident stripes with the reference CPU path on a pthread
     pool (oracle/cpu_baseline.c: one context per thread, views built before the clock). Returns
-    (baseline dict, parity ok)."""
+    (baseline dict, parity ok); `gpu_sample` None (dry run) skips the comparison with GPU output."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from _util import gen_info
     k, r, S = args.k, args.r, args.symbol
@@ -186,7 +278,8 @@ def cpu_baseline(args, erased, gpu_sample):
 
     # bounded sample: passes over the resident stripes, sized from the first pass to the time budget
     t_enc, p_enc = run(0, 1, threads, n), 1
-    parity = all(np.array_equal(stripes[s], gpu_sample[s]) for s in range(min(len(gpu_sample), n)))
+    parity = gpu_sample is None or all(np.array_equal(stripes[s], gpu_sample[s])
+                                       for s in range(min(len(gpu_sample), n)))
     more = int(max(0.0, args.cpu_seconds / 2 - t_enc) / max(t_enc, 1e-9))
     if more:
         t_enc += run(0, more, threads, n)
@@ -256,18 +349,43 @@ def compute_roofline(work_enc, enc_ms, work_dec, dec_ms):
             "peak": round(VALU_PEAK / 1e12, 4), "unit": "T wave-VALU/s", "frac": round(v / t / VALU_PEAK, 4)}
 
 
-def per_rank_times(enc_ms, dec_ms, dev):
-    """[{rank, encode_ms, decode_ms}] of every rank (all_gather; one entry without a process group)."""
+def gather_objects(obj, group):
+    """`obj` of every rank, in rank order (over the CPU-side gloo group; one entry without one)."""
+    import torch.distributed as dist
+    if group is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def per_rank_times(enc_ms, dec_ms, ident, group):
+    """[{rank, encode_ms, decode_ms, pci_bus_id, uuid}] of every rank."""
+    mine = {"encode_ms": round(float(enc_ms), 3), "decode_ms": round(float(dec_ms), 3), **ident}
+    return [dict(rank=i, **p) for i, p in enumerate(gather_objects(mine, group))]
+
+
+def cpu_group_barrier(group):
+    """Barrier over the gloo side group: ranks waiting here (e.g. while rank 0 runs the CPU baseline)
+    block in a socket read instead of spinning on a device collective."""
+    import torch.distributed as dist
+    if group is not None:
+        dist.barrier(group=group)
+
+
+def start_group(backend, local):
+    """Joins the job's process group (`backend`: "nccl" = RCCL, or "gloo" for a dry run) when launched as
+    a rank, plus a gloo side group for host-side exchanges (device identities, per-rank times, waits
+    while rank 0 runs the CPU baseline). Returns the side group, or None for a single process."""
     import torch
     import torch.distributed as dist
-    mine = torch.tensor([enc_ms, dec_ms], dtype=torch.float64, device=dev)
-    if not (dist.is_available() and dist.is_initialized()):
-        parts = [mine]
+    if "WORLD_SIZE" not in os.environ:
+        return None
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
-        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, mine)
-    return [{"rank": i, "encode_ms": round(float(p[0]), 3), "decode_ms": round(float(p[1]), 3)}
-            for i, p in enumerate(parts)]
+        dist.init_process_group(backend)
+    return dist.new_group(backend="gloo") if dist.get_world_size() > 1 else None
 
 
 def base_line(args, world, n, k, r, S, t, elapsed):
@@ -295,24 +413,35 @@ def base_line(args, world, n, k, r, S, t, elapsed):
 def dry_run_main(args, rank, world):
     """The multi-rank protocol without a GPU: gloo process group, the same barrier-bracketed timed
     region and max-over-ranks reduction, per-rank times gathered, no coding work (step = a no-op)."""
-    import torch
     import torch.distributed as dist
     import rs_dist
-    if world > 1:
-        dist.init_process_group("gloo")
+    group = start_group("gloo", local=rank)
     n, k, r, S = args.stripes, args.k, args.r, args.symbol
+    ident = {"pci_bus_id": "dry-run" if args.dry_same_device else f"dry-run:{rank}", "uuid": ""}
+    if not check_distinct_devices(gather_objects(ident, group)):
+        sys.exit(3)
     with rs_dist.TimedRegion(None) as region:
         for _ in range(args.steps):
             time.sleep(0.001 * (1 + rank))
+            if rank == args.dry_fail_rank:
+                print(f"bench.py: rank {rank}: injected failure (--dry-fail-rank)", file=sys.stderr, flush=True)
+                os._exit(3)
+    erased = np.zeros(k + r, np.bool_)
+    erased[[i * max(k // r, 1) for i in range(r)]] = True
+    cpu = None
+    if rank == 0 and not args.no_cpu:  # rank 0 times the CPU path while the others wait (as on the GPU)
+        cpu, _ = cpu_baseline(args, erased, None)
+    cpu_group_barrier(group)
     line = base_line(args, world, n, k, r, S, r, region.max_elapsed)
     line["dry_run"] = True
     line["value"] = None  # no coding work ran: there is no throughput to report
     line["data"] = "dry run: no GPU work, harness protocol only"
     line["rccl_world"] = dist.get_world_size() if dist.is_initialized() else 1
-    line["per_rank"] = per_rank_times(region.elapsed * 1e3, 0.0, "cpu")
+    line["per_rank"] = per_rank_times(region.elapsed * 1e3, 0.0, ident, group)
+    line["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -335,11 +464,13 @@ def main():
         print(f"bench.py: WORLD_SIZE {world} exceeds the {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
         sys.exit(2)
     import rs_amd  # raises if librs_amd.so is missing: no fallback
-    if "WORLD_SIZE" in os.environ:  # launched as ranks (torchrun or --gpus N): RCCL process group, even at N=1
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # launched as ranks (torchrun or --gpus N): RCCL process group, even at N=1, + a gloo side group
+    group = start_group("nccl", local)
+    ident = device_identity(dev)
+    if not check_distinct_devices(gather_objects(ident, group)):  # before any HBM is committed
+        sys.exit(3)
 
     k, r, S, n = args.k, args.r, args.symbol, args.stripes
     erased = rs_amd.bench_pattern(k, r)
@@ -408,11 +539,12 @@ def main():
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev.values()]))
     enc_bytes = n * (k + r) * S
     dec_bytes = n * (k + t) * S
-    per_rank = per_rank_times(enc_ms, dec_ms, dev)
+    per_rank = per_rank_times(enc_ms, dec_ms, ident, group)
+    run_cpu = rank == 0 and not args.no_cpu and not args.profile_only  # every N: rank 0, after the timed region
 
     # verification: restored information == generated information (fingerprints), sampled repair
     parity = "skipped"
-    gpu_sample = np.zeros((0,), np.uint8)
+    gpu_sample = None
     if not args.profile_only:
         # every timed step encoded and restored in place, so the information symbols must still be the
         # generated ones; then poison the erased slots, decode once more and check again
@@ -425,29 +557,32 @@ def main():
         torch.cuda.synchronize()
         good = torch.equal(fp0, fp_ref) and torch.equal(fp1, fp_ref)
         ok = rs_dist.max_over_ranks(0.0 if good else 1.0, dev) == 0.0  # any rank
-        if rank == 0:
+        if run_cpu:  # the CPU leg compares these stripes (global ids 0.. on rank 0) bit for bit
             gpu_sample = stripes[: args.cpu_stripes].cpu().numpy()
         parity = "roundtrip-ok" if ok else "ROUNDTRIP-MISMATCH"
 
     scatter = scatter_leg(args, rank, world, dev) if args.scatter > 0 and world > 1 else None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and not args.profile_only:
+    if run_cpu:  # the other ranks wait at the gloo barrier below (no device spin)
         cpu, cpu_ok = cpu_baseline(args, erased, gpu_sample)
-        parity += ",cpu-bitexact-ok" if cpu_ok else ",CPU-MISMATCH"
+        gpu_sample = None
+        if not args.profile_only:
+            parity += ",cpu-bitexact-ok" if cpu_ok else ",CPU-MISMATCH"
+    cpu_group_barrier(group)
 
     # roofline of the dominant kernel (encode and decode move the same algorithmic bytes here)
     dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, kern_enc) if enc_ms >= dec_ms else (dec_ms, dec_bytes, kern_dec)
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
     cfg_key = f"k{k}_r{r}_S{S}_n{n}_t{t}"
-    traffic = measured_traffic(dom_name, cfg_key)
+    traffic, traffic_src = measured_traffic(dom_name, cfg_key, with_source=True)
     line = base_line(args, world, n, k, r, S, t, elapsed)
     line["config"]["kernel"] = {"encode": kern_enc, "decode": kern_dec}
     line["rccl_world"] = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "kernel": dom_name, "kernel_ms": round(dom_ms, 3), "bytes_per_launch": dom_bytes,
-                        "traffic_key": cfg_key}
+                        "traffic_key": cfg_key, "traffic_source": traffic_src}
     if work_enc[0] + work_dec[0] > 0:  # compute roofline (the kernels are VALU-issue bound)
         line["roofline"]["compute"] = compute_roofline(work_enc, enc_ms, work_dec, dec_ms)
     # both legs: algorithmic bytes and PMC-measured HBM bytes per launch (null when unmeasured)

@@ -18,6 +18,7 @@ import json
 import os
 import re
 import sys
+import time
 
 
 def per_dispatch(d, counter, match):
@@ -120,6 +121,9 @@ def main():
                         "raw_kib": {"FETCH_SIZE": med(fetch), "WRITE_SIZE": med(write)}})
     if not records:
         raise SystemExit("no records")
+    stamp = time.strftime("%Y-%m-%d")
+    for rec in records:
+        rec["measured"] = stamp
     print(json.dumps({"records": records}, indent=1))
 
 

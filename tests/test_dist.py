@@ -166,3 +166,110 @@ def test_bench_launcher_spawns_ranks_dry_run():
     bad = subprocess.run([sys.executable, bench, "--gpus", "2", "--dry-run"], capture_output=True, text=True,
                          timeout=120, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
     assert bad.returncode == 2 and "does not match" in bad.stderr
+
+
+def _run_bench(*argv, timeout=300):
+    import subprocess
+    bench = os.path.join(HERE, "..", "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    return subprocess.run([sys.executable, bench, *argv], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def _rank_pids(stderr):
+    import re
+    return {int(m.group(1)): int(m.group(2)) for m in re.finditer(r"rank (\d+) pid (\d+)", stderr)}
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    try:  # a zombie is not alive (it would only mean the parent did not reap it)
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+def test_bench_launcher_eight_ranks_dry_run():
+    """The C4 shape (BASELINE.json configs[3]): `bench.py --gpus 8` at the default 8192 stripes per rank
+    reports 65536 stripes, 8 distinct ranks on 8 distinct devices, per-rank times, and -- like every
+    N -- a CPU baseline timed by rank 0 after the timed region while the other ranks wait."""
+    p = _run_bench("--gpus", "8", "--dry-run", "--steps", "2", "--cpu-stripes", "2", "--cpu-seconds", "0.1")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = _bench_line(p.stdout)
+    assert line["n_gpus"] == 8 and line["rccl_world"] == 8
+    assert line["config"]["stripes_total"] == 65536
+    assert [e["rank"] for e in line["per_rank"]] == list(range(8))
+    assert len({e["pci_bus_id"] for e in line["per_rank"]}) == 8
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
+    pids = _rank_pids(p.stderr)
+    assert sorted(pids) == list(range(8)) and not any(_alive(q) for q in pids.values())
+
+
+def test_bench_launcher_rank_failure_stops_everyone():
+    """A rank that exits non-zero (here inside the timed region, while the others block in a barrier)
+    makes the launcher exit with that status, and no rank process outlives it."""
+    p = _run_bench("--gpus", "8", "--dry-run", "--steps", "200", "--no-cpu", "--dry-fail-rank", "3")
+    assert p.returncode == 3, p.stderr[-2000:]
+    assert "rank 3 exited with 3" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    pids = _rank_pids(p.stderr)
+    assert sorted(pids) == list(range(8))
+    time.sleep(0.5)
+    assert not any(_alive(q) for q in pids.values()), "orphaned rank processes"
+
+
+def test_bench_duplicate_device_is_fatal():
+    """Two ranks on one device would count one GPU twice: every rank stops before any work."""
+    p = _run_bench("--gpus", "2", "--dry-run", "--no-cpu", "--dry-same-device")
+    assert p.returncode == 3 and "share device" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_visible_gpu_count_without_hip(tmp_path):
+    """The launcher counts GPUs from the KFD topology and the visibility variables, never through HIP."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(HERE, "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    nodes = tmp_path / "nodes"
+    for i, gid in enumerate([0, 0, 4242, 4243, 4244, 4245, 4246, 4247, 4248, 4249]):  # 2 CPU nodes, 8 GPUs
+        (nodes / str(i)).mkdir(parents=True)
+        (nodes / str(i) / "gpu_id").write_text(f"{gid}\n")
+    assert bench.visible_gpu_count({}, str(nodes)) == 8
+    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2"}, str(nodes)) == 3
+    assert bench.visible_gpu_count({"ROCR_VISIBLE_DEVICES": "3"}, str(nodes)) == 1
+    assert bench.visible_gpu_count({"CUDA_VISIBLE_DEVICES": ""}, str(nodes)) == 0
+    assert bench.visible_gpu_count({}, str(tmp_path / "absent")) is None
+    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1"}, str(tmp_path / "absent")) == 2
+
+
+def test_launcher_parent_never_loads_hip():
+    """The `--gpus N` parent counts devices and spawns ranks without importing torch or the HIP library
+    (checked in a fresh interpreter, with the rank processes replaced by no-ops)."""
+    import subprocess
+    code = f"""
+import os, subprocess, sys
+sys.path.insert(0, {os.path.join(HERE, "..")!r})
+for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+    os.environ.pop(v, None)
+os.environ["HIP_VISIBLE_DEVICES"] = "0,1,2,3,4,5,6,7"
+import bench
+class Done:
+    pid = 0
+    def poll(self): return 0
+    def wait(self, timeout=None): return 0
+started = []
+subprocess.Popen = lambda *a, **k: started.append(a) or Done()
+sys.argv = ["bench.py", "--gpus", "8"]
+rc = bench.spawn_ranks(bench.parse(sys.argv[1:]))
+loaded = [m for m in ("torch", "rs_amd") if m in sys.modules]
+hip = [ln for ln in open("/proc/self/maps") if "amdhip" in ln]
+print(rc, len(started), loaded, len(hip))
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.split("\n")[-2] == "0 8 [] 0"
