@@ -22,6 +22,7 @@
 #include "rs_pool.hpp"
 #include "rs_xj.hpp"
 #include <thread>
+#include <unistd.h>
 
 extern "C" {
 #include <memory/seq.h>
@@ -326,8 +327,12 @@ struct DevPlan {
     }
     // before a release from a call on stream st (cache eviction): a plan whose launches all ran on st
     // gets its guard there -- st is alive, and it orders after them -- instead of a device wait
+    // The plans this one owns (second stage, dense twin, route, re-encode D_Rep) are launched by its
+    // calls too, so they get the same treatment: without it their destructors would wait for the device.
     void guard_before_release(hipStream_t st) {
         if (launched && !multi_stream && recorded != launches && used_on == st) (void)record_guard(st);
+        for (DevPlan* q : {second.get(), dense.get(), route.get(), reenc ? reenc->drep.get() : nullptr})
+            if (q) q->guard_before_release(st);
     }
     // called before a launch on stream st: orders it after the build, releases the build's resources
     // once the build is complete
@@ -1232,6 +1237,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     const uint16_t *logt = nullptr, *expt = nullptr;
     const uint8_t* g8 = nullptr;
     if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
+    // d_goff is codec scratch like d_cs: a launch on another stream may still read it (a route encode on
+    // stream A, then a route decode on stream B rewrites it), so wait for that before overwriting it
+    if (int rc = scratch_acquire(c, st)) return rc;
     const int ngo = (cs.ngroups + 3) * 16;
     if (int rc = grow(&c->d_goff[cs.kind], c->goff_cap[cs.kind], size_t(ngo) * 4)) return rc;
     HIP_TRY(launch_cs16_goff(groups ? groups : cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
@@ -1264,11 +1272,10 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         c->work_valu += steps * kValu_bs16;
         c->work_salu += steps * kSalu_bs16;
         c->last_kernel = "bs16";
-        return 0;
+        return scratch_release(c, st);
     }
     const int64_t per = int64_t(cs.D) * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
-    if (int rc = scratch_acquire(c, st)) return rc;
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
     std::string second;
     for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
@@ -1313,6 +1320,9 @@ static int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_s
         k2 = c->last_kernel;
     }
     c->last_kernel = "cs16+bs16+xor+" + k2;
+    // the encode plan's records were read by these launches: its guard must cover them (run_plan does
+    // this for the plans it launches; E is launched through run_cs directly)
+    if (int rc = E.note_use(st)) return rc;
     return scratch_release(c, st);
 }
 
@@ -2173,7 +2183,20 @@ struct ArenaRegistry {
     std::map<uintptr_t, Arena> blocks;
     std::vector<Slab*> slabs;
     bool no_pinning = false;  // page-locked allocation failed once (no GPU): heap from then on
+    size_t pinned = 0;        // page-locked bytes held by blocks and slabs
 };
+
+// Process-wide cap on page-locked symbol memory (arenas, slabs and registered symbols): a quarter of
+// physical RAM, or RS_AMD_PINNED_MAX_MB. Sequences past it go to the heap (the gather / scatter path), so
+// a caller that creates many large sequences cannot page-lock most of the host without knowing it.
+size_t pinned_cap() {
+    static const size_t cap = [] {
+        if (const char* e = std::getenv("RS_AMD_PINNED_MAX_MB")) return size_t(std::strtoull(e, nullptr, 10)) << 20;
+        const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+        return pages > 0 && psz > 0 ? size_t(pages) * size_t(psz) / 4 : size_t(16) << 30;
+    }();
+    return cap;
+}
 ArenaRegistry& arenas() {
     static ArenaRegistry* r = new ArenaRegistry;  // never destroyed: symbols may outlive static destructors
     return *r;
@@ -2204,6 +2227,7 @@ uint8_t* arena_alloc(size_t length, size_t P) {
     std::lock_guard<std::mutex> lk(r.mu);
     if (r.no_pinning) return nullptr;
     if (bytes >= kArenaMin) {
+        if (r.pinned + bytes > pinned_cap()) return nullptr;  // over the cap: heap symbols
         uint8_t* dv = nullptr;
         uint8_t* h = pinned_block(bytes, &dv);
         if (!h) {
@@ -2211,6 +2235,7 @@ uint8_t* arena_alloc(size_t length, size_t P) {
             return nullptr;
         }
         r.blocks[uintptr_t(h)] = Arena{bytes, dv, length};
+        r.pinned += bytes;
         return h;
     }
     const size_t need = (bytes + 255) & ~size_t(255);
@@ -2221,7 +2246,7 @@ uint8_t* arena_alloc(size_t length, size_t P) {
             break;
         }
     if (!sl) {
-        if (r.slabs.size() >= kMaxSlabs) return nullptr;
+        if (r.slabs.size() >= kMaxSlabs || r.pinned + kSlabBytes > pinned_cap()) return nullptr;
         uint8_t* dv = nullptr;
         uint8_t* h = pinned_block(kSlabBytes, &dv);
         if (!h) {
@@ -2230,6 +2255,7 @@ uint8_t* arena_alloc(size_t length, size_t P) {
         }
         sl = new Slab{h, dv};
         r.slabs.push_back(sl);
+        r.pinned += kSlabBytes;
     }
     uint8_t* blk = sl->base + sl->used;
     std::memset(blk, 0, need);  // a reused slab holds old data
@@ -2253,6 +2279,7 @@ bool arena_release(const uint8_t* p) {
         } else {
             (void)hipHostFree(reinterpret_cast<void*>(it->first));
             (void)hipGetLastError();
+            r.pinned -= it->second.bytes;
         }
         r.blocks.erase(it);
     }

@@ -76,6 +76,16 @@ def cases():
     add("c5_dec_rand_2k", "decode", 4096, 1024, 2048, 1, 1024, rand_pattern(4096, 1024, 1024, 9))
     add("c5_dec_t32_1k", "decode", 4096, 1024, 1024, 1, 32, rand_pattern(4096, 1024, 32, 10, info_only=True))
     add("c5_dec_noncw_1k", "decode_noncw", 4096, 1024, 1024, 1, 300, rand_pattern(4096, 1024, 300, 11))
+    # round 3: C5 decodes at n = 2 stripes through the bench decode kernels (re-encode decode, plain
+    # route), and one-stripe C5 decodes with assorted patterns -- batched together they pin the per-stripe
+    # GF(2^16) decode of rsg_decode_batch (every stripe its own pattern; same inputs, stripe 0 of SEED)
+    add("c5_dec_bench_1k_n2", "decode", 4096, 1024, 1024, 2, 1024, bench_pattern(4096, 1024))
+    add("c5_dec_info1000_1k_n2", "decode", 4096, 1024, 1024, 2, 1000,
+        rand_pattern(4096, 1024, 1000, 30, info_only=True))
+    add("c5_dec_mixed_1k_n2", "decode", 4096, 1024, 1024, 2, 1024, rand_pattern(4096, 1024, 1024, 31))
+    for i, (t, info_only) in enumerate([(1, True), (7, False), (64, False), (333, True), (500, False),
+                                        (1000, True), (1023, False), (1024, True)]):
+        add(f"c5ps_t{t}_1k", "decode", 4096, 1024, 1024, 1, t, rand_pattern(4096, 1024, t, 40 + i, info_only))
     # the largest codes (k + r = 65535) on whole 1 KiB columns: the GF(2^16) syndrome route and the
     # re-encode decode at maximum n; sha256 of the outputs
     add("max_n_route_enc_1k", "encode", 64511, 1024, 1024, 1)

@@ -488,6 +488,59 @@ def test_decode_batch_back_to_back_streams(plans):
         assert np.array_equal(got[:, :k], fulls[b][:, :k]), f"batch {b}"
 
 
+@pytest.mark.parametrize("name", ["c5_dec_bench_1k", "c5_dec_bench_1k_n2", "c5_dec_info1000_1k_n2", "c5_dec_mixed_1k_n2"])
+def test_c5_bench_decode_kernels_vs_golden(name):
+    """The C5 bench decode's kernels (reference reed_solomon.c:443-559) pinned to the reference goldens at
+    full 1 KiB chunks, n = 1 and n = 2 stripes: with m16_route_min_bytes = 0 the first launch takes the
+    route -- the re-encode decode (encode route over the surviving information + repair XOR + D_Rep)
+    for information-only patterns with t >= 0.9 r, the plain syndrome route for patterns with repair
+    erasures."""
+    c = case(name)
+    rc, out, kern, m = run_case_gpu(c, "auto", {"m16_route_min_bytes": 0})
+    assert rc == c["rc"] == 0 and m == 16
+    mixed = any(e >= c["k"] for e in c["erased"])
+    assert kern.startswith("cs16+apply" if mixed else "cs16+bs16+xor+"), kern
+    check_golden(c, out)
+
+
+def test_m16_route_encode_then_decode_on_two_streams():
+    """A GF(2^16) route encode on stream A and a route decode on stream B issued back to back with one
+    codec: the decode rewrites the codec's slot-offset scratch (d_goff) that A's k_cs16 may still be
+    reading, so it must wait for A first. Both results bit-exact vs the oracle."""
+    k, r, S, n = 1000, 200, 4096, 48
+    rng = np.random.default_rng(4242)
+    codec = rs_amd.Codec(k, r)
+    a = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(a, k, seed=0x77)
+    b = torch.zeros((2, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(b, k, seed=0x78)
+    codec.encode(b)
+    torch.cuda.synchronize()
+    full_b = b.cpu().numpy()
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k + r, 40, replace=False)] = True  # t <= 64: the route at once
+    poisoned = full_b.copy()
+    poisoned[:, er] = 0
+    b.copy_(torch.from_numpy(poisoned))
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        codec.encode(a, stream=sa)
+        assert codec.last_kernel.startswith("cs16+"), codec.last_kernel
+        codec.decode(b, er, stream=sb)
+        assert codec.last_kernel.startswith("cs16+"), codec.last_kernel
+        torch.cuda.synchronize()
+        assert np.array_equal(b.cpu().numpy(), full_b)
+        b.copy_(torch.from_numpy(poisoned))
+        torch.cuda.synchronize()
+    got = a.cpu().numpy()
+    for s in (0, n // 2, n - 1):
+        want = got[s].copy()
+        want[k:] = 0
+        assert oracle_encode(k, r, want) == 0
+        assert np.array_equal(got[s], want), f"stripe {s}"
+
+
 XJ_SHAPES = [(1, 1), (2, 1), (3, 16), (7, 17), (9, 5), (16, 8), (33, 31), (50, 33), (64, 48), (100, 60), (120, 51),
              (180, 34), (24, 200), (12, 243)]
 
