@@ -612,6 +612,19 @@ struct rsg_codec {
     void* d_reenc = nullptr;  // re-encode decode scratch: [chunk][r][S] (G_U u + y)
     size_t reenc_cap = 0;
     int m16_reenc = 1;  // option m16_reenc: 0 keeps full-pattern decodes on the plain route
+    // rsg_decode_batch of GF(2^16) codes with per-stripe patterns (decode_batch_m16_ps): 1 = the syndrome
+    // route with a device-built plan per stripe (default), 0 = a plan per distinct pattern
+    int m16_ps = 1;
+    std::map<int, std::unique_ptr<DevPlan>> ps_syn;  // k_cs16 plans over all k + r slots, keyed by D
+    std::vector<int> ps_syn_lru;
+    void *d_ps_rec = nullptr, *d_ps_small = nullptr;  // per-stripe records / lists of decode_batch_m16_ps
+    int32_t* d_ps_in = nullptr;                       // its shared input list 0 .. r + 15
+    hipStream_t ps_side = nullptr;                    // plan kernels of the next chunk run here
+    hipEvent_t ps_ev_entry = nullptr, ps_ev_zero[2] = {nullptr, nullptr}, ps_ev_plan[2] = {nullptr, nullptr},
+               ps_ev_used[2] = {nullptr, nullptr};
+    int64_t ps_chunk = 0;   // option m16_ps_chunk: max stripes per chunk (0 = by ps_rec_mib)
+    int64_t ps_rec_mib = 1024;  // records per chunk (MiB); larger chunks keep k_cs16 busier (measured 48-1024)
+    size_t ps_rec_cap = 0, ps_small_cap = 0;
     int m16_cs_col = 256;  // option m16_cs_col: the route kernels' block layout (256 or 1024 bytes, rs_kernels.hip)
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
@@ -657,6 +670,10 @@ struct rsg_codec {
     ~rsg_codec() {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
+        if (ps_side) (void)hipStreamSynchronize(ps_side), (void)hipStreamDestroy(ps_side);
+        for (hipEvent_t e : {ps_ev_entry, ps_ev_zero[0], ps_ev_zero[1], ps_ev_plan[0], ps_ev_plan[1], ps_ev_used[0],
+                             ps_ev_used[1]})
+            if (e) (void)hipEventDestroy(e);
         if (bp16) bp16->d_idx = nullptr;  // d_bp16_rec, freed below
         for (int i = 0; i < 2; ++i) {
             if (bp16_ev[i]) (void)hipEventDestroy(bp16_ev[i]);
@@ -667,7 +684,8 @@ struct rsg_codec {
             if (hbuf[i]) (void)hipFree(hbuf[i]);
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
-                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_reenc, d_goff[0], d_goff[1]})
+                        d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_reenc, d_goff[0], d_goff[1], d_ps_rec,
+                        d_ps_small, static_cast<void*>(d_ps_in)})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
@@ -1192,6 +1210,21 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->m16_reenc = int(value);
         c->dec.clear();
         c->dec_lru.clear();
+        return 0;
+    }
+    if (!std::strcmp(name, "m16_ps")) {  // rsg_decode_batch of GF(2^16) codes: per-stripe route plans
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->m16_ps = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m16_ps_chunk")) {  // its stripes per chunk (0 = sized by m16_ps_rec_mib)
+        if (value < 0 || value > 65535) return RS_ERR_INVALID;
+        c->ps_chunk = value;
+        return 0;
+    }
+    if (!std::strcmp(name, "m16_ps_rec_mib")) {  // its record bytes per chunk
+        if (value < 1 || value > 4096) return RS_ERR_INVALID;
+        c->ps_rec_mib = value;
         return 0;
     }
     if (!std::strcmp(name, "m16_route_min_bytes")) {
@@ -1965,6 +1998,223 @@ static int batch_plan_m16(rsg_codec_t* c, const bool* er, int slot, hipStream_t 
     return 0;
 }
 
+// rsg_decode_batch, GF(2^16) codes with per-stripe patterns: the reference's decode split
+// (reed_solomon.c:527-549) into its pattern-independent part -- the syndromes S_j (j < D, D = the largest
+// t of the batch) of all k + r slots of every stripe, one k_cs16 pass with a fixed plan (cached per D) --
+// and the per-pattern part: each stripe's t_info x t solve W (k_plan16_ps / k_plan16_ps_rec build it on
+// the device from the stripe's mask, straight into k_apply_m16_v1 records), applied to that stripe's
+// first t syndromes by k_apply_m16_v1 in per-stripe mode. Erased information slots are zeroed first (the
+// syndromes read every slot); garbage in an erased repair slot only shifts that slot's own unknown,
+// which is never written.
+static bool ps16_eligible(const rsg_codec_t* c, uint64_t S, int64_t stripe_stride, int64_t symbol_stride,
+                          const void* base) {
+    const int64_t n = int64_t(c->k) + c->r;
+    return c->m > 8 && c->m16_ps && c->r <= kPs16MaxR && S % 1024 == 0 && int64_t(S) < (int64_t(1) << 31) &&
+           (n - 1) * symbol_stride + int64_t(S) < (int64_t(1) << 31) && int64_t(c->r) * int64_t(S) < (int64_t(1) << 31) &&
+           (stripe_stride % 16) == 0 && (symbol_stride % 16) == 0 && (uintptr_t(base) % 16) == 0 &&
+           symbol_stride >= int64_t(S);
+}
+
+static int ps16_syn_plan(rsg_codec_t* c, int D, hipStream_t st, DevPlan** out) {
+    auto it = c->ps_syn.find(D);
+    if (it == c->ps_syn.end()) {
+        if (c->ps_syn.size() >= 4) {  // small LRU: batches usually share a few D values
+            const int old = c->ps_syn_lru.front();
+            c->ps_syn_lru.erase(c->ps_syn_lru.begin());
+            auto o = c->ps_syn.find(old);
+            if (o != c->ps_syn.end()) {
+                o->second->guard_before_release(st);
+                c->ps_syn.erase(o);
+            }
+        }
+        const int n = int(c->k) + c->r;
+        std::vector<int32_t> all(static_cast<size_t>(n));
+        for (int i = 0; i < n; ++i) all[size_t(i)] = i;
+        auto p = std::make_unique<DevPlan>();
+        p->device = c->device;
+        p->m = 16;
+        p->K = n;
+        p->R = D;
+        p->in_slots = all;
+        if (int rc = build_cs16(*p, c->positions, all, D, st)) return rc;
+        it = c->ps_syn.emplace(D, std::move(p)).first;
+    } else {
+        c->ps_syn_lru.erase(std::find(c->ps_syn_lru.begin(), c->ps_syn_lru.end(), D));
+    }
+    c->ps_syn_lru.push_back(D);
+    *out = it->second.get();
+    return 0;
+}
+
+static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                               uint64_t n_stripes, uint64_t S, const bool* is_erased, hipStream_t st) {
+    const size_t n = size_t(c->k) + c->r;
+    std::vector<int32_t> ids;
+    std::vector<uint8_t> masks;
+    int tmax = 0, rmax = 0;
+    masks.reserve(size_t(n_stripes) * n);
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const bool* e = is_erased + s * n;
+        const int R = int(std::count(e, e + c->k, true));
+        if (!R) continue;
+        const int t = R + int(std::count(e + c->k, e + n, true));
+        tmax = std::max(tmax, t);
+        rmax = std::max(rmax, R);
+        ids.push_back(int32_t(s));
+        masks.insert(masks.end(), reinterpret_cast<const uint8_t*>(e), reinterpret_cast<const uint8_t*>(e) + n);
+    }
+    if (ids.empty()) return 0;
+    int rc = scratch_acquire(c, st);
+    if (rc) return rc;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
+    if (!c->d_elem) {
+        const Field& F = field();
+        std::vector<uint16_t> el(n);
+        for (size_t i = 0; i < n; ++i) el[i] = F.exp[c->positions[i]];
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_elem), el.data(), n * 2))) return rc;
+    }
+    // D: the batch's largest t rounded up to a multiple of 32 (fewer distinct cached syndrome plans)
+    const int D = std::min<int>(c->r, (tmax + 31) / 32 * 32);
+    DevPlan* syn = nullptr;
+    if ((rc = ps16_syn_plan(c, D, st, &syn))) return rc;
+    if ((rc = syn->order_after_build(st))) return rc;
+    const DevPlan::Cs& cs = *syn->cs;
+    const int64_t nsel = int64_t(ids.size());
+    const int tiles = (rmax + 63) / 64;
+    const int64_t out_stride = int64_t(tiles) * 64;
+    const int64_t rec_stride = int64_t(tiles) * (D + 1) * 64;  // dwords
+    const int64_t per = int64_t(D) * int64_t(S);                // syndrome bytes per stripe
+    // chunks of stripes, at most m16_ps_rec_mib of records each: larger chunks measured faster (C5, 256
+    // stripes: 48 MiB 0.260, 160 MiB 0.204, 1024 MiB 0.184 ms a stripe; option m16_ps_chunk caps it)
+    int64_t chunk = std::max<int64_t>(
+        1, std::min<int64_t>({nsel, (int64_t(1) << 30) / per, (int64_t(c->ps_rec_mib) << 20) / (rec_stride * 4), 65535}));
+    if (c->ps_chunk > 0) chunk = std::min<int64_t>(chunk, c->ps_chunk);
+    const int64_t nchunk = (nsel + chunk - 1) / chunk;
+    chunk = (nsel + nchunk - 1) / nchunk;  // even chunks (no small tail chunk)
+    // small per-stripe arrays in one buffer: kr [2] i32, ee [r] u16, pe [out_stride] u16, pout
+    // [out_stride] i32, cf [r + 1] u16 (each part 256-byte aligned)
+    auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+    const int64_t o_kr = 0, o_ee = al(chunk * 8), o_pe = o_ee + al(chunk * c->r * 2),
+                  o_po = o_pe + al(chunk * out_stride * 2), o_cf = o_po + al(chunk * out_stride * 4),
+                  small = o_cf + al(chunk * (int64_t(c->r) + 1) * 2);
+    size_t ids_bytes = c->ids_cap * 4;
+    rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
+    c->ids_cap = ids_bytes / 4;
+    if (rc) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, masks.size()))) return rc;
+    if ((rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per)))) return rc;
+    // two sets of plan buffers: chunk i + 1's plans are built on the side stream while chunk i runs
+    const int64_t rec_set = al(chunk * rec_stride * 4);
+    if ((rc = grow(&c->d_ps_rec, c->ps_rec_cap, size_t(2 * rec_set)))) return rc;
+    if ((rc = grow(&c->d_ps_small, c->ps_small_cap, size_t(2 * small)))) return rc;
+    if (!c->ps_side) HIP_TRY(hipStreamCreateWithFlags(&c->ps_side, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1],
+                          &c->ps_ev_used[0], &c->ps_ev_used[1]})
+        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    const int ngo = (cs.ngroups + 3) * 16;
+    if ((rc = grow(&c->d_goff[0], c->goff_cap[0], size_t(ngo) * 4))) return rc;
+    // the host lists must outlive the copies: upload on the caller's stream, then wait once
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[0]), ngo, symbol_stride, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    Ps16Args pa{};
+    pa.elem = c->d_elem;
+    pa.logt = logt;
+    pa.expt = expt;
+    pa.k = c->k;
+    pa.r = c->r;
+    pa.n = int32_t(n);
+    pa.out_stride = out_stride;
+    pa.rec_stride = rec_stride;
+    pa.tblocks = (tiles + 3) / 4;
+    pa.base = base;
+    pa.stripe_stride = stripe_stride;
+    pa.symbol_stride = symbol_stride;
+    pa.S = int64_t(S);
+    Cs16Args ca{};
+    ca.src = base;
+    ca.src_stripe = stripe_stride;
+    ca.src_sym = symbol_stride;
+    ca.goff = static_cast<const uint32_t*>(c->d_goff[0]);
+    ca.in_bytes = uint32_t(cs.max_slot * symbol_stride + int64_t(S));
+    ca.rec = cs.rec;
+    ca.fin = cs.fin;
+    ca.fin_off = cs.fin_off;
+    ca.fin_stride = cs.fin_stride;
+    ca.dst_stripe = per;
+    ca.dst_sym = int64_t(S);
+    ca.logt = logt;
+    ca.expt = expt;
+    for (int q = 0; q < 16; ++q) ca.nblog[q] = cs.nblog[q];
+    ca.ngroups = cs.ngroups;
+    ca.ntiles = cs.ntiles;
+    ca.colw = c->m16_cs_col == 1024 ? 1024 : 256;
+    ca.nchunks = int64_t(S) / ca.colw;
+    if (!c->d_ps_in) {  // the apply's shared input list: input j = syndrome j of the stripe (j < r, + padding)
+        std::vector<int32_t> in_list(size_t(c->r) + 16);
+        for (size_t j = 0; j < in_list.size(); ++j) in_list[j] = int32_t(j);
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_ps_in), in_list.data(), in_list.size() * 4))) return rc;
+    }
+    // the side stream starts after the caller's earlier work on st (the plans zero erased slots)
+    HIP_TRY(hipEventRecord(c->ps_ev_entry, st));
+    HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_entry, 0));
+    for (int64_t c0 = 0, ci = 0; c0 < nsel; c0 += chunk, ++ci) {
+        const int64_t cn = std::min(chunk, nsel - c0);
+        const int set = int(ci & 1);
+        uint8_t* sm = static_cast<uint8_t*>(c->d_ps_small) + set * small;
+        pa.kr = reinterpret_cast<int32_t*>(sm + o_kr);
+        pa.ee = reinterpret_cast<uint16_t*>(sm + o_ee);
+        pa.pe = reinterpret_cast<uint16_t*>(sm + o_pe);
+        pa.pout = reinterpret_cast<int32_t*>(sm + o_po);
+        pa.cf = reinterpret_cast<uint16_t*>(sm + o_cf);
+        pa.rec = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_ps_rec) + set * rec_set);
+        pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+        pa.ids = c->d_ids + c0;
+        // plans of this chunk on the side stream, once chunk ci - 2 (same buffer set) has been applied
+        if (ci >= 2) HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_used[set], 0));
+        HIP_TRY(launch_plan16_ps(pa, cn, c->ps_side));
+        HIP_TRY(hipEventRecord(c->ps_ev_zero[set], c->ps_side));
+        HIP_TRY(launch_plan16_ps_rec(pa, cn, c->ps_side));  // runs beside this chunk's syndrome pass
+        HIP_TRY(hipEventRecord(c->ps_ev_plan[set], c->ps_side));
+        // syndromes (after the zeroing: they read every slot), then the apply (after the records)
+        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_zero[set], 0));
+        ca.dst = static_cast<uint8_t*>(c->d_cs);
+        ca.ids = c->d_ids + c0;
+        ca.units = cn * ca.nchunks;
+        HIP_TRY(launch_cs16(ca, st));
+        const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        c->work_valu += steps * kValu_cs16a;
+        c->work_salu += steps * kSalu_cs16a;
+        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
+        V1Args v{};
+        v.src = static_cast<const uint8_t*>(c->d_cs);
+        v.src_stripe = per;
+        v.src_sym = int64_t(S);
+        v.src_local = 1;
+        v.in_idx = c->d_ps_in;
+        v.dst = base;
+        v.dst_stripe = stripe_stride;
+        v.dst_sym = symbol_stride;
+        v.out_idx = pa.pout;
+        v.idx = pa.rec;
+        v.ids = c->d_ids + c0;
+        v.ps_kr = pa.kr;
+        v.ps_in = 0;
+        v.ps_out = out_stride;
+        v.ps_idx = rec_stride;
+        v.K = D;
+        v.R = rmax;
+        HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
+        HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
+    }
+    if ((rc = syn->note_use(st))) return rc;
+    c->last_kernel = "ps16+cs16+apply_m16_v1_ps";
+    return scratch_release(c, st);
+}
+
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
@@ -1991,6 +2241,11 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups)))
         return decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
                                          int64_t(symbol_stride), n_stripes, symbol_size, is_erased, st);
+    // GF(2^16): more than one pattern -> per-stripe plans on the syndrome route (one shared syndrome pass)
+    if (c->m > 8 && (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > 1)) &&
+        ps16_eligible(c, symbol_size, int64_t(stripe_stride), int64_t(symbol_stride), d_rcv))
+        return decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride), int64_t(symbol_stride),
+                                   n_stripes, symbol_size, is_erased, st);
     std::vector<int32_t> ids;
     std::vector<size_t> first;
     for (auto& g : groups) {
@@ -2020,8 +2275,11 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         DevPlan* p = nullptr;
         int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
         if (rc) return rc;
+        // a pattern shared by every stripe, in order: no stripe-id list (the GF(2^16) route and the re-encode
+        // decode cover only that form)
+        const bool all = g.second.size() == n_stripes && g.second.front() == 0 && g.second.back() == int32_t(n_stripes - 1);
         rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
-                      int64_t(symbol_stride), g.second.size(), symbol_size, st, c->d_ids + first[gi]);
+                      int64_t(symbol_stride), g.second.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
         if (rc) return rc;
         ++gi;
     }

@@ -528,14 +528,27 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     const int64_t stripe = RS_STRIPE(a.ids, local);
     const int64_t chunk0 = (unit - local * a.nchunks) * 1024;
     const int slice = blockIdx.z;
+    // per-stripe plans (rsg_decode_batch, GF(2^16) route): this stripe's K, R, lists and records
+    int Kp = a.K, Rp = a.R;
+    const int32_t* in_list = a.in_idx;
+    const int32_t* out_list = a.out_idx;
+    const uint32_t* idxb = a.idx;
+    if (a.ps_kr) {
+        Kp = sload(a.ps_kr + 2 * local);
+        Rp = sload(a.ps_kr + 2 * local + 1);
+        in_list += local * a.ps_in;
+        out_list += local * a.ps_out;
+        idxb += local * a.ps_idx;
+        if (tile * 64 >= Rp) return;  // the stripe has fewer row tiles than the launch
+    }
     // split-K: this workgroup takes inputs [i0, i0 + K) of the full list
-    const int i0 = a.kslices > 1 ? int(int64_t(a.K) * slice / a.kslices) : 0;
-    const int K = a.kslices > 1 ? int(int64_t(a.K) * (slice + 1) / a.kslices) - i0 : a.K;
+    const int i0 = a.kslices > 1 ? int(int64_t(Kp) * slice / a.kslices) : 0;
+    const int K = a.kslices > 1 ? int(int64_t(Kp) * (slice + 1) / a.kslices) - i0 : Kp;
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
-    const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
-    const int32_t* in_idx = a.in_idx + i0;
+    const uint8_t* gl = a.src + (a.src_local ? local : stripe) * a.src_stripe + chunk0 + 16 * lane;
+    const int32_t* in_idx = in_list + i0;
     auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
     const int nb = (K + 3) / 4;
     auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
@@ -561,7 +574,7 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     asm volatile("s_barrier" ::: "memory");
     // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
     // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
-    const uint32_t* rec = a.idx + (size_t(tile) * (a.K + 1) + i0) * 64;
+    const uint32_t* rec = idxb + (size_t(tile) * (Kp + 1) + i0) * 64;
     u32x16 plane;  // plane 0 of the next step's record, requested one step ahead (s[40:55] in the asm)
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");
     for (int b = 0; b < nb; ++b) {
@@ -578,7 +591,7 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
     }
-    const int rows = min(64, a.R - tile * 64);
+    const int rows = min(64, Rp - tile * 64);
     if (a.kslices > 1) {  // partial products: [slice][stripe][tile * 64 + p][chunk dwords]
         const int64_t nloc = a.units ? a.units / a.nchunks : gridDim.x / a.nchunks;
         const int64_t rpad = int64_t(a.units ? a.tiles : gridDim.y) * 64, cw = a.nchunks * 256;
@@ -593,7 +606,7 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     for (int p = 0; p < 64; ++p) {
         if (p < rows) {
             const uint32_t v = p < 16 ? a0[p & 15] : p < 32 ? a1[p & 15] : p < 48 ? a2[p & 15] : a3[p & 15];
-            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(a.out_idx + tile * 64 + p)) * a.dst_sym) = v;
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out_list + tile * 64 + p)) * a.dst_sym) = v;
         }
     }
 }
@@ -1478,6 +1491,191 @@ hipError_t launch_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_put_rows, dim3(unsigned((units + 255) / 256), unsigned(nrows)), dim3(256), 0, st, dst, dpitch,
                        src, spitch, rows, units);
+    return hipGetLastError();
+}
+
+// ------------------------------------------- per-stripe GF(2^16) decode plans (Ps16Args, rs_kernels.hpp)
+// One workgroup per selected stripe: the erased slots in slot order (ee, and the information ones as rows
+// pe / pout), the coefficients of P(x) = prod (x + X_e), and the erased information slots zeroed.
+__global__ void __launch_bounds__(256) k_plan16_ps(Ps16Args a) {
+    constexpr int Q = kPs16MaxR / 4 + 2;
+    __shared__ uint16_t ee[kPs16MaxR];
+    __shared__ uint16_t sub[4][2][Q];                           // per-wave sub-products (double buffer)
+    __shared__ uint16_t hv[kPs16MaxR + 4], hl[kPs16MaxR + 4];  // halves P01, P23: values, logs
+    __shared__ int cnt[4][2];
+    constexpr uint32_t N = 65535u;
+    constexpr uint16_t kZeroLog = 0xFFFF;
+    const int64_t s = blockIdx.x;
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    const uint8_t* mask = a.masks + s * a.n;
+    uint16_t* pe = a.pe + s * a.out_stride;
+    int32_t* pout = a.pout + s * a.out_stride;
+    int t = 0, R = 0;  // block-uniform running counts
+    for (int c0 = 0; c0 < a.n; c0 += 256) {
+        const int i = c0 + j;
+        const bool er = i < a.n && mask[i] != 0;
+        const bool info = er && i < a.k;
+        const uint64_t be = __ballot(er), bp = __ballot(info);
+        if (lane == 0) {
+            cnt[w][0] = __popcll(be);
+            cnt[w][1] = __popcll(bp);
+        }
+        __syncthreads();
+        int oe = t, op = R, te = 0, tp = 0;
+        for (int v = 0; v < 4; ++v) {
+            if (v < w) oe += cnt[v][0], op += cnt[v][1];
+            te += cnt[v][0];
+            tp += cnt[v][1];
+        }
+        if (er) {
+            const uint16_t x = a.elem[i];
+            const int ie = oe + __popcll(be & below);
+            if (ie < a.r) ee[ie] = x;  // t <= r: checked by the host
+            if (info) {
+                const int ip = op + __popcll(bp & below);
+                pe[ip] = x;
+                pout[ip] = i;
+            }
+        }
+        t += te;
+        R += tp;
+        __syncthreads();  // cnt is rewritten by the next chunk
+    }
+    t = min(t, a.r);
+    for (int p = R + j; p < a.out_stride; p += 256) pe[p] = 0, pout[p] = 0;
+    if (j == 0) {
+        a.kr[2 * s] = t;
+        a.kr[2 * s + 1] = R;
+    }
+    uint16_t* eg = a.ee + s * a.r;
+    for (int e = j; e < t; e += 256) eg[e] = ee[e];
+    auto lg = [&](uint32_t x) -> uint16_t { return x ? a.logt[x] : kZeroLog; };
+    auto emul = [&](uint16_t la, uint16_t lb) -> uint32_t {  // product from logs (kZeroLog: zero)
+        return (la == kZeroLog || lb == kZeroLog) ? 0u : uint32_t(a.expt[(uint32_t(la) + lb) % N]);
+    };
+    // P(x) = prod (x + X_e) as a product tree: wave w multiplies out its quarter of E one linear factor at
+    // a time (wave-synchronous, no block barrier), then the halves P01 = P0 P1, P23 = P2 P3 and P = P01 P23
+    // (one output coefficient per thread, products through the logs of the factors' coefficients).
+    const int q0 = t * w / 4, m = t * (w + 1) / 4 - q0;
+    for (int i = lane; i <= m; i += 64) sub[w][0][i] = i == 0 ? 1 : 0;
+    __builtin_amdgcn_wave_barrier();
+    int cur = 0;
+    for (int e = 0; e < m; ++e) {  // (x + X_e) * B: new[i] = B[i - 1] + X_e B[i]
+        const uint16_t lx = lg(ee[q0 + e]);
+        const uint16_t* o = sub[w][cur];
+        uint16_t* nw = sub[w][cur ^ 1];
+        for (int i = lane; i <= e + 1; i += 64)
+            nw[i] = uint16_t((i ? o[i - 1] : 0u) ^ (i <= e ? emul(lx, lg(o[i])) : 0u));
+        __builtin_amdgcn_wave_barrier();
+        cur ^= 1;
+    }
+    // logs of the sub-products into their free halves
+    for (int i = lane; i <= m; i += 64) sub[w][cur ^ 1][i] = lg(sub[w][cur][i]);
+    __syncthreads();
+    int mq[4], cq[4];
+    for (int v = 0; v < 4; ++v) {
+        mq[v] = t * (v + 1) / 4 - t * v / 4;
+        cq[v] = mq[v] & 1;  // buffer holding sub-product v's values (cur after mq[v] toggles)
+    }
+    const int d01 = mq[0] + mq[1], d23 = mq[2] + mq[3];
+    for (int o = j; o <= d01 + 1 + d23; o += 256) {  // level 1: hv[0 .. d01] = P01, hv[d01 + 1 ..] = P23
+        const int A = o <= d01 ? 0 : 2, oo = o <= d01 ? o : o - d01 - 1;
+        const uint16_t* la = sub[A][cq[A] ^ 1];
+        const uint16_t* lb = sub[A + 1][cq[A + 1] ^ 1];
+        uint32_t acc = 0;
+        for (int x = max(0, oo - mq[A + 1]); x <= min(oo, mq[A]); ++x) acc ^= emul(la[x], lb[oo - x]);
+        hv[o] = uint16_t(acc);
+        hl[o] = lg(acc);
+    }
+    __syncthreads();
+    uint16_t* cg = a.cf + s * (int64_t(a.r) + 1);
+    for (int o = j; o <= t; o += 256) {  // level 2: P = P01 * P23
+        uint32_t acc = 0;
+        for (int x = max(0, o - d23); x <= min(o, d01); ++x) acc ^= emul(hl[x], hl[d01 + 1 + o - x]);
+        cg[o] = uint16_t(acc);
+    }
+    // zero the erased information slots of the stripe (16-byte stores; S and strides are multiples of 16)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint8_t* sb = a.base + int64_t(a.ids[s]) * a.stripe_stride;
+    const int64_t units = a.S / 16;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int p = 0; p < R; ++p) {
+        u32x4* d = reinterpret_cast<u32x4*>(sb + int64_t(pout[p]) * a.symbol_stride);
+        for (int64_t x = j; x < units; x += 256) d[x] = z;
+    }
+}
+
+// The records of W (k_apply_m16_v1 format, see rs_api.cpp:build_plan): one wave per (stripe, 64-row
+// tile), one lane per row p. ld = log prod_{e != p} (X_p + X_e); then the synthetic division of P by
+// (x + X_p) from the top, q_{t-1} = 1, q_{i-1} = cf_i + X_p q_i, emits W[p][i] = q_i / prod for i = t-1 .. 0;
+// the wave packs the 64 rows' index bytes of input i in LDS and stores the 256-byte record.
+__global__ void __launch_bounds__(256) k_plan16_ps_rec(Ps16Args a) {
+    __shared__ uint32_t buf[4][2][64];
+    constexpr uint32_t N = 65535u;
+    const int64_t s = blockIdx.x / a.tblocks;
+    const int wave = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
+    const int tile = int(blockIdx.x - s * a.tblocks) * 4 + wave;
+    const int t = a.kr[2 * s], R = a.kr[2 * s + 1];
+    if (tile * 64 >= R) return;
+    const int row = tile * 64 + lane;
+    const bool live = row < R;
+    const uint16_t* ee = a.ee + s * a.r;
+    const uint16_t* cf = a.cf + s * (int64_t(a.r) + 1);
+    const uint32_t xp = live ? a.pe[s * a.out_stride + row] : 0u;
+    uint32_t ld = 0;
+    if (live) {
+        for (int e = 0; e < t; ++e) {
+            const uint32_t x = ee[e];
+            if (x != xp) ld += a.logt[xp ^ x];
+        }
+        ld %= N;
+    }
+    const uint32_t lxp = a.logt[xp];
+    uint32_t* rec = a.rec + s * a.rec_stride + size_t(tile) * size_t(t + 1) * 64;
+    uint8_t* lb = reinterpret_cast<uint8_t*>(&buf[wave][0][0]);
+    const int slot0 = 4 * (2 * (lane >> 3) + (lane & 1)) + ((lane & 7) >> 1);  // byte of plane 0
+    uint32_t q = 1;
+    for (int i = t - 1; i >= 0; --i) {
+        uint32_t c = 0, lq = 0;
+        if (live && q) {
+            lq = a.logt[q];
+            c = a.expt[(lq + N - ld) % N];
+        }
+        uint8_t* b = lb + (i & 1) * 256;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) b[64 * n + slot0] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
+        __builtin_amdgcn_wave_barrier();
+        rec[size_t(i) * 64 + lane] = reinterpret_cast<const uint32_t*>(b)[lane];
+        if (i > 0) q = uint32_t(cf[i]) ^ (q ? uint32_t(a.expt[(lxp + lq) % N]) : 0u);
+    }
+}
+
+hipError_t launch_plan16_ps(const Ps16Args& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0) return hipSuccess;
+    if (a.r > kPs16MaxR || (a.S & 15) || (a.symbol_stride & 15) || (a.stripe_stride & 15) ||
+        (uintptr_t(a.base) & 15))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_plan16_ps, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan16_ps_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0 || a.tblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_plan16_ps_rec, dim3(unsigned(n_sel * a.tblocks)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st) {
+    const int64_t full = nbytes / 1024;
+    if (n_sel <= 0 || tiles <= 0 || full <= 0) return hipSuccess;
+    if (nbytes % 1024 || !v.ps_kr) return hipErrorInvalidValue;
+    V1Args f = v;
+    f.nchunks = full;
+    f.kslices = 1;
+    f.units = n_sel * full;  // XCD-aware order: a unit's tiles back to back on one XCD
+    f.tiles = tiles;
+    hipLaunchKernelGGL((k_apply_m16_v1<0>), dim3(unsigned((f.units + 7) / 8 * 8 * tiles)), dim3(256), 0, st, f);
     return hipGetLastError();
 }
 

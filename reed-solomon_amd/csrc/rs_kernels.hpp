@@ -90,6 +90,37 @@ struct Plan16Args {
     int32_t K, d, R, rt;
 };
 hipError_t launch_plan_m16(const Plan16Args& a, hipStream_t st);
+// Per-stripe GF(2^16) decode (rsg_decode_batch, the syndrome route with a plan per stripe). With E the
+// stripe's erased slots (t <= r) and P(x) = prod_{e in E} (x + X_e), the reference's evaluator / Forney
+// restore (reed_solomon.c:186-336) solves sum_{e in E} X_e^j d_e = S_j, j < t, over the syndromes of all
+// k + r slots (fft.c:39-100, erased slots read as zero). Its inverse row for erased information slot p is
+// W[p][j] = q_{p,j} / prod_{e != p} (X_p + X_e), q_p = P(x) / (x + X_p) (Lagrange; the same linear map,
+// so results are bit-identical).
+constexpr int kPs16MaxR = 4096;  // r bound of the path (P's product tree lives in LDS)
+struct Ps16Args {
+    const uint8_t* masks;  // [n_sel][n] 1 = erased
+    const uint16_t* elem;  // [n] X_i = alpha^position of slot i
+    const uint16_t* logt;  // [65536] discrete log
+    const uint16_t* expt;  // [65536] alpha^e, e < 65535
+    int32_t k, r, n;
+    int32_t* kr;           // [n_sel][2] t, R (erased information slots)
+    uint16_t* ee;          // [n_sel][r] erased elements X_e, slot order
+    uint16_t* pe;          // [n_sel][out_stride] elements of the erased information slots (rows), zero-padded
+    int32_t* pout;         // [n_sel][out_stride] erased information slots, zero-padded
+    uint16_t* cf;          // [n_sel][r + 1] coefficients of P (cf[t] = 1)
+    int64_t out_stride;    // row tiles * 64
+    uint32_t* rec;         // [n_sel][rec_stride] k_apply_m16_v1 records of W: [tile][t + 1][64] dwords
+    int64_t rec_stride;
+    int32_t tblocks;       // workgroups (4 tiles each) per stripe of the record build
+    uint8_t* base;         // stripes: the erased information slots are zeroed (the syndromes read every slot)
+    int64_t stripe_stride, symbol_stride, S;
+    const int32_t* ids;    // [n_sel] stripe indices
+};
+// lists, P and the zeroing (one workgroup per stripe), then the records (tblocks workgroups per stripe)
+hipError_t launch_plan16_ps(const Ps16Args& a, int64_t n_sel, hipStream_t st);
+hipError_t launch_plan16_ps_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st);
+// k_apply_m16_v1 in per-stripe mode over the full 1 KiB chunks (v.ps_* set, tiles = the largest stripe's)
+hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 // V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 

@@ -34,6 +34,9 @@ struct V1Args {
     // L2 copy of the unit's inputs. units == 0: grid (units, tiles) in the plain order.
     int64_t units;
     int32_t tiles;
+    // k_apply_m16_v1 per-stripe mode (ps_kr set): nonzero = inputs come from the launch-local stripe
+    // (src + local * src_stripe: a per-stripe scratch, e.g. syndromes), outputs from ids (RS_STRIPE)
+    int32_t src_local;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -1,6 +1,7 @@
 """rsg_decode_batch at C5 (k=4096, r=1024, 1 KiB symbols) with a different erasure pattern on every
-stripe: GF(2^16) codes group the stripes by pattern and build one decode plan per pattern on the
-device, then launch per pattern: one plan rebuilt on the stream per pattern (default) vs cached
+stripe: GF(2^16) codes take the per-stripe syndrome route (default since round 3: one syndrome pass over every
+stripe, a device-built t_info x t solve per stripe) or, with m16_ps=0, build one decode plan per
+pattern on the device and launch per pattern (one plan rebuilt on the stream per pattern), or cache
 per-pattern plans (batch_plans=0). Compared with one shared pattern over the same stripes.
 GB/s counts survivors read + information symbols written."""
 import json
@@ -39,8 +40,15 @@ def fp():
 ref_fp = fp()
 orig = dev.clone()  # the codewords: erased repair slots stay zero after a decode (only info is restored)
 mask = torch.from_numpy(pats).to("cuda")
-for label, cdc in (("distinct_patterns_stream_plans", codec),
-                   ("distinct_patterns_cached_plans", rs_amd.Codec(k, r, batch_plans=0))):
+old = rs_amd.Codec(k, r)
+old.set_option("m16_ps", 0)
+runs = [("distinct_patterns_ps16_route", codec)]
+for mib in [int(x) for x in os.environ.get("PS_REC_MIB", "").split(",") if x]:  # chunk-size sweep
+    cm = rs_amd.Codec(k, r)
+    cm.set_option("m16_ps_rec_mib", mib)
+    runs.append((f"distinct_patterns_ps16_route_rec{mib}MiB", cm))
+runs += [("distinct_patterns_stream_plans", old), ("distinct_patterns_cached_plans", rs_amd.Codec(k, r, batch_plans=0))]
+for label, cdc in runs:
     times = []
     for _ in range(3):
         dev.masked_fill_(mask[:, :, None], 0)

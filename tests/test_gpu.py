@@ -371,6 +371,86 @@ def test_decode_batch_m16_stream_plans(k, r, S, n):
     assert np.array_equal(dev.cpu().numpy(), got)
 
 
+def test_decode_batch_m16_per_stripe_route_vs_golden():
+    """rsg_decode_batch at C5 with a different pattern on every stripe (reference reed_solomon.c:443-559):
+    the per-stripe GF(2^16) route (one syndrome pass over all k + r slots, then each stripe's own
+    device-built t_info x t solve). Every stripe's output equals the reference golden of its pattern;
+    erased information slots hold garbage on input; a repair-only stripe and a stripe without erasures
+    are left untouched."""
+    cases = [case(nm) for nm in GPU_CASES if nm.startswith("c5ps_")]
+    assert len(cases) >= 8
+    k, r, S = 4096, 1024, 1024
+    buf0, _ = case_inputs(cases[0], 0)
+    n = len(cases) + 2
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    dev[:, :k] = torch.from_numpy(buf0[:k]).cuda()
+    codec = rs_amd.Codec(k, r)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s, c in enumerate(cases):
+        pats[s, c["erased"]] = True
+    pats[len(cases), k + np.arange(5)] = True  # repair-only: nothing to restore
+    rng = np.random.default_rng(5)
+    host = full.copy()
+    host[pats] = 0
+    info_er = pats.copy()
+    info_er[:, k:] = False
+    host[info_er] = rng.integers(0, 256, (int(info_er.sum()), S), dtype=np.uint8)  # garbage: zeroed first
+    dev.copy_(torch.from_numpy(host))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert codec.last_kernel == "ps16+cs16+apply_m16_v1_ps", codec.last_kernel
+    got = dev.cpu().numpy()
+    for s, c in enumerate(cases):
+        check_golden(c, got[s].tobytes())
+    assert np.array_equal(got[len(cases)], host[len(cases)])
+    assert np.array_equal(got[-1], full[-1])
+
+
+@pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 37), (300, 64, 1024, 70), (600, 100, 3072, 5)])
+def test_decode_batch_m16_per_stripe_route(k, r, S, n):
+    """The per-stripe GF(2^16) route on assorted shapes: random patterns of 1..r erasures anywhere (garbage
+    in erased slots), against the oracle on a sample and byte-identical to the per-pattern plans
+    (m16_ps = 0); erased repair slots keep what they held."""
+    rng = np.random.default_rng(k + r + n)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xE1)
+    codec = rs_amd.Codec(k, r)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    pats[0, :] = False
+    pats[0, :r] = True  # r information erasures
+    host = full.copy()
+    host[pats] = rng.integers(0, 256, (int(pats.sum()), S), dtype=np.uint8)
+    dev.copy_(torch.from_numpy(host))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert codec.last_kernel == "ps16+cs16+apply_m16_v1_ps", codec.last_kernel
+    got = dev.cpu().numpy()
+    assert np.array_equal(got[:, :k], full[:, :k])
+    rep = pats.copy()
+    rep[:, :k] = False
+    assert np.array_equal(got[rep], host[rep])  # erased repair slots not written
+    for s in list(range(0, n, max(1, n // 5))) + [n - 1]:
+        want = host[s].copy()
+        want[pats[s]] = 0
+        assert oracle_decode(k, r, want, pats[s], int(pats[s].sum())) == 0
+        assert np.array_equal(got[s, :k], want[:k]), f"stripe {s}"
+    old = rs_amd.Codec(k, r)
+    old.set_option("m16_ps", 0)
+    dev.copy_(torch.from_numpy(host))
+    assert old.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert old.last_kernel != codec.last_kernel
+    assert np.array_equal(dev.cpu().numpy()[:, :k], got[:, :k])
+
+
 @pytest.mark.parametrize("route", [0, 1])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030)])
@@ -521,6 +601,8 @@ def test_m16_route_encode_then_decode_on_two_streams():
     er[rng.choice(k + r, 40, replace=False)] = True  # t <= 64: the route at once
     poisoned = full_b.copy()
     poisoned[:, er] = 0
+    want_b = full_b.copy()
+    want_b[:, k:][:, er[k:]] = 0  # erased repair slots are not restored
     b.copy_(torch.from_numpy(poisoned))
     torch.cuda.synchronize()
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
@@ -530,7 +612,7 @@ def test_m16_route_encode_then_decode_on_two_streams():
         codec.decode(b, er, stream=sb)
         assert codec.last_kernel.startswith("cs16+"), codec.last_kernel
         torch.cuda.synchronize()
-        assert np.array_equal(b.cpu().numpy(), full_b)
+        assert np.array_equal(b.cpu().numpy(), want_b)
         b.copy_(torch.from_numpy(poisoned))
         torch.cuda.synchronize()
     got = a.cpu().numpy()
