@@ -127,6 +127,13 @@ int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
  * (out = m2 * syndromes). info = {D, ngroups, ntiles, fin_stride, R}; arrays may be NULL. Host only. */
 int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                    uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2);
+/* The k_bs16 second stage of the GF(2^16) route for the encode (is_erased NULL) or decode matrix, when it
+ * applies (encode: the repair cosets; decode: an erased set closed under x -> x^(2^d), d < 16): records
+ * [ntiles][ngroups + 2][4][64] bytes, finish lists [ntiles][fin_stride] (local coset | rotation << 4 |
+ * output slot << 8) and [ntiles][5]. info = {applies, D, ngroups, ntiles, fin_stride, d}; arrays may be
+ * NULL and are written only when it applies. Host only. */
+int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
+                  int32_t* fin, int32_t* fin_off);
 const char* rsg_version(void);
 
 #ifdef __cplusplus

@@ -889,26 +889,32 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
 // coset c accumulates u_t = sum_j bit_t(z_(c, j)) S_j with z = normal repr of M2[L][j], and the finish
 // S_(L 2^b) = sum_t nb_((t + b) mod 16) u_t gives all its outputs (as k_cs16's). Returns false when the
 // rows do not have that structure (then the plain matrix plan applies M2).
+//
+// Decode (round 3): when the erased set E is closed under x -> x^(2^d) (d in {2, 4, 8}: e.g. the bench
+// pattern, every 4th slot of 16-slot cosets, is closed under x^16), Lambda_E has coefficients in
+// GF(2^d) and the rows along an orbit {X, X^(2^d), ...} are conjugates by the same rule with step d:
+// runs of rows whose positions multiply by 2^d, finish rotation d * b. d = 1 is the encode case.
 static bool bs16_host(const std::vector<uint16_t>& M2, int D, const std::vector<uint16_t>& targets,
-                      const std::vector<int>& emit, const std::vector<int32_t>& out_slots, CsHost& h) {
+                      const std::vector<int>& emit, const std::vector<int32_t>& out_slots, CsHost& h, int d = 1) {
     const Field& F = field();
     const int R = int(emit.size());
-    // output cosets: runs of rows whose positions double
+    // output orbits: runs of rows whose positions multiply by 2^d (at most 16 / d rows)
     std::vector<std::pair<int, int>> cos;  // (first row, size)
     for (int r = 0; r < R;) {
         int e = r + 1;
-        while (e < R && e - r < 16 &&
-               targets[size_t(emit[size_t(e)])] == uint16_t((uint32_t(targets[size_t(emit[size_t(e - 1)])]) << 1) % kN))
+        while (e < R && e - r < 16 / d &&
+               targets[size_t(emit[size_t(e)])] == uint16_t((uint64_t(targets[size_t(emit[size_t(e - 1)])]) << d) % kN))
             ++e;
         cos.emplace_back(r, e - r);
         r = e;
     }
-    for (auto& c : cos)  // M2[r0 + b][j] = M2[r0 + b - 1][j]^2
+    for (auto& c : cos)  // M2[r0 + b][j] = M2[r0 + b - 1][j]^(2^d)
         for (int b = 1; b < c.second; ++b)
             for (int j = 0; j < D; ++j) {
                 const uint16_t x = M2[size_t(c.first + b - 1) * D + j];
-                if (M2[size_t(c.first + b) * D + j] != (x ? F.exp[(2u * F.log[x]) % kN] : 0)) return false;
+                if (M2[size_t(c.first + b) * D + j] != (x ? F.exp[((uint64_t(1) << d) * F.log[x]) % kN] : 0)) return false;
             }
+    if (d > 1 && 2 * cos.size() > size_t(R)) return false;  // runs shorter than 2 rows on average: dense is cheaper
     constexpr int CW = 4;
     const int ngr = (D + 15) / 16, ng = ngr + (ngr & 1), C = int(cos.size()), ntiles = (C + CW - 1) / CW;
     h = CsHost();
@@ -937,7 +943,7 @@ static bool bs16_host(const std::vector<uint16_t>& M2, int D, const std::vector<
             if (c >= C) continue;
             const int r0 = cos[size_t(c)].first;
             for (int b = 0; b < cos[size_t(c)].second; ++b)
-                h.fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (b << 4) | (out_slots[size_t(r0 + b)] << 8);
+                h.fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | ((d * b) << 4) | (out_slots[size_t(r0 + b)] << 8);
             for (int j = 0; j < D; ++j) {
                 const uint16_t v = M2[size_t(r0) * D + j];
                 z[size_t(j)] = v ? rep[F.log[v]] : 0;
@@ -958,6 +964,23 @@ static bool bs16_host(const std::vector<uint16_t>& M2, int D, const std::vector<
         h.fin_off[size_t(t) * (CW + 1) + CW] = e;
     }
     return true;
+}
+
+// Smallest d in {1, 2, 4, 8} such that the position set is closed under p -> p * 2^d (mod N), i.e. the
+// erased elements under x -> x^(2^d); 16 when none is.
+static int orbit_step(const std::vector<uint16_t>& pos) {
+    std::vector<char> in(kN, 0);
+    for (uint16_t p : pos) in[p % kN] = 1;
+    for (int d = 1; d < 16; d *= 2) {
+        bool closed = true;
+        for (uint16_t p : pos)
+            if (!in[size_t((uint64_t(p) << d) % kN)]) {
+                closed = false;
+                break;
+            }
+        if (closed) return d;
+    }
+    return 16;
 }
 
 // the syndrome route pays when both sides of the matrix are large
@@ -991,7 +1014,9 @@ static int make_plan_cs(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevP
     std::vector<uint16_t> M2 = syndrome_solve_matrix(targets, emit);
     std::unique_ptr<DevPlan> second;
     CsHost bh;
-    if (!erased && bs16_host(M2, D, targets, emit, outs, bh)) {  // encode: Frobenius rows, k_bs16
+    // encode: Frobenius rows, k_bs16; decode: the same when E is closed under a Frobenius power (orbit_step)
+    const int dstep = erased ? orbit_step(targets) : 1;
+    if (dstep < 16 && bs16_host(M2, D, targets, emit, outs, bh, dstep)) {
         second = std::make_unique<DevPlan>();
         second->device = c->device;
         second->m = 16;
@@ -1019,7 +1044,13 @@ static bool reenc_eligible(const rsg_codec_t* c, const bool* erased) {
     for (int i = 0; i < c->k; ++i) t += erased[i] ? 1 : 0;
     for (int i = c->k; i < c->k + c->r; ++i)
         if (erased[i]) return false;
-    return t >= 1 && 10 * t >= 9 * c->r && c->k - t >= 64;
+    if (!(t >= 1 && 10 * t >= 9 * c->r && c->k - t >= 64)) return false;
+    // an erased set closed under x -> x^16 (or a smaller Frobenius step) gives the plain route a k_bs16
+    // second stage with orbits of >= 4 rows (bs16_host): cheaper than re-encoding + the dense t x r stage
+    std::vector<uint16_t> pos;
+    for (int i = 0; i < c->k; ++i)
+        if (erased[i]) pos.push_back(c->positions[size_t(i)]);
+    return orbit_step(pos) > 4;
 }
 
 static int make_plan_reenc(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {
@@ -3113,27 +3144,23 @@ extern "C" void cc_cosets_to_positions(const coset_t* cs, uint16_t cosets_cnt, u
 
 // ============================================================================ context-free host ops
 // gf_add / gf_mul / gf_madd and the fft_* transforms take host symbols and no codec. They run on the
-// GPU through one process-wide engine: the current device at first use, one non-blocking stream,
-// pinned + device staging that only grows, and an m = 16 codec shell whose matrix kernels, options
-// and split-K scratch the transforms use. Calls are serialised by the engine's mutex.
+// GPU through a pool of engines: a call leases one (a mutex only around the pool's free list, so
+// concurrent callers run side by side), and each engine has its own non-blocking stream, page-locked
+// mapped staging that only grows (with its device-visible address) and an m = 16 codec shell whose
+// matrix kernels, options and split-K scratch the transforms use. An engine serves the device that was
+// current when it was created; leases prefer an engine of the caller's current device.
 namespace {
 
 struct HostOps {
-    std::mutex mu;
     int device = -1;
     hipStream_t stream = nullptr;
-    uint8_t* h = nullptr;
-    uint8_t* d = nullptr;
-    size_t cap = 0;
+    uint8_t* h = nullptr;   // page-locked, mapped
+    uint8_t* hd = nullptr;  // its device-visible address (zero-copy kernels)
+    uint8_t* d = nullptr;   // device staging (transforms)
+    size_t cap = 0, dcap = 0;
     std::unique_ptr<rsg_codec> codec;
-    int init() {
+    int init(int dev) {
         if (device >= 0) return 0;
-        int ndev = 0, dev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-            std::fprintf(stderr, "librs_amd: no usable HIP device for the symbol operations (no CPU fallback)\n");
-            return RS_ERR_DEVICE;
-        }
-        HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipSetDevice(dev));
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         auto c = std::make_unique<rsg_codec>();
@@ -3144,44 +3171,110 @@ struct HostOps {
         device = dev;
         return 0;
     }
-    int reserve(size_t bytes) {
+    int reserve_host(size_t bytes) {  // mapped staging
         if (bytes <= cap) return 0;
         if (h) (void)hipHostFree(h);
-        if (d) (void)hipFree(d);
-        h = nullptr;
-        d = nullptr;
+        h = hd = nullptr;
         cap = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h), bytes, hipHostMallocMapped | hipHostMallocPortable));
+        void* dv = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dv, h, 0));
+        hd = static_cast<uint8_t*>(dv);
         cap = bytes;
+        return 0;
+    }
+    int reserve_dev(size_t bytes) {
+        if (bytes <= dcap) return 0;
+        if (d) (void)hipFree(d);
+        d = nullptr;
+        dcap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+        dcap = bytes;
         return 0;
     }
 };
 
-HostOps& hostops() {
-    static HostOps* ops = new HostOps();  // never destroyed: outlives the HIP runtime's teardown
-    return *ops;
+struct HostOpsPool {
+    std::mutex mu;
+    std::map<int, std::vector<HostOps*>> idle;  // per device; engines are never destroyed (they outlive
+                                                // the HIP runtime's teardown at exit)
+};
+HostOpsPool& hostops_pool() {
+    static HostOpsPool* p = new HostOpsPool();
+    return *p;
 }
 
-// a ^= b (op 0), a = coef * a (1), a ^= coef * b (2) over symbol_size / 2 words, on the GPU
+// an engine for the duration of one call
+struct EngineLease {
+    HostOps* e = nullptr;
+    int rc = 0;
+    EngineLease() {
+        int ndev = 0, dev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            std::fprintf(stderr, "librs_amd: no usable HIP device for the symbol operations (no CPU fallback)\n");
+            rc = RS_ERR_DEVICE;
+            return;
+        }
+        HostOpsPool& P = hostops_pool();
+        {
+            std::lock_guard<std::mutex> lk(P.mu);
+            auto& v = P.idle[dev];
+            if (!v.empty()) {
+                e = v.back();
+                v.pop_back();
+            }
+        }
+        if (!e) e = new HostOps();
+        rc = e->init(dev);
+        if (!rc && hipSetDevice(e->device) != hipSuccess) rc = RS_ERR_DEVICE;
+    }
+    ~EngineLease() {
+        if (!e) return;
+        if (e->device < 0) {  // never initialised: nothing to keep
+            delete e;
+            return;
+        }
+        HostOpsPool& P = hostops_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.idle[e->device].push_back(e);
+    }
+};
+
+constexpr size_t kSymbolOpDmaBytes = size_t(256) << 10;
+
+// a ^= b (op 0), a = coef * a (1), a ^= coef * b (2) over symbol_size / 2 words, on the GPU: the operands
+// are copied into the engine's mapped staging and one kernel reads and writes them there across PCIe
+// (zero-copy: no DMA round trips); its completion is the call's only wait
 int symbol_op(int op, void* a, element_t coef, const void* b, size_t symbol_size) {
     const size_t nw = symbol_size / 2, bytes = nw * 2, P = pad16(bytes);
     if (!nw) return 0;
-    HostOps& o = hostops();
-    std::lock_guard<std::mutex> lk(o.mu);
-    if (int rc = o.init()) return rc;
-    HIP_TRY(hipSetDevice(o.device));
-    if (int rc = o.reserve(2 * P)) return rc;
+    EngineLease L;
+    if (L.rc) return L.rc;
+    HostOps& o = *L.e;
+    if (int rc = o.reserve_host(2 * P)) return rc;
     const uint16_t *logt = nullptr, *expt = nullptr;
     const uint8_t* g8 = nullptr;
     if (int rc = plan_tables(o.device, &logt, &g8, &expt)) return rc;
     std::memcpy(o.h, a, bytes);
-    if (op != 1) std::memcpy(o.h + P, b, bytes);
-    HIP_TRY(hipMemcpyAsync(o.d, o.h, op != 1 ? P + bytes : bytes, hipMemcpyHostToDevice, o.stream));
+    if (P > bytes) std::memset(o.h + bytes, 0, P - bytes);
+    if (op != 1) {
+        std::memcpy(o.h + P, b, bytes);
+        if (P > bytes) std::memset(o.h + P + bytes, 0, P - bytes);
+    }
     const uint32_t lc = op == 0 ? 0u : field().log[coef];
-    HIP_TRY(launch_symbol_op(reinterpret_cast<uint16_t*>(o.d), reinterpret_cast<const uint16_t*>(o.d + P), op, lc,
-                             int64_t(nw), logt, expt, o.stream));
-    HIP_TRY(hipMemcpyAsync(o.h, o.d, bytes, hipMemcpyDeviceToHost, o.stream));
+    // large operands: DMA in and out (the copy engines beat the kernel's own PCIe reads there: 1 MiB
+    // gf_madd 172 us with DMA vs 199 us zero-copy, profiles/r3_hostops.jsonl)
+    const bool dma = P >= kSymbolOpDmaBytes;
+    uint8_t* dv = o.hd;
+    if (dma) {
+        if (int rc = o.reserve_dev(2 * P)) return rc;
+        dv = o.d;
+        HIP_TRY(hipMemcpyAsync(o.d, o.h, op != 1 ? 2 * P : P, hipMemcpyHostToDevice, o.stream));
+    }
+    HIP_TRY(launch_symbol_op(reinterpret_cast<uint16_t*>(dv), reinterpret_cast<const uint16_t*>(dv + P), op, lc,
+                             int64_t(P / 2), logt, expt, o.stream));
+    if (dma) HIP_TRY(hipMemcpyAsync(o.h, o.d, bytes, hipMemcpyDeviceToHost, o.stream));
     HIP_TRY(hipStreamSynchronize(o.stream));
     std::memcpy(a, o.h, bytes);
     return 0;
@@ -3206,12 +3299,12 @@ int transform_apply(std::vector<uint16_t> M, const symbol_seq_t* f, symbol_seq_t
         return 0;
     }
     if (K > kN || R > kN) return RS_ERR_INVALID;
-    HostOps& o = hostops();
-    std::lock_guard<std::mutex> lk(o.mu);
-    if (int rc = o.init()) return rc;
-    HIP_TRY(hipSetDevice(o.device));
+    EngineLease L;
+    if (L.rc) return L.rc;
+    HostOps& o = *L.e;
     const size_t P = pad16(Se);
-    if (int rc = o.reserve((K + R) * P)) return rc;
+    if (int rc = o.reserve_host((K + R) * P)) return rc;
+    if (int rc = o.reserve_dev((K + R) * P)) return rc;
     for (size_t i = 0; i < K; ++i) std::memcpy(o.h + i * P, f->symbols[i]->data, Se);
     HIP_TRY(hipMemcpyAsync(o.d, o.h, K * P, hipMemcpyHostToDevice, o.stream));
     std::vector<int32_t> in(K), out(R);
@@ -3325,6 +3418,33 @@ extern "C" int fft_partial_transform_cycl(GF_t* gf, const symbol_seq_t* f, const
 // Host-only view of the GF(2^16) syndrome route of the encode (is_erased == NULL) or decode matrix: the
 // k_cs16 plan (groups, records, finish lists) and the second-stage matrix M2 [R][D]. info = {D, ngroups,
 // ntiles, fin_stride, R}; array arguments may be NULL (query the sizes first). No GPU is used.
+extern "C" int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
+                             int32_t* fin, int32_t* fin_off) {
+    if (uint32_t(k) + r > kN || (is_erased && t > r)) return RS_ERR_INVALID;
+    const std::vector<uint16_t> pos = code_positions(k, r);
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(pos, k, r, is_erased, targets, emit, sources, in, outs);
+    const int D = int(targets.size());
+    const std::vector<uint16_t> M2 = syndrome_solve_matrix(targets, emit);
+    const int d = is_erased ? orbit_step(targets) : 1;
+    CsHost h;
+    const bool ok = d < 16 && bs16_host(M2, D, targets, emit, outs, h, d);
+    if (info) {
+        info[0] = ok ? 1 : 0;
+        info[1] = D;
+        info[2] = ok ? h.ngroups : 0;
+        info[3] = ok ? h.ntiles : 0;
+        info[4] = ok ? h.fin_stride : 0;
+        info[5] = d;
+    }
+    if (ok && rec) std::memcpy(rec, h.rec.data(), h.rec.size());
+    if (ok && fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
+    if (ok && fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);
+    return 0;
+}
+
 extern "C" int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                               uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2) {
     if (uint32_t(k) + r > kN || (is_erased && t > r)) return RS_ERR_INVALID;

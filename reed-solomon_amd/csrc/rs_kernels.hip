@@ -896,25 +896,42 @@ hipError_t launch_cs16(const Cs16Args& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------- symbol-wide ops (gf_add / gf_mul / gf_madd)
-// One word (LE u16) per lane, reference src/rs/gf65536.c:155-219: add a ^= b; mul a = c * a; madd
+// Eight words (16 bytes) per lane, reference src/rs/gf65536.c:155-219: add a ^= b; mul a = c * a; madd
 // a ^= c * b, products through the log / exp tables with zero words skipped (lc = log c, c != 0, 1).
+// nw is a multiple of 8 (the callers' staging is padded with zero words: a zero word of b adds nothing,
+// a zero word of a stays zero under mul); 16-byte accesses also suit operands read across PCIe.
 __global__ void __launch_bounds__(256) k_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw,
                                                    const uint16_t* __restrict__ logt, const uint16_t* __restrict__ expt) {
-    for (int64_t w = int64_t(blockIdx.x) * 256 + threadIdx.x; w < nw; w += int64_t(gridDim.x) * 256) {
-        const uint32_t x = op == 1 ? a[w] : b[w];
-        uint32_t v = x;
-        if (op != 0 && x) {
-            const uint32_t e = logt[x] + lc;
-            v = expt[e >= 65535u ? e - 65535u : e];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const int64_t nu = nw / 8;
+    for (int64_t u = int64_t(blockIdx.x) * 256 + threadIdx.x; u < nu; u += int64_t(gridDim.x) * 256) {
+        u32x4 va = reinterpret_cast<u32x4*>(a)[u];
+        const u32x4 src = op == 1 ? va : reinterpret_cast<const u32x4*>(b)[u];
+        u32x4 v = src;
+        if (op != 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t r = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t x = (src[q] >> (16 * h)) & 0xFFFFu;
+                    if (x) {
+                        const uint32_t e = logt[x] + lc;
+                        r |= uint32_t(expt[e >= 65535u ? e - 65535u : e]) << (16 * h);
+                    }
+                }
+                v[q] = r;
+            }
         }
-        a[w] = op == 1 ? uint16_t(v) : uint16_t(a[w] ^ v);
+        reinterpret_cast<u32x4*>(a)[u] = op == 1 ? v : (va ^ v);
     }
 }
 
 hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw, const uint16_t* logt,
                             const uint16_t* expt, hipStream_t st) {
     if (nw <= 0) return hipSuccess;
-    const unsigned grid = unsigned(std::min<int64_t>((nw + 255) / 256, 4096));
+    if (nw % 8 || (uintptr_t(a) | uintptr_t(b)) % 16) return hipErrorInvalidValue;
+    const unsigned grid = unsigned(std::min<int64_t>((nw / 8 + 255) / 256, 4096));
     hipLaunchKernelGGL(k_symbol_op, dim3(grid), dim3(256), 0, st, a, b, op, lc, nw, logt, expt);
     return hipGetLastError();
 }

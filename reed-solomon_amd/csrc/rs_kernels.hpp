@@ -168,8 +168,8 @@ hipError_t launch_bs16(const Cs16Args& a, hipStream_t st);
 // goff[i] = slots[i] * sym (0x80000000 for slots[i] < 0), i < n
 hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t sym, hipStream_t st);
 
-// symbol-wide word ops over nw words: op 0 a ^= b, 1 a = c * a, 2 a ^= c * b (lc = log c; logt / expt:
-// discrete log and alpha^i tables, i < 65535)
+// symbol-wide word ops over nw words (a multiple of 8; a, b 16-byte aligned): op 0 a ^= b, 1 a = c * a,
+// 2 a ^= c * b (lc = log c; logt / expt: discrete log and alpha^i tables, i < 65535)
 hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw, const uint16_t* logt,
                             const uint16_t* expt, hipStream_t st);
 

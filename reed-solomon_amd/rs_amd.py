@@ -93,6 +93,7 @@ _sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
 _sig("rsg_jit_precompile", ctypes.c_int, u16, u16, P, u16)
 _sig("rsg_gamma_tables", ctypes.c_int, P, P, P)
 _sig("rsg_route_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P, P)
+_sig("rsg_bs16_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("gf_create", P)
 _sig("gf_destroy", None, P)
@@ -164,6 +165,28 @@ def route_dump(k, r, is_erased=None):
     if rc:
         raise RSError(rc, "rsg_route_dump")
     return dict(D=D, groups=groups, rec=rec, fin=fin, fin_off=fin_off, m2=m2)
+
+
+def bs16_dump(k, r, is_erased=None):
+    """The k_bs16 second stage of the GF(2^16) route (host only), or None when it does not apply: dict
+    with D, d (Frobenius step of the row orbits), rec [ntiles][ngroups + 2][4][64] (bytes), fin
+    [ntiles][fin_stride], fin_off [ntiles][5]."""
+    er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
+    t = 0 if er is None else int(er.sum())
+    info = np.zeros(6, np.int32)
+    rc = _lib.rsg_bs16_dump(k, r, _np_ptr(er), t, _np_ptr(info), None, None, None)
+    if rc:
+        raise RSError(rc, "rsg_bs16_dump")
+    ok, D, ng, nt, fs, d = (int(v) for v in info)
+    if not ok:
+        return None
+    rec = np.zeros((nt, ng + 2, 4, 64), np.uint8)
+    fin = np.zeros((nt, fs), np.int32)
+    fin_off = np.zeros((nt, 5), np.int32)
+    rc = _lib.rsg_bs16_dump(k, r, _np_ptr(er), t, None, _np_ptr(rec), _np_ptr(fin), _np_ptr(fin_off))
+    if rc:
+        raise RSError(rc, "rsg_bs16_dump")
+    return dict(D=D, d=d, ngroups=ng, rec=rec, fin=fin, fin_off=fin_off)
 
 
 def gamma_tables():

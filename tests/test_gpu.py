@@ -572,14 +572,19 @@ def test_decode_batch_back_to_back_streams(plans):
 def test_c5_bench_decode_kernels_vs_golden(name):
     """The C5 bench decode's kernels (reference reed_solomon.c:443-559) pinned to the reference goldens at
     full 1 KiB chunks, n = 1 and n = 2 stripes: with m16_route_min_bytes = 0 the first launch takes the
-    route -- the re-encode decode (encode route over the surviving information + repair XOR + D_Rep)
-    for information-only patterns with t >= 0.9 r, the plain syndrome route for patterns with repair
-    erasures."""
+    route -- for the bench pattern (closed under x -> x^16) the plain syndrome route with the k_bs16
+    second stage over row orbits of 4; for other information-only patterns with t >= 0.9 r the
+    re-encode decode (encode route over the surviving information + repair XOR + D_Rep); the plain
+    route with the dense second stage for patterns with repair erasures."""
     c = case(name)
     rc, out, kern, m = run_case_gpu(c, "auto", {"m16_route_min_bytes": 0})
     assert rc == c["rc"] == 0 and m == 16
-    mixed = any(e >= c["k"] for e in c["erased"])
-    assert kern.startswith("cs16+apply" if mixed else "cs16+bs16+xor+"), kern
+    if "bench" in name:  # erased set closed under x -> x^16: the plain route with the k_bs16 second stage
+        assert kern == "cs16+bs16", kern
+    elif any(e >= c["k"] for e in c["erased"]):
+        assert kern.startswith("cs16+apply"), kern
+    else:
+        assert kern.startswith("cs16+bs16+xor+"), kern
     check_golden(c, out)
 
 

@@ -101,3 +101,73 @@ def test_cs16_plan_model_gives_the_syndromes(kind, k, r, t):
     want = gf_apply(H, X[srcs].astype(np.uint16))
     assert np.array_equal(got.astype(np.uint16), want)
     assert sorted(set(np.concatenate([d["groups"].ravel(), [-1]]))) == [-1] + srcs  # each source in one group slot
+
+
+def _model_bs16(d, Syn, nb):
+    """k_bs16's arithmetic on CPU: syndromes Syn [D][W] -> {output slot: words}. Per (tile, group of 16
+    syndromes) four subset tables over syndromes 4q .. 4q + 3; record byte 16q + t of a local coset is the
+    table index added into accumulator u_t; finish out = sum_t nb_((t + b) mod 16) u_t."""
+    exp, log = gf_tables()
+    rec, fin, fin_off = d["rec"], d["fin"], d["fin_off"]
+    nt, W, D = rec.shape[0], Syn.shape[1], d["D"]
+    out = {}
+    for tile in range(nt):
+        acc = np.zeros((4, 16, W), np.int64)
+        for g in range(d["ngroups"]):
+            f = np.array([Syn[16 * g + i] if 16 * g + i < D else np.zeros(W, np.int64) for i in range(16)])
+            for q in range(4):
+                tab = np.zeros((16, W), np.int64)
+                for e in range(16):
+                    for dd in range(4):
+                        if e >> dd & 1:
+                            tab[e] ^= f[4 * q + dd]
+                for c in range(4):
+                    for tb in range(16):
+                        acc[c, tb] ^= tab[rec[tile, g, c, 16 * q + tb]]
+        for c in range(4):
+            for e in range(fin_off[tile, c], fin_off[tile, c + 1]):
+                ent = int(fin[tile, e])
+                assert ent & 15 == c
+                b, slot = (ent >> 4) & 15, ent >> 8
+                v = np.zeros(W, np.int64)
+                for t in range(16):
+                    u = acc[c, t]
+                    v ^= np.where(u != 0, exp[(log[u] + log[nb[(t + b) % 16]]) % 65535], 0)
+                out[slot] = v
+    return out
+
+
+@pytest.mark.parametrize("kind,k,r,t,step", [("enc", 300, 200, None, 1), ("dec_bench", 4096, 1024, 1024, 4),
+                                              ("dec_bench", 1024, 256, 256, 4), ("dec_cosets", 640, 128, 96, 1),
+                                              ("dec", 600, 100, 80, None)])
+def test_bs16_second_stage_model(kind, k, r, t, step):
+    """k_bs16 as the route's second stage: the encode (repair cosets, Frobenius step 1) and decodes whose
+    erased set is closed under a Frobenius power (the C5 bench pattern: every 4th slot of the 16-slot
+    information cosets, closed under x -> x^16; whole information cosets: step 1). A numpy model of the
+    kernel over the dumped records equals M2 * syndromes for every output; a random pattern has no such
+    structure (None: the dense second stage)."""
+    er = None
+    if kind == "dec_bench":
+        er = _pattern(kind, k, r, t)
+    elif kind == "dec_cosets":  # whole 16-slot information cosets (slots 16 i .. 16 i + 15 of the first t / 16)
+        er = np.zeros(k + r, bool)
+        er[:t] = True
+    elif kind == "dec":
+        er = _pattern(kind, k, r, t, seed=9)
+    d = rs_amd.bs16_dump(k, r, er)
+    if step is None:
+        assert d is None
+        return
+    assert d is not None and d["d"] == step
+    route = rs_amd.route_dump(k, r, er)
+    m2 = route["m2"]
+    rng = np.random.default_rng(k + r)
+    Syn = rng.integers(0, 65536, (d["D"], 2)).astype(np.int64)
+    got = _model_bs16(d, Syn, normal_basis(16))
+    _, _, tgts = _lists(k, r, er)
+    outs = [s for s in (range(k, k + r) if er is None else tgts) if er is None or s < k]
+    want = gf_apply(m2, Syn.astype(np.uint16))
+    slots = [s - k for s in outs] if er is None else outs
+    assert sorted(got) == sorted(slots)
+    for i, sl in enumerate(slots):
+        assert np.array_equal(got[sl].astype(np.uint16), want[i]), f"output slot {sl}"
