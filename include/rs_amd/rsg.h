@@ -37,21 +37,36 @@ void rsg_codec_destroy(rsg_codec_t* c);
 /* Subfield degree m of the code (8 => GF(256) kernels, 16 => general kernels). */
 int rsg_codec_subfield(const rsg_codec_t* c);
 
-/* Options: "m8_mode" for GF(256) codes without a specialised kernel (18 = one dword per lane,
- * gpr-index lookups, the default; 2 = two dwords per lane; 0 = register tables with compiler
- * indexing; 1 = masked multiples; 10-19 timing ablations), "jit" (matrix-specialised kernels
- * compiled with hiprtc and cached on disk: 0 = off, 1 = every eligible matrix, 2 = the encode matrix
- * and decode matrices from their second use, the default), "dec_jit_uses" (launches of a decode plan
- * of at least 1 MiB before it is specialised under jit = 2; default 2), "xj" (1 = bit-plane XOR kernels, the default;
- * 0 = nibble-table kernels), "batch_plans" (rsg_decode_batch: 0 = host plans per distinct pattern,
- * 1 = device-built plans -- per stripe for m <= 8, rebuilt on the stream per pattern for GF(2^16) codes --,
- * 2 = device plans above 16 distinct patterns, the default), "syn_route"
- * (device-plan decodes of m <= 8 codes with symbol sizes a multiple of 2 KiB: 1 = syndromes of every slot on
- * the bit-plane XOR kernel, then a per-stripe t_info x t solve, the default; 0 = per-stripe survivor
- * matrices), "m16_mode"
- * (GF(2^16) codes: 0 = hand-scheduled gpr-index kernel for more than 32 outputs, the default; 1 = its
- * timing ablation; 2 = the compiled kernel), "m16_plans" (GF(2^16) coding matrices: 0 = built on the
- * host, 1 = on the device, 2 = on the device from 64K coefficients, the default; rebuilds the encode plan).
+/* Options (release build; every value gives identical results, they choose kernels and plans):
+ *   "jit"          matrix-specialised GF(256) kernels (hiprtc, cached on disk): 0 off, 1 every eligible
+ *                  matrix, 2 the encode matrix and decode matrices from their dec_jit_uses-th launch
+ *                  (default)
+ *   "dec_jit_uses" launches of >= 1 MiB before a decode plan is specialised under jit = 2 (default 2)
+ *   "xj"           specialised family: 1 bit-plane XOR kernels (default), 0 nibble-table kernels
+ *   "m8_mode"      GF(256) kernel without specialisation: 18 one dword per lane, gpr-index lookups
+ *                  (default); 2 two dwords per lane; 0 register tables, compiler indexing; 1 masked
+ *                  multiples; 3, 4, 14 other register layouts of the gpr-index kernels
+ *   "batch_plans"  rsg_decode_batch: 0 host plans per distinct pattern; 1 device-built plans (GF(256):
+ *                  per stripe; GF(2^16): see m16_ps); 2 device plans past 16 distinct patterns for GF(256)
+ *                  codes and past one pattern for GF(2^16) codes (default)
+ *   "syn_route"    GF(256) device-plan decodes (S a multiple of 2 KiB): 1 syndromes of every slot on the
+ *                  bit-plane XOR kernel, then a per-stripe t_info x t solve (default); 0 survivor matrices
+ *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
+ *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
+ *                  0 one plan per pattern rebuilt on the stream
+ *   "m16_ps_chunk" / "m16_ps_rec_mib"  stripes / record MiB per chunk of that path (0 / 1024 defaults)
+ *   "m16_mode"     GF(2^16) dense kernels: 0 hand-scheduled gpr-index kernel for > 32 outputs (default),
+ *                  2 the compiled kernel
+ *   "m16_plans"    GF(2^16) dense matrices: 0 built on the host, 1 on the device, 2 on the device from 64K
+ *                  coefficients (default); rebuilds the encode plan
+ *   "m16_route"    GF(2^16) syndrome route (cyclotomic k_cs16 + second stage): 1 matrices with >= 64
+ *                  inputs (default), 0 never, 2 every matrix
+ *   "m16_route_min_bytes"  bytes a dense decode plan with t > 64 moves before it switches to the route
+ *                  (default 1 GiB; 0 = at once)
+ *   "m16_reenc"    GF(2^16) decodes without repair erasures and t >= 0.9 r by re-encoding: 1 (default), 0
+ *   "m16_cs_col"   route kernels' block layout: 256 (default) or 1024 bytes per column unit
+ * The timing ablations (m8_mode 10-13, 15-17, 19; m16_mode 1; "stamp_buffer") exist only in the
+ * diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
@@ -127,6 +142,9 @@ int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
  * (out = m2 * syndromes). info = {D, ngroups, ntiles, fin_stride, R}; arrays may be NULL. Host only. */
 int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                    uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2);
+/* Symbol data from symbol_create of >= 16 KiB (page-aligned, registrable): 1 once a per-call use has
+ * page-locked and mapped it (hipHostRegister, until symbol_destroy), 0 before; -1 for any other pointer. */
+int rsg_symbol_registered(const void* data);
 /* The k_bs16 second stage of the GF(2^16) route for the encode (is_erased NULL) or decode matrix, when it
  * applies (encode: the repair cosets; decode: an erased set closed under x -> x^(2^d), d < 16): records
  * [ntiles][ngroups + 2][4][64] bytes, finish lists [ntiles][fin_stride] (local coset | rotation << 4 |

@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -2600,6 +2601,105 @@ const uint8_t* arena_run(symbol_t* const* syms, size_t cnt, size_t S, size_t* pi
     return b;
 }
 
+// Caller-owned symbols outside the arenas (symbol_create; seq_create with RS_AMD_PINNED_SEQ=0): data of
+// kRegMinBytes or more is allocated page-aligned in whole pages, so no two symbols share a page, and
+// recorded here. A per-call use page-locks and maps it once (hipHostRegister, within the pinned cap,
+// cached until symbol_destroy); from then on a call moves such symbols with one gather kernel and one
+// scatter kernel across PCIe (launch_gather_ptrs / launch_scatter_ptrs) instead of host copies through
+// staging. Only buffers this library allocated are registered: it alone knows when they are freed.
+constexpr size_t kRegMinBytes = size_t(16) << 10;
+constexpr size_t kPage = 4096;
+struct SymEnt {
+    size_t bytes;         // whole pages
+    uint8_t* dev;         // device-visible address once registered
+};
+struct SymRegistry {
+    std::mutex mu;
+    std::unordered_map<uintptr_t, SymEnt> m;
+};
+SymRegistry& symreg() {
+    static SymRegistry* r = new SymRegistry;  // never destroyed: symbols may outlive static destructors
+    return *r;
+}
+
+bool sym_register(uint8_t* p, SymEnt& e);
+
+uint8_t* sym_alloc(size_t S) {
+    if (S < kRegMinBytes) return nullptr;
+    const size_t bytes = (S + kPage - 1) / kPage * kPage;
+    void* p = std::aligned_alloc(kPage, bytes);
+    if (!p) return nullptr;
+    std::memset(p, 0, bytes);
+    SymRegistry& R = symreg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    SymEnt& e = R.m[uintptr_t(p)] = SymEnt{bytes, nullptr};
+    // page-lock it now, as seq_create's arenas are (the per-call path then never pays for it); a failure
+    // (no GPU, the pinned cap) leaves it to the first use
+    (void)sym_register(static_cast<uint8_t*>(p), e);
+    return static_cast<uint8_t*>(p);
+}
+
+// page-locks and maps one registry entry (its mutex held); false when the cap or the runtime refuses
+bool sym_register(uint8_t* p, SymEnt& e) {
+    if (e.dev) return true;
+    ArenaRegistry& A = arenas();
+    {
+        std::lock_guard<std::mutex> la(A.mu);
+        if (A.no_pinning || A.pinned + e.bytes > pinned_cap()) return false;
+        A.pinned += e.bytes;
+    }
+    void* dv = nullptr;
+    if (hipHostRegister(p, e.bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess ||
+        hipHostGetDevicePointer(&dv, p, 0) != hipSuccess) {
+        (void)hipHostUnregister(p);
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> la(A.mu);
+        A.pinned -= e.bytes;
+        return false;
+    }
+    e.dev = static_cast<uint8_t*>(dv);
+    return true;
+}
+
+// true (and p freed, unregistered first) when p came from sym_alloc
+bool sym_release(uint8_t* p) {
+    SymRegistry& R = symreg();
+    size_t pinned = 0;
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        auto it = R.m.find(uintptr_t(p));
+        if (it == R.m.end()) return false;
+        if (it->second.dev) {
+            (void)hipHostUnregister(p);
+            (void)hipGetLastError();
+            pinned = it->second.bytes;
+        }
+        R.m.erase(it);
+    }
+    if (pinned) {
+        ArenaRegistry& A = arenas();
+        std::lock_guard<std::mutex> lk(A.mu);
+        A.pinned -= pinned;
+    }
+    std::free(p);
+    return true;
+}
+
+// device-visible addresses of cnt symbols of at least S bytes, all from sym_alloc, registering the ones
+// not yet registered; false (nothing to do for the caller's fast path) when any is not eligible
+bool sym_devptrs(symbol_t* const* syms, size_t cnt, size_t S, uint64_t* out) {
+    SymRegistry& R = symreg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    for (size_t i = 0; i < cnt; ++i) {
+        if (!syms[i]) return false;
+        auto it = R.m.find(uintptr_t(syms[i]->data));
+        if (it == R.m.end() || it->second.bytes < S) return false;
+        if (!it->second.dev && !sym_register(syms[i]->data, it->second)) return false;
+        out[i] = uint64_t(reinterpret_cast<uintptr_t>(it->second.dev));
+    }
+    return true;
+}
+
 struct Impl {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2622,11 +2722,29 @@ struct Impl {
     int32_t* h_rows = nullptr;  // pinned / device row list of the decode's packed copy-back
     int32_t* d_rows = nullptr;
     size_t rows_cap = 0;
+    // registered caller symbols: [n] device-visible symbol addresses, [n] gathered rows, [n] scattered
+    // rows (pinned; uploaded by one copy per call)
+    uint8_t* h_ptrs = nullptr;
+    uint8_t* d_ptrs = nullptr;
+    size_t ptrs_cap = 0;
+    int reserve_ptrs(size_t n) {
+        if (n <= ptrs_cap) return 0;
+        if (h_ptrs) (void)hipHostFree(h_ptrs);
+        if (d_ptrs) (void)hipFree(d_ptrs);
+        h_ptrs = d_ptrs = nullptr;
+        ptrs_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&h_ptrs), n * 16, hipHostMallocDefault) != hipSuccess) return 1;
+        if (hipMalloc(reinterpret_cast<void**>(&d_ptrs), n * 16) != hipSuccess) return 1;
+        ptrs_cap = n;
+        return 0;
+    }
     ~Impl() {
         (void)hipSetDevice(device);
         codecs.clear();
         if (h_rows) (void)hipHostFree(h_rows);
         if (d_rows) (void)hipFree(d_rows);
+        if (h_ptrs) (void)hipHostFree(h_ptrs);
+        if (d_ptrs) (void)hipFree(d_ptrs);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : ev_in)
@@ -2755,6 +2873,32 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
         HIP_TRY(hipEventSynchronize(im.ev[0]));
         return 0;
     }
+    // registered caller symbols (sym_alloc): one gather kernel, the encode, one scatter kernel
+    if (!ib && !rb && S % 16 == 0 && S >= kRegMinBytes) {
+        if (im.reserve_ptrs(n)) return 1;
+        uint64_t* hp = reinterpret_cast<uint64_t*>(im.h_ptrs);
+        if (sym_devptrs(inf->symbols, k, S, hp) && sym_devptrs(rep->symbols, r, S, hp + k)) {
+            if (im.reserve(n * P)) return 1;
+            uint8_t* d = im.d_buf;
+            const uint64_t* dp = reinterpret_cast<const uint64_t*>(im.d_ptrs);
+            HIP_TRY(hipMemcpyAsync(im.d_ptrs, im.h_ptrs, n * 8, hipMemcpyHostToDevice, im.in_stream));
+            // column chunks: the gather of chunk c + 1 (in_stream) reads across PCIe while chunk c is encoded
+            // and its repair columns are written back (stream)
+            const size_t Wr = chunk_width(S, kMaxChunks), nr = (S + Wr - 1) / Wr;
+            for (size_t ch = 0; ch < nr; ++ch) {
+                const size_t off = ch * Wr, w = std::min(Wr, S - off);
+                HIP_TRY(launch_gather_ptrs(d, int64_t(P), dp, nullptr, int64_t(k), int64_t(off), int64_t(w), im.in_stream));
+                HIP_TRY(hipEventRecord(im.ev_in[ch], im.in_stream));
+                HIP_TRY(hipStreamWaitEvent(im.stream, im.ev_in[ch], 0));
+                if ((rc = rsg_encode(c, d + off, n * P, P, d + size_t(k) * P + off, n * P, P, 1, w, im.stream))) return rc;
+                HIP_TRY(launch_scatter_ptrs(dp + k, d + size_t(k) * P, int64_t(P), nullptr, int64_t(r), int64_t(off),
+                                            int64_t(w), im.stream));
+            }
+            HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+            HIP_TRY(hipEventSynchronize(im.ev[0]));
+            return 0;
+        }
+    }
     if (im.reserve(n * P)) return 1;
     uint8_t *h = im.h_buf, *d = im.d_buf;
     // chunk c: gather k columns -> H2D (2D) -> encode -> D2H (2D); scatter of c - 1 overlaps it
@@ -2835,6 +2979,40 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
         HIP_TRY(hipEventRecord(im.ev[0], im.stream));
         HIP_TRY(hipEventSynchronize(im.ev[0]));
         return 0;
+    }
+    // registered caller symbols (sym_alloc): surviving rows gathered by one kernel, the decode, the restored
+    // rows scattered by one kernel
+    if (!sb && S % 16 == 0 && S >= kRegMinBytes) {
+        if (im.reserve_ptrs(n)) return 1;
+        uint64_t* hp = reinterpret_cast<uint64_t*>(im.h_ptrs);
+        if (sym_devptrs(rcv->symbols, n, S, hp)) {
+            const size_t P = pad16(S);
+            if (im.reserve(n * P)) return 1;
+            int32_t* hk = reinterpret_cast<int32_t*>(im.h_ptrs + n * 8);
+            int32_t* hl = hk + keep.size();
+            std::memcpy(hk, keep.data(), keep.size() * 4);
+            std::memcpy(hl, lost.data(), lost.size() * 4);
+            uint8_t* d = im.d_buf;
+            const uint64_t* dp = reinterpret_cast<const uint64_t*>(im.d_ptrs);
+            const int32_t* dk = reinterpret_cast<const int32_t*>(im.d_ptrs + n * 8);
+            HIP_TRY(hipMemcpyAsync(im.d_ptrs, im.h_ptrs, n * 8 + (keep.size() + lost.size()) * 4, hipMemcpyHostToDevice,
+                                   im.in_stream));
+            // column chunks as the encode's (a pattern still on its generic kernel decodes in one piece)
+            const size_t Wr = pending ? S : chunk_width(S, kMaxChunks), nr = (S + Wr - 1) / Wr;
+            for (size_t ch = 0; ch < nr; ++ch) {
+                const size_t off = ch * Wr, w = std::min(Wr, S - off);
+                HIP_TRY(launch_gather_ptrs(d, int64_t(P), dp, dk, int64_t(keep.size()), int64_t(off), int64_t(w),
+                                           im.in_stream));
+                HIP_TRY(hipEventRecord(im.ev_in[ch], im.in_stream));
+                HIP_TRY(hipStreamWaitEvent(im.stream, im.ev_in[ch], 0));
+                if ((rc = rsg_decode(c, d + off, n * P, P, 1, w, is_erased, t, im.stream))) return rc;
+                HIP_TRY(launch_scatter_ptrs(dp, d, int64_t(P), dk + keep.size(), int64_t(lost.size()), int64_t(off),
+                                            int64_t(w), im.stream));
+            }
+            HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+            HIP_TRY(hipEventSynchronize(im.ev[0]));
+            return 0;
+        }
     }
     // a stripe in a page-locked arena (seq_create) is copied in place: all n rows in by one 2D DMA
     // (erased rows ride along unread), restored rows out by DMA of their span or, when scattered,
@@ -2921,7 +3099,8 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
 extern "C" symbol_t* symbol_create(size_t symbol_size) {
     symbol_t* s = static_cast<symbol_t*>(std::calloc(1, sizeof(symbol_t)));
     if (!s) return nullptr;
-    s->data = static_cast<uint8_t*>(std::calloc(symbol_size ? symbol_size : 1, 1));
+    s->data = sym_alloc(symbol_size);  // whole zeroed pages, registrable (>= kRegMinBytes), or:
+    if (!s->data) s->data = static_cast<uint8_t*>(std::calloc(symbol_size ? symbol_size : 1, 1));
     if (!s->data) {
         std::free(s);
         return nullptr;
@@ -2931,7 +3110,7 @@ extern "C" symbol_t* symbol_create(size_t symbol_size) {
 
 extern "C" void symbol_destroy(symbol_t* s) {
     if (!s) return;
-    if (!arena_release(s->data)) std::free(s->data);
+    if (!arena_release(s->data) && !sym_release(s->data)) std::free(s->data);
     std::free(s);
 }
 
@@ -3418,6 +3597,13 @@ extern "C" int fft_partial_transform_cycl(GF_t* gf, const symbol_seq_t* f, const
 // Host-only view of the GF(2^16) syndrome route of the encode (is_erased == NULL) or decode matrix: the
 // k_cs16 plan (groups, records, finish lists) and the second-stage matrix M2 [R][D]. info = {D, ngroups,
 // ntiles, fin_stride, R}; array arguments may be NULL (query the sizes first). No GPU is used.
+extern "C" int rsg_symbol_registered(const void* data) {
+    SymRegistry& R = symreg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.m.find(uintptr_t(data));
+    return it == R.m.end() ? -1 : (it->second.dev ? 1 : 0);
+}
+
 extern "C" int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
                              int32_t* fin, int32_t* fin_off) {
     if (uint32_t(k) + r > kN || (is_erased && t > r)) return RS_ERR_INVALID;

@@ -1696,6 +1696,46 @@ hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, i
     return hipGetLastError();
 }
 
+// drop-in path over registered caller symbols: whole rows between per-symbol host addresses (mapped,
+// read / written across PCIe) and the device staging stripe
+__global__ void __launch_bounds__(256) k_gather_ptrs(uint8_t* dst, int64_t dpitch, const uint64_t* ptrs,
+                                                     const int32_t* rows, int64_t off, int64_t units) {
+    const int64_t u = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (u >= units) return;
+    const int64_t i = rows ? rows[blockIdx.y] : int64_t(blockIdx.y);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<u32x4*>(dst + i * dpitch + off)[u] = reinterpret_cast<const u32x4*>(uintptr_t(ptrs[i]) + off)[u];
+}
+
+__global__ void __launch_bounds__(256) k_scatter_ptrs(const uint64_t* ptrs, const uint8_t* src, int64_t spitch,
+                                                      const int32_t* rows, int64_t off, int64_t units) {
+    const int64_t u = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (u >= units) return;
+    const int64_t i = rows ? rows[blockIdx.y] : int64_t(blockIdx.y);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<u32x4*>(uintptr_t(ptrs[i]) + off)[u] = reinterpret_cast<const u32x4*>(src + i * spitch + off)[u];
+}
+
+hipError_t launch_gather_ptrs(uint8_t* dst, int64_t dpitch, const uint64_t* ptrs, const int32_t* rows, int64_t nrows,
+                              int64_t off, int64_t width, hipStream_t st) {
+    const int64_t units = width / 16;
+    if (nrows <= 0 || units <= 0) return hipSuccess;
+    if ((width & 15) || (off & 15) || (dpitch & 15) || (uintptr_t(dst) & 15) || nrows > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gather_ptrs, dim3(unsigned((units + 255) / 256), unsigned(nrows)), dim3(256), 0, st, dst, dpitch,
+                       ptrs, rows, off, units);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_ptrs(const uint64_t* ptrs, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                               int64_t nrows, int64_t off, int64_t width, hipStream_t st) {
+    const int64_t units = width / 16;
+    if (nrows <= 0 || units <= 0) return hipSuccess;
+    if ((width & 15) || (off & 15) || (spitch & 15) || (uintptr_t(src) & 15) || nrows > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scatter_ptrs, dim3(unsigned((units + 255) / 256), unsigned(nrows)), dim3(256), 0, st, ptrs, src,
+                       spitch, rows, off, units);
+    return hipGetLastError();
+}
+
 hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
     if (n_sel <= 0) return hipSuccess;
     if (a.n > 256) return hipErrorInvalidValue;

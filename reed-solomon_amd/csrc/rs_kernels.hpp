@@ -132,6 +132,13 @@ hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, 
 // rows == nullptr: rows 0 .. nrows - 1
 hipError_t launch_put_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,
                            int64_t nrows, int64_t width, hipStream_t st);
+// registered caller symbols (rs_api.cpp, drop-in path): bytes [off, off + width) of dst row i = those of
+// the symbol at device-visible address ptrs[i], for the rows i in rows[0 .. nrows) (rows null: 0 .. nrows
+// - 1), and back (scatter). 16-byte units: addresses, pitch, offset and width multiples of 16.
+hipError_t launch_gather_ptrs(uint8_t* dst, int64_t dpitch, const uint64_t* ptrs, const int32_t* rows, int64_t nrows,
+                              int64_t off, int64_t width, hipStream_t st);
+hipError_t launch_scatter_ptrs(const uint64_t* ptrs, const uint8_t* src, int64_t spitch, const int32_t* rows,
+                               int64_t nrows, int64_t off, int64_t width, hipStream_t st);
 // row p of stripe s of dst ^= the same row of src (p < nrows, S bytes, 4-byte aligned; the re-encode decode)
 hipError_t launch_xor_rows(uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, const uint8_t* src, int64_t src_stripe,
                            int64_t src_sym, int64_t nrows, int64_t S, int64_t n_stripes, hipStream_t st);

@@ -94,6 +94,7 @@ _sig("rsg_jit_precompile", ctypes.c_int, u16, u16, P, u16)
 _sig("rsg_gamma_tables", ctypes.c_int, P, P, P)
 _sig("rsg_route_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P, P)
 _sig("rsg_bs16_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P)
+_sig("rsg_symbol_registered", ctypes.c_int, P)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("gf_create", P)
 _sig("gf_destroy", None, P)
@@ -165,6 +166,11 @@ def route_dump(k, r, is_erased=None):
     if rc:
         raise RSError(rc, "rsg_route_dump")
     return dict(D=D, groups=groups, rec=rec, fin=fin, fin_off=fin_off, m2=m2)
+
+
+def symbol_registered(arr):
+    """1 / 0: a symbol_create buffer (>= 16 KiB) is / is not yet page-locked for the per-call path; -1: other."""
+    return int(_lib.rsg_symbol_registered(ctypes.c_void_p(arr.ctypes.data)))
 
 
 def bs16_dump(k, r, is_erased=None):

@@ -863,15 +863,17 @@ def test_drop_in_m16_large_symbols():
                                            (128, 32, 65536, "random"), (300, 64, 8192 + 6, "random"),
                                            (64, 16, 16384 + 2, "bench"), (4, 2, 256, "random"),
                                            (10, 4, 4096, "bench"), (200, 55, 66, "random"),
-                                           (300, 64, 64, "random"), (300, 70, 1024, "random")])
+                                           (300, 64, 64, "random"), (300, 70, 1024, "random"),
+                                           (300, 64, 16384, "random"), (128, 32, 32768, "span")])
 def test_drop_in_pinned_seq(k, r, S, pattern):
     """seq_create places sequences in page-locked memory (own block from 1 MiB, slab share below) and
     the per-call API works on them in place: zero-copy launches (specialised XOR kernels; any kernel on
     stripes up to 1 MiB), else 2D DMA in and restored rows out by DMA of their span or k_put_rows.
     Encode and restore bit-exact vs the oracle for scattered (bench, random) and contiguous (span)
     erasures, GF(16) / GF(256) / GF(2^16) codes, symbol sizes that are not multiples of 16 (padded
-    pitch); the same calls on pageable symbols (RS_AMD_PINNED_SEQ=0 -> calloc per symbol) give the same
-    bytes."""
+    pitch); the same calls on separately allocated symbols (RS_AMD_PINNED_SEQ=0 -> symbol_create per
+    symbol: from 16 KiB page-aligned buffers page-locked at creation, moved by gather / scatter kernels
+    when S is a multiple of 16; else calloc and host copies) give the same bytes."""
     import os
     rng = np.random.default_rng(k * 7 + S)
     data = rng.integers(0, 256, (k, S), dtype=np.uint8)
@@ -899,6 +901,8 @@ def test_drop_in_pinned_seq(k, r, S, pattern):
             assert pitch == _pad(S), "seq_create did not place the sequence in one arena"
         for i in range(k):
             q.symbols[i][:] = data[i]
+        own = S >= 16384 and flag == "0"  # symbol_create buffers from 16 KiB: page-aligned, page-locked
+        assert all(rs_amd.symbol_registered(x) == (1 if own else -1) for x in q.symbols)
         for call in range(4):  # decode calls 3+ of a GF(256) pattern run the specialised plan, 4+ zero-copy
             assert rs.generate_repair_symbols(q, r) == 0
             got = np.stack(q.symbols)
