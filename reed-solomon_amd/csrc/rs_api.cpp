@@ -2700,6 +2700,18 @@ bool sym_devptrs(symbol_t* const* syms, size_t cnt, size_t S, uint64_t* out) {
     return true;
 }
 
+// cnt device addresses at one stride >= S (16-byte aligned) with 32-bit kernel offsets; *pitch = it
+bool strided_run(const uint64_t* p, size_t cnt, size_t S, size_t* pitch) {
+    if (!cnt || (p[0] & 15)) return false;
+    const uint64_t d = cnt > 1 ? p[1] - p[0] : pad16(S);
+    if (cnt > 1 && (p[1] <= p[0] || d < S || (d & 15))) return false;
+    for (size_t i = 2; i < cnt; ++i)
+        if (p[i] != p[0] + i * d) return false;
+    if ((cnt - 1) * d + S >= (uint64_t(1) << 31)) return false;
+    *pitch = size_t(d);
+    return true;
+}
+
 struct Impl {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2719,6 +2731,7 @@ struct Impl {
     int arena_chunks = 2;
     bool arena_put = true;
     bool arena_zc = true;  // RS_AMD_DROPIN_ZC=0: no zero-copy launches (see streams_once)
+    int reg_chunks = 1;    // registered caller symbols: column chunks per call (RS_AMD_REG_CHUNKS, 1..kMaxChunks)
     int32_t* h_rows = nullptr;  // pinned / device row list of the decode's packed copy-back
     int32_t* d_rows = nullptr;
     size_t rows_cap = 0;
@@ -2821,6 +2834,7 @@ extern "C" RS_t* rs_create(void) {
     if (const char* e = std::getenv("RS_AMD_DROPIN_CHUNKS")) impl->arena_chunks = std::clamp(std::atoi(e), 1, kMaxChunks);
     if (const char* e = std::getenv("RS_AMD_DROPIN_PUT")) impl->arena_put = e[0] == '1';
     if (const char* e = std::getenv("RS_AMD_DROPIN_ZC")) impl->arena_zc = e[0] != '0';
+    if (const char* e = std::getenv("RS_AMD_REG_CHUNKS")) impl->reg_chunks = std::clamp(std::atoi(e), 1, kMaxChunks);
     bool ev_ok = true;
     for (hipEvent_t& e : impl->ev) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (hipEvent_t& e : impl->ev_in) ev_ok = ev_ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
@@ -2878,13 +2892,26 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
         if (im.reserve_ptrs(n)) return 1;
         uint64_t* hp = reinterpret_cast<uint64_t*>(im.h_ptrs);
         if (sym_devptrs(inf->symbols, k, S, hp) && sym_devptrs(rep->symbols, r, S, hp + k)) {
+            size_t ip2 = 0, rp2 = 0;
+            if (im.arena_zc && streams_once(*c->enc, S) && strided_run(hp, k, S, &ip2) && strided_run(hp + k, r, S, &rp2)) {
+                // the symbols sit at one stride in the device's view (consecutive symbol_create calls usually
+                // do): the encode kernel streams them across PCIe itself, as for arena stripes
+                uint8_t* di = reinterpret_cast<uint8_t*>(uintptr_t(hp[0]));
+                uint8_t* dr = reinterpret_cast<uint8_t*>(uintptr_t(hp[k]));
+                if ((rc = rsg_encode(c, di, int64_t(k * ip2), int64_t(ip2), dr, int64_t(r * rp2), int64_t(rp2), 1,
+                                     int64_t(S), im.stream)))
+                    return rc;
+                HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+                HIP_TRY(hipEventSynchronize(im.ev[0]));
+                return 0;
+            }
             if (im.reserve(n * P)) return 1;
             uint8_t* d = im.d_buf;
             const uint64_t* dp = reinterpret_cast<const uint64_t*>(im.d_ptrs);
             HIP_TRY(hipMemcpyAsync(im.d_ptrs, im.h_ptrs, n * 8, hipMemcpyHostToDevice, im.in_stream));
             // column chunks: the gather of chunk c + 1 (in_stream) reads across PCIe while chunk c is encoded
             // and its repair columns are written back (stream)
-            const size_t Wr = chunk_width(S, kMaxChunks), nr = (S + Wr - 1) / Wr;
+            const size_t Wr = chunk_width(S, im.reg_chunks), nr = (S + Wr - 1) / Wr;
             for (size_t ch = 0; ch < nr; ++ch) {
                 const size_t off = ch * Wr, w = std::min(Wr, S - off);
                 HIP_TRY(launch_gather_ptrs(d, int64_t(P), dp, nullptr, int64_t(k), int64_t(off), int64_t(w), im.in_stream));
@@ -2986,6 +3013,14 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
         if (im.reserve_ptrs(n)) return 1;
         uint64_t* hp = reinterpret_cast<uint64_t*>(im.h_ptrs);
         if (sym_devptrs(rcv->symbols, n, S, hp)) {
+            size_t sp2 = 0;
+            if (im.arena_zc && streams_once(*dplan, S) && strided_run(hp, n, S, &sp2)) {  // in place, one launch
+                uint8_t* ds = reinterpret_cast<uint8_t*>(uintptr_t(hp[0]));
+                if ((rc = rsg_decode(c, ds, n * sp2, sp2, 1, S, is_erased, t, im.stream))) return rc;
+                HIP_TRY(hipEventRecord(im.ev[0], im.stream));
+                HIP_TRY(hipEventSynchronize(im.ev[0]));
+                return 0;
+            }
             const size_t P = pad16(S);
             if (im.reserve(n * P)) return 1;
             int32_t* hk = reinterpret_cast<int32_t*>(im.h_ptrs + n * 8);
@@ -2998,7 +3033,7 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
             HIP_TRY(hipMemcpyAsync(im.d_ptrs, im.h_ptrs, n * 8 + (keep.size() + lost.size()) * 4, hipMemcpyHostToDevice,
                                    im.in_stream));
             // column chunks as the encode's (a pattern still on its generic kernel decodes in one piece)
-            const size_t Wr = pending ? S : chunk_width(S, kMaxChunks), nr = (S + Wr - 1) / Wr;
+            const size_t Wr = pending ? S : chunk_width(S, im.reg_chunks), nr = (S + Wr - 1) / Wr;
             for (size_t ch = 0; ch < nr; ++ch) {
                 const size_t off = ch * Wr, w = std::min(Wr, S - off);
                 HIP_TRY(launch_gather_ptrs(d, int64_t(P), dp, dk, int64_t(keep.size()), int64_t(off), int64_t(w),
