@@ -2391,7 +2391,7 @@ extern "C" int rsg_xj_source(uint16_t k, uint16_t r, const bool* is_erased, uint
     std::vector<int32_t> in, outs;
     codec_matrix(pos, k, r, is_erased, M, in, outs);
     if (!xj_supported(8, int(in.size()), int(outs.size()))) return RS_ERR_INVALID;
-    const std::string src = xj_source(M, int(in.size()), int(outs.size()), in, outs);
+    const std::string src = xj_source(M, int(in.size()), int(outs.size()), in, outs, true);
     if (len) *len = src.size();
     if (buf && cap) {
         const size_t n = std::min(cap - 1, src.size());
@@ -2402,7 +2402,7 @@ extern "C" int rsg_xj_source(uint16_t k, uint16_t r, const bool* is_erased, uint
 }
 
 extern "C" int rsg_xj_basis(int32_t* pivots, uint16_t* beta_y, uint8_t* bits256) {
-    const XjBasis& B = xj_basis(xj_horner());
+    const XjBasis& B = xj_basis(xj_horner(true));  // inspection API: honours RS_XJ_HORNER like rsg_xj_source
     if (pivots)
         for (int t = 0; t < 8; ++t) pivots[t] = B.pivots[t];
     if (beta_y)

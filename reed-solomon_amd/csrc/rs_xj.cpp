@@ -169,8 +169,15 @@ struct XjConfig {
                        // 3: 1 over each early load burst
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
-    explicit XjConfig(int R = 0) {
-        auto env = [](const char* n, int& v) {
+    // env: read the RS_XJ_* generation knobs (experiments, the emulator tests through rsg_xj_source, the
+    // diagnostic build). The kernels the release library launches are generated with the defaults
+    // whatever the environment says, so no deployment's environment changes the shipped kernel.
+    explicit XjConfig(int R = 0, bool env_knobs = false) {
+#ifdef RS_AMD_DIAG
+        env_knobs = true;
+#endif
+        auto env = [env_knobs](const char* n, int& v) {
+            if (!env_knobs) return;
             if (const char* e = std::getenv(n)) v = std::atoi(e);
         };
         env("RS_XJ_OPR", opr);
@@ -813,8 +820,8 @@ static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::v
 }
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots) {
-    XjConfig C(R);
+                      const std::vector<int32_t>& out_slots, bool env_knobs) {
+    XjConfig C(R, env_knobs);
     C.set_k(K);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
@@ -897,7 +904,7 @@ int xj_roles(int R) {
     const int opr = XjConfig(R).opr;
     return (R + opr - 1) / opr;
 }
-int xj_horner() { return XjConfig().horner; }
+int xj_horner(bool env_knobs) { return XjConfig(0, env_knobs).horner; }
 int xj_fin() { return XjConfig().lfin; }
 int xj_max_roles(int R) {
     // all role waves of a column are one workgroup, so they must fit one CU at the layout's VGPR

@@ -74,7 +74,7 @@ struct XjBasis {
     uint16_t inv_row_[16];  // row j of the inverse of [z^0 .. z^15] over GF(2)
 };
 const XjBasis& xj_basis(int horner);
-int xj_horner();  // generation setting (RS_XJ_HORNER, default 0)
+int xj_horner(bool env_knobs = false);  // generation setting (RS_XJ_HORNER, default 0)
 
 bool xj_supported(int m, int K, int R);
 int xj_outputs_per_role();  // generation setting (RS_XJ_OPR, default 16)
@@ -83,8 +83,9 @@ int xj_max_roles(int R);     // role waves that fit one CU at the layout's VGPR 
 int xj_fin();                // generation setting (RS_XJ_FIN, default 0)
 int xj_pairs(int R);         // columns per workgroup (1 unless the LDS-table finish is on)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
+// env_knobs: honour the RS_XJ_* generation knobs (inspection / emulator tests; the launched kernels never do)
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots);
+                      const std::vector<int32_t>& out_slots, bool env_knobs = false);
 int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
              const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out);
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,

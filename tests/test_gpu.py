@@ -949,9 +949,10 @@ def test_host_memory_batches(k, r, S, n, pinned):
 
 
 def test_release_build_ignores_diagnostic_knobs():
-    """The product library rejects the ablation options (RS_ERR_INVALID) and ignores the ablation
-    environment variables: with RS_XJ_ABLATE / RS_XJ_ALIAS set, a fresh process still encodes and
-    decodes bit-exactly through the XOR kernel."""
+    """The product library rejects the ablation options (RS_ERR_INVALID) and ignores every RS_XJ_*
+    environment variable when it generates the kernels it launches: with ablation and generation knobs
+    set, a fresh process still encodes and decodes bit-exactly through the same XOR kernel (same content
+    hash in its name) as without them."""
     codec = rs_amd.Codec(128, 32)
     for name, value in [("m8_mode", v) for v in (10, 11, 12, 13, 15, 16, 17, 19)] + [("m16_mode", 1), ("stamp_buffer", 1)]:
         with pytest.raises(rs_amd.RSError):
@@ -982,9 +983,16 @@ for _ in range(2):
 print("ok", c.last_kernel)
 """
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, RS_XJ_ABLATE="1", RS_XJ_ALIAS="1", PYTHONPATH=os.path.dirname(rs_amd.__file__))
+    base = dict(os.environ, PYTHONPATH=os.path.dirname(rs_amd.__file__))
+    for k in [v for v in base if v.startswith("RS_XJ_")]:
+        base.pop(k)
+    plain = subprocess.run([sys.executable, "-c", code, here], env=base, capture_output=True, text=True, timeout=300)
+    assert plain.returncode == 0 and plain.stdout.startswith("ok rs_xj"), plain.stdout + plain.stderr
+    # neither the ablations nor the generation knobs change the shipped kernel (same content hash)
+    env = dict(base, RS_XJ_ABLATE="1", RS_XJ_ALIAS="1", RS_XJ_OPR="8", RS_XJ_EARLY="0", RS_XJ_HORNER="1")
     p = subprocess.run([sys.executable, "-c", code, here], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and p.stdout.startswith("ok rs_xj"), p.stdout + p.stderr
+    assert p.stdout.split()[-1] == plain.stdout.split()[-1], (p.stdout, plain.stdout)
 
 
 @pytest.mark.parametrize("name", EXTRA_CASES)
