@@ -142,8 +142,9 @@ int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
  * (out = m2 * syndromes). info = {D, ngroups, ntiles, fin_stride, R}; arrays may be NULL. Host only. */
 int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                    uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2);
-/* Symbol data from symbol_create of >= 16 KiB (page-aligned, registrable): 1 once a per-call use has
- * page-locked and mapped it (hipHostRegister, until symbol_destroy), 0 before; -1 for any other pointer. */
+/* Symbol data from symbol_create of >= 16 KiB (page-aligned whole pages): 1 when symbol_create page-locked
+ * and mapped it (hipHostRegister, until symbol_destroy), 0 when that registration was refused (the symbol
+ * then goes by the staging path); -1 for any other pointer. */
 int rsg_symbol_registered(const void* data);
 /* The k_bs16 second stage of the GF(2^16) route for the encode (is_erased NULL) or decode matrix, when it
  * applies (encode: the repair cosets; decode: an erased set closed under x -> x^(2^d), d < 16): records

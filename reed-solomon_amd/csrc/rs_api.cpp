@@ -2648,11 +2648,19 @@ bool sym_register(uint8_t* p, SymEnt& e) {
         if (A.no_pinning || A.pinned + e.bytes > pinned_cap()) return false;
         A.pinned += e.bytes;
     }
+    // never touch a range the runtime already knows (another registration, its own pinned buffers): a
+    // failed registration must not be followed by an unregister, which would remove the owner's mapping
+    hipPointerAttribute_t attr{};
+    const bool known = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type != hipMemoryTypeUnregistered;
+    (void)hipGetLastError();
+    bool ok = !known && hipHostRegister(p, e.bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess;
     void* dv = nullptr;
-    if (hipHostRegister(p, e.bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess ||
-        hipHostGetDevicePointer(&dv, p, 0) != hipSuccess) {
-        (void)hipHostUnregister(p);
-        (void)hipGetLastError();
+    if (ok && hipHostGetDevicePointer(&dv, p, 0) != hipSuccess) {
+        (void)hipHostUnregister(p);  // ours: registered just above
+        ok = false;
+    }
+    (void)hipGetLastError();
+    if (!ok) {
         std::lock_guard<std::mutex> la(A.mu);
         A.pinned -= e.bytes;
         return false;

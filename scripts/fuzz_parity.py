@@ -3,8 +3,10 @@ symbol sizes with and without tail columns, stripe counts and erasure patterns, 
 path: matrix-specialised XOR kernels (jit=1), generic GF(256) kernels (jit=0), GF(2^16) codes
 (hand-scheduled kernel, split-K on small grids, device-built plans), and rsg_decode_batch with a
 pattern per stripe (device-built plans; for GF(2^16) codes, "batch16", one plan rebuilt on the stream
-per pattern), the GF(2^16) syndrome route ("route": k_cs16 + k_bs16 / second stage) and the per-call
-drop-in API on seq_create arenas ("dropin"). Prints one JSON line per case and a summary.
+per pattern), the GF(2^16) syndrome route ("route": k_cs16 + k_bs16 / second stage), the per-call
+drop-in API on seq_create arenas ("dropin"); round 3: the per-stripe GF(2^16) route ("ps16"), decode
+patterns closed under a Frobenius power ("orbit": the k_bs16 stage over row orbits) and the per-call API
+on registered symbol_create buffers ("dropin_reg"). Prints one JSON line per case and a summary.
 usage: fuzz_parity.py [seed] [seconds] [family,family,...]"""
 import json
 import os
@@ -20,8 +22,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import rs_amd  # noqa: E402
 from _util import oracle_decode, oracle_encode  # noqa: E402
 
-rng = np.random.default_rng(int(sys.argv[1]) if len(sys.argv) > 1 else 2024)
-budget = float(sys.argv[2]) if len(sys.argv) > 2 else 240.0
+rng = np.random.default_rng(int(sys.argv[1]) if len(sys.argv) > 1 and __name__ == "__main__" else 2024)
+budget = float(sys.argv[2]) if len(sys.argv) > 2 and __name__ == "__main__" else 240.0
 t_end = time.time() + budget
 counts = {}
 fails = 0
@@ -66,9 +68,146 @@ def one_dropin():
     return dict(family="dropin", k=k, r=r, S=S, stripes=1, t=int(er.sum()), arena=pitch == (S + 15) // 16 * 16, ok=ok)
 
 
+def one_dropin_reg():
+    """Per-call API on separately allocated symbols (RS_AMD_PINNED_SEQ=0: symbol_create per symbol, from
+    16 KiB page-aligned and page-locked at creation): zero-copy kernels when the symbols sit at one stride,
+    else gather / scatter kernels over the symbol pointers; GF(256) and GF(2^16) codes."""
+    if rng.integers(0, 2):
+        k = int(rng.integers(20, 200))
+        r = int(rng.integers(1, min(255 - k, 64) + 1))
+    else:
+        k = int(rng.integers(200, 600))
+        r = int(rng.integers(max(1, 256 - k), 150))
+    S = 16 * int(rng.integers(1024, 4096 + 1))  # 16 .. 64 KiB, multiples of 16
+    os.environ["RS_AMD_PINNED_SEQ"] = "0"
+    try:
+        q = rs_amd.Seq(k + r, S)
+    finally:
+        os.environ.pop("RS_AMD_PINNED_SEQ")
+    registered = all(rs_amd.symbol_registered(x) == 1 for x in q.symbols)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    for i in range(k):
+        q.symbols[i][:] = data[i]
+    rs = rs_amd.RS()
+    want = np.zeros((k + r, S), np.uint8)
+    want[:k] = data
+    assert oracle_encode(k, r, want) == 0
+    ok = registered
+    er = np.zeros(k + r, bool)
+    er[rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    for call in range(4):
+        assert rs.generate_repair_symbols(q, r) == 0
+        ok = ok and bool(np.array_equal(np.stack(q.symbols), want))
+        for i in np.nonzero(er)[0]:
+            q.symbols[i][:] = 0
+        assert rs.restore_symbols(k, r, q, er, int(er.sum())) == 0
+        got = np.stack(q.symbols)
+        ok = ok and bool(np.array_equal(got[:k], data)) and not got[k:][er[k:]].any()
+    q.close()
+    rs.close()
+    return dict(family="dropin_reg", k=k, r=r, S=S, stripes=1, t=int(er.sum()), registered=registered, ok=ok)
+
+
+def one_ps16():
+    """rsg_decode_batch of a GF(2^16) code with a different pattern on every stripe: the per-stripe route
+    (syndromes of all slots + a device-built solve per stripe); garbage in erased slots."""
+    k = int(rng.integers(150, 700))
+    r = int(rng.integers(max(1, 256 - k), 300))
+    S = 1024 * int(rng.integers(1, 5))
+    n = int(rng.integers(3, 40))
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev.copy_(torch.from_numpy(host))
+    codec = rs_amd.Codec(k, r)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    rcv = full.copy()
+    rcv[pats] = rng.integers(0, 256, (int(pats.sum()), S), dtype=np.uint8)
+    dev.copy_(torch.from_numpy(rcv))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    out = dev.cpu().numpy()
+    ok = bool(np.array_equal(out[:, :k], full[:, :k]))
+    rep = pats.copy()
+    rep[:, :k] = False
+    ok = ok and bool(np.array_equal(out[rep], rcv[rep]))
+    for s in rng.choice(n, min(n, 3), replace=False):
+        ref = rcv[s].copy()
+        ref[pats[s]] = 0
+        assert oracle_decode(k, r, ref, pats[s], int(pats[s].sum())) == 0
+        ok = ok and bool(np.array_equal(out[s, :k], ref[:k]))
+    kern = codec.last_kernel
+    codec.close()
+    return dict(family="ps16", k=k, r=r, S=S, stripes=n, decode=kern, ok=ok)
+
+
+def one_orbit():
+    """GF(2^16) decode patterns closed under a Frobenius power (runs of slots spaced 16 / 2^j apart inside
+    the 16-slot cosets, whole cosets, like the C5 bench pattern): the plain route with the k_bs16 stage
+    over row orbits; repair cosets or parts of them may be erased too."""
+    k = 16 * int(rng.integers(20, 90))
+    r = 16 * int(rng.integers(4, 18))
+    S = 1024 * int(rng.integers(1, 3))
+    n = int(rng.integers(1, 3))
+    from _util import oracle_positions
+    pos = oracle_positions(k, r).astype(np.int64)
+    runs, i = [], 0
+    while i < k + r:  # cosets: runs of slots whose positions double
+        j = i + 1
+        while j < k + r and j - i < 16 and pos[j] == (2 * pos[j - 1]) % 65535:
+            j += 1
+        runs.append((i, j - i))
+        i = j
+    step = int(rng.choice([1, 2, 4, 8]))  # slot spacing inside a coset: orbit under x -> x^(2^step)
+    er = np.zeros(k + r, bool)
+    for a, m in [runs[x] for x in rng.permutation(len(runs))]:
+        if m != 16:
+            continue
+        c = int(rng.integers(0, step))
+        sl = [a + c + step * b for b in range(16 // step)]
+        if er.sum() + len(sl) > r:
+            break
+        er[sl] = True
+    if not er[:k].any():
+        return dict(family="orbit", k=k, r=r, S=S, stripes=n, skipped=True, ok=True)
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route_min_bytes", 0)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    poisoned = got.copy()
+    poisoned[:, er] = 0
+    dev.copy_(torch.from_numpy(poisoned))
+    codec.decode(dev, er)
+    torch.cuda.synchronize()
+    out = dev.cpu().numpy()
+    ok = True
+    for s in range(n):
+        ref = poisoned[s].copy()
+        assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
+        ok = ok and bool(np.array_equal(out[s], ref))
+    kern = codec.last_kernel
+    codec.close()
+    return dict(family="orbit", k=k, r=r, S=S, stripes=n, t=int(er.sum()), step=step, decode=kern, ok=ok)
+
+
 def one(family):
     if family == "dropin":
         return one_dropin()
+    if family == "dropin_reg":
+        return one_dropin_reg()
+    if family == "ps16":
+        return one_ps16()
+    if family == "orbit":
+        return one_orbit()
     if family in ("xj", "generic", "batch"):
         k = int(rng.integers(1, 200))
         r = int(rng.integers(1, min(255 - k, 80) + 1))
@@ -140,15 +279,16 @@ def one(family):
     return dict(family=family, k=k, r=r, S=S, stripes=n, encode=enc_kernel, decode=dec_kernel, ok=ok)
 
 
-families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "reenc", "batch",
-                                                             "batch16", "dropin"]
-i = 0
-while time.time() < t_end:
-    fam = families[i % len(families)]
-    i += 1
-    res = one(fam)
-    counts[fam] = counts.get(fam, 0) + 1
-    fails += 0 if res["ok"] else 1
-    print(json.dumps(res), flush=True)
-print(json.dumps({"summary": True, "cases": counts, "failures": fails}), flush=True)
-sys.exit(1 if fails else 0)
+if __name__ == "__main__":
+    families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "reenc", "batch",
+                                                                 "batch16", "dropin", "ps16", "orbit", "dropin_reg"]
+    i = 0
+    while time.time() < t_end:
+        fam = families[i % len(families)]
+        i += 1
+        res = one(fam)
+        counts[fam] = counts.get(fam, 0) + 1
+        fails += 0 if res["ok"] else 1
+        print(json.dumps(res), flush=True)
+    print(json.dumps({"summary": True, "cases": counts, "failures": fails}), flush=True)
+    sys.exit(1 if fails else 0)
