@@ -24,6 +24,7 @@
 #include "rs_xj.hpp"
 #include <thread>
 #include <unistd.h>
+#include <sys/mman.h>
 
 extern "C" {
 #include <memory/seq.h>
@@ -2602,11 +2603,15 @@ const uint8_t* arena_run(symbol_t* const* syms, size_t cnt, size_t S, size_t* pi
 }
 
 // Caller-owned symbols outside the arenas (symbol_create; seq_create with RS_AMD_PINNED_SEQ=0): data of
-// kRegMinBytes or more is allocated page-aligned in whole pages, so no two symbols share a page, and
-// recorded here. A per-call use page-locks and maps it once (hipHostRegister, within the pinned cap,
-// cached until symbol_destroy); from then on a call moves such symbols with one gather kernel and one
-// scatter kernel across PCIe (launch_gather_ptrs / launch_scatter_ptrs) instead of host copies through
-// staging. Only buffers this library allocated are registered: it alone knows when they are freed.
+// kRegMinBytes or more lives in whole pages of its own (sym_va_take), recorded here and page-locked and mapped at
+// creation (hipHostRegister, within the pinned cap). A per-call use then moves such symbols with zero-copy
+// or gather / scatter kernels across PCIe instead of host copies through staging. Only buffers this
+// library allocated are registered: it alone knows when they are freed.
+// A registered range is never handed back to the process for reuse: symbol_destroy parks it, still
+// registered, in an idle pool (later symbol_create calls of a similar size take it back: no second
+// registration), and past the pool's cap unregisters it and leaves its address range reserved with no
+// memory behind it (PROT_NONE). Once-registered addresses reused by other allocations -- pageable torch /
+// numpy buffers that the runtime copies into -- were followed by GPU faults in those copies.
 constexpr size_t kRegMinBytes = size_t(16) << 10;
 constexpr size_t kPage = 4096;
 struct SymEnt {
@@ -2615,23 +2620,80 @@ struct SymEnt {
 };
 struct SymRegistry {
     std::mutex mu;
-    std::unordered_map<uintptr_t, SymEnt> m;
+    std::unordered_map<uintptr_t, SymEnt> m;  // live symbols
+    size_t idle_bytes = 0;                    // blocks parked in sym_idle()
+    uint8_t* va_base = nullptr;               // current address reservation (sym_va_take)
+    size_t va_size = 0, va_used = 0;
 };
 SymRegistry& symreg() {
     static SymRegistry* r = new SymRegistry;  // never destroyed: symbols may outlive static destructors
     return *r;
 }
+size_t sym_pool_cap() {
+    static const size_t cap = [] {
+        if (const char* e = std::getenv("RS_AMD_SYM_POOL_MB")) return size_t(std::strtoull(e, nullptr, 10)) << 20;
+        return size_t(1) << 30;
+    }();
+    return cap;
+}
 
 bool sym_register(uint8_t* p, SymEnt& e);
+
+// Fresh pages at increasing addresses from a reserved address range (64 GiB per reservation, no memory
+// behind it until used), so consecutive symbol_create calls of one size sit at one stride (the zero-copy
+// kernels' condition) and no address is ever handed out twice except through the idle pool.
+uint8_t* sym_va_take(SymRegistry& R, size_t bytes) {
+    if (!R.va_base || R.va_used + bytes > R.va_size) {
+        const size_t sz = std::max(size_t(64) << 30, bytes);
+        void* r = mmap(nullptr, sz, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (r == MAP_FAILED) return nullptr;
+        R.va_base = static_cast<uint8_t*>(r);
+        R.va_size = sz;
+        R.va_used = 0;
+    }
+    uint8_t* p = R.va_base + R.va_used;
+    if (mmap(p, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED, -1, 0) == MAP_FAILED)
+        return nullptr;
+    R.va_used += bytes;
+    return p;
+}
+
+// back to a reserved range without memory (the address is never reused)
+void sym_va_retire(uint8_t* p, size_t bytes) {
+    (void)mmap(p, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+}
+
+// a parked block (registered, or not when the cap or a missing GPU refused it): host address and entry
+struct IdleBlock {
+    uint8_t* host;
+    SymEnt e;
+};
+std::multimap<size_t, IdleBlock>& sym_idle() {
+    static auto* m = new std::multimap<size_t, IdleBlock>;  // guarded by symreg().mu
+    return *m;
+}
 
 uint8_t* sym_alloc(size_t S) {
     if (S < kRegMinBytes) return nullptr;
     const size_t bytes = (S + kPage - 1) / kPage * kPage;
-    void* p = std::aligned_alloc(kPage, bytes);
-    if (!p) return nullptr;
-    std::memset(p, 0, bytes);
     SymRegistry& R = symreg();
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        auto& idle = sym_idle();
+        auto it = idle.lower_bound(bytes);
+        if (it != idle.end() && it->first <= 2 * bytes) {  // a parked registered block of a similar size
+            IdleBlock b = it->second;
+            idle.erase(it);
+            R.idle_bytes -= b.e.bytes;
+            std::memset(b.host, 0, b.e.bytes);
+            SymEnt& e = R.m[uintptr_t(b.host)] = b.e;
+            (void)sym_register(b.host, e);  // parked unregistered (cap, no GPU then): try again
+            return b.host;
+        }
+    }
     std::lock_guard<std::mutex> lk(R.mu);
+    uint8_t* p = sym_va_take(R, bytes);
+    if (!p) return nullptr;
     SymEnt& e = R.m[uintptr_t(p)] = SymEnt{bytes, nullptr};
     // page-lock it now, as seq_create's arenas are (the per-call path then never pays for it); a failure
     // (no GPU, the pinned cap) leaves it to the first use
@@ -2648,8 +2710,8 @@ bool sym_register(uint8_t* p, SymEnt& e) {
         if (A.no_pinning || A.pinned + e.bytes > pinned_cap()) return false;
         A.pinned += e.bytes;
     }
-    // never touch a range the runtime already knows (another registration, its own pinned buffers): a
-    // failed registration must not be followed by an unregister, which would remove the owner's mapping
+    // never touch a range the runtime already knows: a failed registration must not be followed by an
+    // unregister, which would remove the owner's mapping
     hipPointerAttribute_t attr{};
     const bool known = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type != hipMemoryTypeUnregistered;
     (void)hipGetLastError();
@@ -2669,27 +2731,33 @@ bool sym_register(uint8_t* p, SymEnt& e) {
     return true;
 }
 
-// true (and p freed, unregistered first) when p came from sym_alloc
+// true (and p parked or released) when p came from sym_alloc
 bool sym_release(uint8_t* p) {
     SymRegistry& R = symreg();
-    size_t pinned = 0;
+    SymEnt e;
     {
         std::lock_guard<std::mutex> lk(R.mu);
         auto it = R.m.find(uintptr_t(p));
         if (it == R.m.end()) return false;
-        if (it->second.dev) {
-            (void)hipHostUnregister(p);
-            (void)hipGetLastError();
-            pinned = it->second.bytes;
-        }
+        e = it->second;
         R.m.erase(it);
+        if (R.idle_bytes + e.bytes <= sym_pool_cap()) {
+            sym_idle().emplace(e.bytes, IdleBlock{p, e});
+            R.idle_bytes += e.bytes;
+            return true;
+        }
+        if (!e.dev) {  // never registered
+            sym_va_retire(p, e.bytes);
+            return true;
+        }
     }
-    if (pinned) {
-        ArenaRegistry& A = arenas();
-        std::lock_guard<std::mutex> lk(A.mu);
-        A.pinned -= pinned;
-    }
-    std::free(p);
+    // over the pool's cap: unregister, then keep the address range reserved without memory behind it
+    (void)hipHostUnregister(p);
+    (void)hipGetLastError();
+    sym_va_retire(p, e.bytes);
+    ArenaRegistry& A = arenas();
+    std::lock_guard<std::mutex> lk(A.mu);
+    A.pinned -= e.bytes;
     return true;
 }
 

@@ -246,3 +246,32 @@ def test_seq_create_without_gpu_falls_back_to_heap():
     small = rs_amd.Seq(4, 16)  # below the arena threshold: always heap
     assert len(small.symbols) == 4
     small.close()
+
+
+def test_symbol_create_pages_and_pool():
+    """symbol_create from 16 KiB (seq_create with RS_AMD_PINNED_SEQ=0): whole zeroed pages of their own at
+    increasing addresses (consecutive symbols of one size at one stride, the zero-copy condition);
+    symbol_destroy parks them (registered ones stay registered) and the next symbols of that size take
+    the same addresses back, zeroed, so a once-registered address never returns to other allocators.
+    Without a GPU the registration is refused (0), never -1 (unknown pointer)."""
+    S = 3 * 4096 + 4096 + 100
+    os.environ["RS_AMD_PINNED_SEQ"] = "0"
+    try:
+        q = rs_amd.Seq(6, S)
+        addrs = [x.ctypes.data for x in q.symbols]
+        page = (S + 4095) // 4096 * 4096
+        assert all(a % 4096 == 0 for a in addrs)
+        assert [b - a for a, b in zip(addrs, addrs[1:])] == [page] * 5
+        assert all(rs_amd.symbol_registered(x) in (0, 1) for x in q.symbols)
+        for x in q.symbols:
+            x[:] = 0xA5
+        q.close()
+        q2 = rs_amd.Seq(6, S)
+        assert sorted(x.ctypes.data for x in q2.symbols) == sorted(addrs)
+        assert all(not x.any() for x in q2.symbols)
+        q2.close()
+    finally:
+        os.environ.pop("RS_AMD_PINNED_SEQ")
+    small = rs_amd.Seq(3, 4096)  # below 16 KiB: calloc, not tracked
+    assert all(rs_amd.symbol_registered(x) == -1 for x in small.symbols)
+    small.close()
