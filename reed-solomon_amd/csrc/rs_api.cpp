@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "gen/asm_counts.h"
+#include "gen/cs16t_off.h"
 #include "gf16.hpp"
 #include "rs_jit.hpp"
 #include "rs_kernels.hpp"
@@ -273,6 +274,8 @@ struct DevPlan {
         int64_t max_slot = 0;       // largest input slot (the loads' byte range)
         int32_t* groups = nullptr;  // [ngroups + 2][16] input slots, -1 = none
         uint32_t* rec = nullptr;
+        uint32_t* rec_t = nullptr;  // k_cs16t's records (kind 0): [ntiles][ngroups + 2][16] block offsets
+        uint64_t valu_t = 0;        // k_cs16t VALU per column unit (sum over tiles and groups of its blocks)
         int32_t* fin = nullptr;
         int32_t* fin_off = nullptr;
         uint32_t nblog[16] = {};
@@ -627,6 +630,7 @@ struct rsg_codec {
     int64_t ps_chunk = 0;   // option m16_ps_chunk: max stripes per chunk (0 = by ps_rec_mib)
     int64_t ps_rec_mib = 1024;  // records per chunk (MiB); larger chunks keep k_cs16 busier (measured 48-1024)
     size_t ps_rec_cap = 0, ps_small_cap = 0;
+    int m16_cs_thread = 1;  // option m16_cs_thread: 1 k_cs16t (threaded blocks), 0 k_cs16 (gpr-index lookups)
     int m16_cs_col = 256;  // option m16_cs_col: the route kernels' block layout (256 or 1024 bytes, rs_kernels.hip)
     size_t cs_cap = 0;
     void* d_goff[2] = {nullptr, nullptr};  // syndrome route: input slots as byte offsets (per stage)
@@ -771,6 +775,8 @@ struct CsHost {
     int D = 0, ngroups = 0, ntiles = 0, fin_stride = 1;
     std::vector<int32_t> groups, fin, fin_off;
     std::vector<uint8_t> rec;
+    std::vector<uint32_t> rec_t;  // k_cs16t (gen_asm.py cs16t): block p = 4c + n of a step is (c, n, nibble n of z)
+    uint64_t valu_t = 0;
 };
 
 static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int32_t>& in_slots, int D) {
@@ -824,6 +830,10 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
     std::vector<uint8_t> rec(size_t(ntiles) * size_t(ng + 2) * CW * 16, 0);
     std::vector<int32_t> fin(size_t(ntiles) * size_t(std::max(fin_stride, 1)), 0),
         fin_off(size_t(ntiles) * (CW + 1), 0);
+    // k_cs16t records: every entry names a block of its own position p (padding: the empty block v = 0),
+    // so every step's chain runs blocks 0..15 and returns
+    std::vector<uint32_t> rec_t(size_t(ntiles) * size_t(ng + 2) * 16);
+    for (size_t i = 0; i < rec_t.size(); ++i) rec_t[i] = kCs16tOff[(i % 16) * 16];
     for (int t = 0; t < ntiles; ++t) {
         int e = 0;
         for (int cl = 0; cl < CW; ++cl) {
@@ -840,11 +850,23 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
                     for (int d = 0; d < 4; ++d) v = uint8_t(v | (((z >> ((tp - d + 16) % 16)) & 1u) << d));
                     r[tp] = v;
                 }
+                uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * 16;
+                for (int nb = 0; nb < 4; ++nb) rt[4 * cl + nb] = kCs16tOff[(4 * cl + nb) * 16 + ((z >> (4 * nb)) & 15u)];
             }
         }
         fin_off[size_t(t) * (CW + 1) + CW] = e;
     }
+    uint64_t valu_t = 0;  // moves + address adds (32) and the blocks' VALU, every step of every tile
+    std::vector<uint32_t> off_valu(kCs16tOff[255] + 1, 0);
+    for (int b = 0; b < 256; ++b) off_valu[kCs16tOff[b]] = kCs16tValu[b];
+    for (int t = 0; t < ntiles; ++t)
+        for (int g = 0; g < ng; ++g) {
+            valu_t += 32;
+            for (int p = 0; p < 16; ++p) valu_t += off_valu[rec_t[(size_t(t) * size_t(ng + 2) + size_t(g)) * 16 + size_t(p)]];
+        }
     CsHost h;
+    h.rec_t = std::move(rec_t);
+    h.valu_t = valu_t;
     h.D = D;
     h.ngroups = ng;
     h.ntiles = ntiles;
@@ -867,6 +889,7 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
     PlanBlob blob;  // groups, records and finish lists in the plan's one allocation
     const size_t o_g = blob.add(h.groups.data(), h.groups.size() * 4), o_r = blob.add(h.rec.data(), h.rec.size());
     const size_t o_f = blob.add(h.fin.data(), h.fin.size() * 4), o_fo = blob.add(h.fin_off.data(), h.fin_off.size() * 4);
+    const size_t o_t = h.rec_t.empty() ? 0 : blob.add(h.rec_t.data(), h.rec_t.size() * 4);
     if (int rc = blob.upload(p, st)) return rc;
     if (int rc = PlanBlob::finish(p)) return rc;
     auto cs = std::make_unique<DevPlan::Cs>();
@@ -878,6 +901,8 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
     cs->groups = PlanBlob::at<int32_t>(p, o_g);
     cs->h_groups = h.groups;
     cs->rec = PlanBlob::at<uint32_t>(p, o_r);
+    if (!h.rec_t.empty()) cs->rec_t = PlanBlob::at<uint32_t>(p, o_t);
+    cs->valu_t = h.valu_t;
     cs->fin = PlanBlob::at<int32_t>(p, o_f);
     cs->fin_off = PlanBlob::at<int32_t>(p, o_fo);
     for (int32_t v : in_slots) cs->max_slot = std::max<int64_t>(cs->max_slot, v);
@@ -1233,6 +1258,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         }
         return 0;
     }
+    if (!std::strcmp(name, "m16_cs_thread")) {  // k_cs16t (1) or k_cs16 (0) syndromes (results identical)
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->m16_cs_thread = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "m16_cs_col")) {  // k_cs16 / k_bs16 block layout (results identical)
         if (value != 256 && value != 1024) return RS_ERR_INVALID;
         c->m16_cs_col = int(value);
@@ -1340,6 +1370,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         c->last_kernel = "bs16";
         return scratch_release(c, st);
     }
+    const bool thr = c->m16_cs_thread && cs.rec_t;
     const int64_t per = int64_t(cs.D) * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
@@ -1350,16 +1381,23 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst = static_cast<uint8_t*>(c->d_cs);
         a.dst_stripe = per;
         a.units = cn * a.nchunks;
-        HIP_TRY(launch_cs16(a, st));
-        const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
-        c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
-        c->work_salu += steps * kSalu_cs16a;
+        if (thr) {
+            a.rec = cs.rec_t;
+            HIP_TRY(launch_cs16t(a, st));
+            c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
+            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups) * kSalu_cs16t;
+        } else {
+            HIP_TRY(launch_cs16(a, st));
+            const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+            c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
+            c->work_salu += steps * kSalu_cs16a;
+        }
         if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,
                               dst_stripe, dst_sym, uint64_t(cn), S, st))
             return rc;
         second = c->last_kernel;
     }
-    c->last_kernel = "cs16+" + second;
+    c->last_kernel = (thr ? "cs16t+" : "cs16+") + second;
     return scratch_release(c, st);
 }
 
@@ -1374,18 +1412,19 @@ static int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_s
     if (int rc = scratch_acquire(c, st)) return rc;
     if (int rc = grow(&c->d_reenc, c->reenc_cap, size_t(chunk * per))) return rc;
     uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
-    std::string k2;
+    std::string k1, k2;
     for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
         const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
         uint8_t* b = base + c0 * stripe_stride;
         if (int rc = run_cs(c, E, b, stripe_stride, sym, y, per, int64_t(S), uint64_t(cn), S, st, p.reenc->groups))
             return rc;
+        k1 = c->last_kernel;  // the encode route over U: "cs16t+bs16" / "cs16+bs16"
         HIP_TRY(launch_xor_rows(y, per, int64_t(S), b + k * sym, stripe_stride, sym, r, int64_t(S), cn, st));
         if (int rc = run_plan(c, *p.reenc->drep, y, per, int64_t(S), b, stripe_stride, sym, uint64_t(cn), S, st))
             return rc;
         k2 = c->last_kernel;
     }
-    c->last_kernel = "cs16+bs16+xor+" + k2;
+    c->last_kernel = k1 + "+xor+" + k2;
     // the encode plan's records were read by these launches: its guard must cover them (run_plan does
     // this for the plans it launches; E is launched through run_cs directly)
     if (int rc = E.note_use(st)) return rc;
@@ -2173,7 +2212,8 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     ca.src_sym = symbol_stride;
     ca.goff = static_cast<const uint32_t*>(c->d_goff[0]);
     ca.in_bytes = uint32_t(cs.max_slot * symbol_stride + int64_t(S));
-    ca.rec = cs.rec;
+    const bool thr = c->m16_cs_thread && cs.rec_t;
+    ca.rec = thr ? cs.rec_t : cs.rec;
     ca.fin = cs.fin;
     ca.fin_off = cs.fin_off;
     ca.fin_stride = cs.fin_stride;
@@ -2217,10 +2257,16 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
         ca.dst = static_cast<uint8_t*>(c->d_cs);
         ca.ids = c->d_ids + c0;
         ca.units = cn * ca.nchunks;
-        HIP_TRY(launch_cs16(ca, st));
         const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
-        c->work_valu += steps * kValu_cs16a;
-        c->work_salu += steps * kSalu_cs16a;
+        if (thr) {
+            HIP_TRY(launch_cs16t(ca, st));
+            c->work_valu += uint64_t(ca.units) * uint64_t(ca.colw / 256) * cs.valu_t;
+            c->work_salu += steps * kSalu_cs16t;
+        } else {
+            HIP_TRY(launch_cs16(ca, st));
+            c->work_valu += steps * kValu_cs16a;
+            c->work_salu += steps * kSalu_cs16a;
+        }
         HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
         V1Args v{};
         v.src = static_cast<const uint8_t*>(c->d_cs);
@@ -2244,7 +2290,7 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
         HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
     }
     if ((rc = syn->note_use(st))) return rc;
-    c->last_kernel = "ps16+cs16+apply_m16_v1_ps";
+    c->last_kernel = thr ? "ps16+cs16t+apply_m16_v1_ps" : "ps16+cs16+apply_m16_v1_ps";
     return scratch_release(c, st);
 }
 

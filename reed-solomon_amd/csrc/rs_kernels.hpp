@@ -169,6 +169,9 @@ struct Cs16Args {
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);
+// the same syndromes by threaded code blocks (k_cs16t): records [ntiles][ngroups + 2][16] uint32 block
+// offsets (gen/cs16t_off.h), one group per step (ngroups need not be even)
+hipError_t launch_cs16t(const Cs16Args& a, hipStream_t st);
 // binary accumulation with per-accumulator indices (k_bs16): records [ntiles][ngroups + 2][4][64] bytes,
 // finish entries' j = output slot, written at dst + stripe * dst_stripe + j * dst_sym
 hipError_t launch_bs16(const Cs16Args& a, hipStream_t st);

@@ -31,8 +31,8 @@ def per_dispatch(d, counter, match):
     return sorted(vals.values())
 
 
-# components of the composite GF(2^16) route legs (bench names "cs16+bs16", "cs16+bs16+xor+apply_m16_v1")
-_PART = {"cs16": "rsamd::k_cs16(", "bs16": "rsamd::k_bs16(", "xor": "rsamd::k_xor_rows(",
+# components of the composite GF(2^16) route legs (bench names "cs16t+bs16", "cs16t+bs16+xor+apply_m16_v1"; cs16 = the gpr-indexed syndrome kernel)
+_PART = {"cs16": "rsamd::k_cs16(", "cs16t": "rsamd::k_cs16t(", "bs16": "rsamd::k_bs16(", "xor": "rsamd::k_xor_rows(",
          "apply_m16_v1": "k_apply_m16_v1<"}
 
 

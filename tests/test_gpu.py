@@ -20,7 +20,11 @@ pytestmark = pytest.mark.gpu
 # kernels (one / two dwords per lane), table / mask = compiler-indexed reference kernels; "auto" is
 # the library default policy (JIT for encode, generic then JIT for repeated decode patterns)
 VARIANTS = {"jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(m8_mode=18, jit=0), "idx": dict(m8_mode=2, jit=0),
-            "table": dict(m8_mode=0, jit=0), "mask": dict(m8_mode=1, jit=0), "auto": dict()}
+            "table": dict(m8_mode=0, jit=0), "mask": dict(m8_mode=1, jit=0), "auto": dict(), "cs_idx": dict()}
+# codec options of a variant (set after construction): "cs_idx" runs the GF(2^16) route's syndromes on
+# the gpr-indexed k_cs16 instead of the default threaded k_cs16t
+VARIANT_OPTS = {"cs_idx": {"m16_cs_thread": 0}}
+CS_DEFAULT = "cs16t"  # rsg_last_kernel prefix of the default GF(2^16) syndrome kernel
 
 
 def _pad(S):
@@ -37,7 +41,7 @@ def run_case_gpu(c, variant, options=None):
         host[s, :, :S] = buf
     dev = torch.from_numpy(host).cuda()
     codec = rs_amd.Codec(k, r, **VARIANTS[variant])
-    for name, value in (options or {}).items():
+    for name, value in {**VARIANT_OPTS.get(variant, {}), **(options or {})}.items():
         codec.set_option(name, value)
     st = torch.cuda.current_stream()
     base = dev.data_ptr()
@@ -67,19 +71,23 @@ M16_PRODUCTION = ("apply_m16_v1", "apply_m16_rt16", "apply_m16_rt32")  # R <= 32
 @pytest.mark.parametrize("name", GPU_CASES)
 def test_golden_batch_api(name, variant):
     c = case(name)
-    if variant != "mask" and c["k"] + c["r"] > 255 and c["op"] != "gmatrix":
-        pytest.skip("m = 16 code: one kernel family, covered by the 'mask' parametrisation")
+    m16 = c["k"] + c["r"] > 255 and c["op"] != "gmatrix"
+    if variant not in ("mask", "cs_idx") and m16:
+        pytest.skip("m = 16 code: one kernel family, covered by the 'mask' and 'cs_idx' parametrisations")
+    if variant == "cs_idx" and not m16:
+        pytest.skip("GF(256) code: no syndrome route")
+    cs = "cs16" if variant == "cs_idx" else CS_DEFAULT
     rc, out, kern, m = run_case_gpu(c, variant)
     assert rc == c["rc"], (rc, kern)
     if name.startswith("c5_") and name.endswith(("_1k", "_2k")):  # full 1 KiB chunks: the production GF(2^16) path
-        assert kern in M16_PRODUCTION or kern.startswith("cs16+"), kern
+        assert kern in M16_PRODUCTION or kern.startswith(cs + "+"), kern
     if name.startswith("max_n_route"):  # k + r = 65535 on whole 1 KiB columns
         # encode: the syndrome route; decode: a new pattern's first 64 MiB launch runs the dense plan
         # (m16_route_min_bytes), so the route is pinned by a second run that takes it at once
-        assert kern.startswith("cs16+") if c["op"] == "encode" else kern in M16_PRODUCTION, kern
+        assert kern.startswith(cs + "+") if c["op"] == "encode" else kern in M16_PRODUCTION, kern
         if c["op"] == "decode":
             rc2, out2, kern2, _ = run_case_gpu(c, variant, {"m16_route_min_bytes": 0})
-            assert rc2 == c["rc"] and kern2.startswith("cs16+bs16+xor+"), kern2  # the re-encode decode
+            assert rc2 == c["rc"] and kern2.startswith(cs + "+bs16+xor+"), kern2  # the re-encode decode
             check_golden(c, out2)
     check_golden(c, out)
 
@@ -401,7 +409,7 @@ def test_decode_batch_m16_per_stripe_route_vs_golden():
     dev.copy_(torch.from_numpy(host))
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert codec.last_kernel == "ps16+cs16+apply_m16_v1_ps", codec.last_kernel
+    assert codec.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", codec.last_kernel
     got = dev.cpu().numpy()
     for s, c in enumerate(cases):
         check_golden(c, got[s].tobytes())
@@ -431,7 +439,7 @@ def test_decode_batch_m16_per_stripe_route(k, r, S, n):
     dev.copy_(torch.from_numpy(host))
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert codec.last_kernel == "ps16+cs16+apply_m16_v1_ps", codec.last_kernel
+    assert codec.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", codec.last_kernel
     got = dev.cpu().numpy()
     assert np.array_equal(got[:, :k], full[:, :k])
     rep = pats.copy()
@@ -580,12 +588,51 @@ def test_c5_bench_decode_kernels_vs_golden(name):
     rc, out, kern, m = run_case_gpu(c, "auto", {"m16_route_min_bytes": 0})
     assert rc == c["rc"] == 0 and m == 16
     if "bench" in name:  # erased set closed under x -> x^16: the plain route with the k_bs16 second stage
-        assert kern == "cs16+bs16", kern
+        assert kern == CS_DEFAULT + "+bs16", kern
     elif any(e >= c["k"] for e in c["erased"]):
-        assert kern.startswith("cs16+apply"), kern
+        assert kern.startswith(CS_DEFAULT + "+apply"), kern
     else:
-        assert kern.startswith("cs16+bs16+xor+"), kern
+        assert kern.startswith(CS_DEFAULT + "+bs16+xor+"), kern
     check_golden(c, out)
+
+
+@pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 12), (4096, 1024, 1024, 2), (300, 64, 3072, 9)])
+def test_cs16_threaded_matches_indexed(k, r, S, n):
+    """The threaded syndrome kernel k_cs16t (default) and the gpr-indexed k_cs16 (m16_cs_thread = 0) give
+    byte-identical repair symbols, and byte-identical restores for the bench pattern, a random information
+    pattern and a mixed pattern on the route (m16_route_min_bytes = 0); the restores equal the encoded
+    stripes and stripe 0's repair equals the oracle's."""
+    outs = {}
+    for thr in (1, 0):
+        dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+        rs_amd.fill_info(dev, k, seed=0xC516)
+        codec = rs_amd.Codec(k, r)
+        codec.set_option("m16_cs_thread", thr)
+        codec.set_option("m16_route_min_bytes", 0)
+        codec.encode(dev)
+        torch.cuda.synchronize()
+        assert codec.last_kernel.startswith("cs16t+" if thr else "cs16+"), codec.last_kernel
+        full = dev.cpu().numpy()
+        res = [full[:, k:].copy()]
+        pats = [rs_amd.bench_pattern(k, r), np.zeros(k + r, bool), np.zeros(k + r, bool)]
+        pats[1][np.random.default_rng(k).choice(k, r, replace=False)] = True
+        pats[2][np.random.default_rng(r).choice(k + r, r, replace=False)] = True
+        for er in pats:
+            dev.copy_(torch.from_numpy(full))
+            dev[:, torch.from_numpy(er)] = 0
+            assert codec.decode(dev, er) == 0
+            torch.cuda.synchronize()
+            assert codec.last_kernel.split("+")[0] == ("cs16t" if thr else "cs16"), codec.last_kernel
+            got = dev.cpu().numpy()
+            assert np.array_equal(got[:, :k], full[:, :k]), codec.last_kernel
+            res.append(got[:, :k].copy())
+        outs[thr] = (full, res)
+    for a, b in zip(outs[1][1], outs[0][1]):
+        assert np.array_equal(a, b)
+    if k + r <= 1500:
+        want = outs[1][0][0].copy()
+        assert oracle_encode(k, r, want) == 0
+        assert np.array_equal(outs[1][0][0, k:], want[k:])
 
 
 def test_m16_route_encode_then_decode_on_two_streams():
@@ -613,9 +660,9 @@ def test_m16_route_encode_then_decode_on_two_streams():
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
     for _ in range(3):
         codec.encode(a, stream=sa)
-        assert codec.last_kernel.startswith("cs16+"), codec.last_kernel
+        assert codec.last_kernel.startswith(CS_DEFAULT + "+"), codec.last_kernel
         codec.decode(b, er, stream=sb)
-        assert codec.last_kernel.startswith("cs16+"), codec.last_kernel
+        assert codec.last_kernel.startswith(CS_DEFAULT + "+"), codec.last_kernel
         torch.cuda.synchronize()
         assert np.array_equal(b.cpu().numpy(), want_b)
         b.copy_(torch.from_numpy(poisoned))
@@ -696,7 +743,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route, col):
     torch.cuda.synchronize()
     routed = route == 1 and k >= 64 and S % 1024 == 0
     dense = "apply_m16_v1" if r > 32 else f"apply_m16_rt{16 if r <= 16 else 32}"
-    assert codec.last_kernel == ("cs16+bs16" if routed else dense), codec.last_kernel
+    assert codec.last_kernel == (CS_DEFAULT + "+bs16" if routed else dense), codec.last_kernel
     got = dev.cpu().numpy()
     want = host.copy()
     for s in range(n):
@@ -746,7 +793,7 @@ def test_m16_decode_moves_to_route():
         torch.cuda.synchronize()
         kernels.append(codec.last_kernel)
         assert np.array_equal(dev.cpu().numpy(), want), f"call {call} ({codec.last_kernel})"
-    assert kernels[0] == "apply_m16_v1" and kernels[1].startswith("cs16+") and kernels[2] == kernels[1], kernels
+    assert kernels[0] == "apply_m16_v1" and kernels[1].startswith(CS_DEFAULT + "+") and kernels[2] == kernels[1], kernels
 
 
 @pytest.mark.parametrize("k,r,t,S", [(1000, 200, 200, 2048), (700, 96, 90, 1024), (4096, 1024, 1024, 1024)])
@@ -774,7 +821,7 @@ def test_m16_reenc_decode(k, r, t, S):
         dev.copy_(torch.from_numpy(poisoned))
         codec.decode(dev, er)
         torch.cuda.synchronize()
-        assert codec.last_kernel.startswith("cs16+bs16+xor+" if reenc else "cs16+apply"), codec.last_kernel
+        assert codec.last_kernel.startswith(CS_DEFAULT + ("+bs16+xor+" if reenc else "+apply")), codec.last_kernel
         outs.append(dev.cpu().numpy())
     assert np.array_equal(outs[0][:, :k], got[:, :k])
     assert np.array_equal(outs[0], outs[1])

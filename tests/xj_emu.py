@@ -164,6 +164,10 @@ class Wave:
                 self.run(finish, finish, self.call)
             elif op == "s_mov_b32":
                 self.sset(a[0], self.val(a[1]))
+            elif op == "s_mov_b64":
+                lo = int(re.match(r"s\[(\d+):", a[0]).group(1))
+                v = self.pair(a[1])
+                self.s[lo], self.s[lo + 1] = np.uint64(v & 0xFFFFFFFF), np.uint64(v >> 32)
             elif op == "s_lshr_b64":
                 lo = int(re.match(r"s\[(\d+):", a[0]).group(1))
                 v = self.pair(a[1]) >> (self.val(a[2]) & 63)
