@@ -820,22 +820,21 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
 // k_cs16t: k_cs16 without gpr-indexed VALU (gen_asm.py cs16t / cs16t_pro). The circulant of each
 // (group, syndrome coset) is run as four code blocks chosen by z's nibbles, XORing raw inputs into fixed
 // accumulator registers at full rate; the blocks are threaded by code offsets in the records
-// ([tile][ngroups + 2][16] uint32, block p = 4c + n of the step). No subset tables: 104 VGPRs in the
-// steps, 4 waves per SIMD. Same tiles, finish and block layout as k_cs16.
+// ([tile][ngroups + 2][16] uint32, block p = 4c + n of the step). No subset tables and no load ring:
+// at most 96 VGPRs, 5 waves per SIMD. Same tiles, finish and block layout as k_cs16.
 __device__ __forceinline__ void cs16t_step(const uint32_t* cp, const uint32_t* gp, u32x4s rsrc, uint32_t lane,
-                                           uint64_t base, u32x16& F, u32x16& ld, u32x16& ra, u32x16& rb,
-                                           u32x16& goff, u32x16& a0, u32x16& a1, u32x16& a2, u32x16& a3) {
+                                           uint64_t base, u32x16& F, u32x16& ra, u32x16& rb, u32x16& goff,
+                                           u32x16& a0, u32x16& a1, u32x16& a2, u32x16& a3) {
     uint32_t t0, t1;
     asm volatile(
 #include "gen/m8_idx_asm_cs16t.inc"
         : "+{v[24:39]}"(a0), "+{v[40:55]}"(a1), "+{v[56:71]}"(a2), "+{v[72:87]}"(a3), "+{v[8:23]}"(F),
-          "+{v[88:103]}"(ld), "+{s[40:55]}"(ra), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff), [t0] "=&v"(t0),
-          [t1] "=&v"(t1)
+          "+{s[40:55]}"(ra), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff), [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [cp] "s"(cp), [gp] "s"(gp), [rsrc] "s"(rsrc), [lane] "v"(lane), "{s[92:93]}"(base)
         : "s72", "s73", "s74", "s75", "memory");
 }
 
-__global__ void __launch_bounds__(256) k_cs16t(Cs16Args a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_cs16t(Cs16Args a) {
     int tile;
     int64_t local;
     uint32_t col;
@@ -845,20 +844,20 @@ __global__ void __launch_bounds__(256) k_cs16t(Cs16Args a) {
     const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
     const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 16;  // [tile][ngroups + 2][16]
     const uint32_t* goffs = a.goff;
-    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0, F = 0;
-    u32x16 ld, ra = 0, rb, goff;
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    u32x16 F, ra = 0, rb, goff;
     uint64_t base;
     uint32_t t0;
     asm volatile(
 #include "gen/m8_idx_asm_cs16t_pro.inc"
-        : "={v[88:103]}"(ld), "={s[76:91]}"(goff), "={s[56:71]}"(rb), "={s[92:93]}"(base), [t0] "=&v"(t0)
+        : "={v[8:23]}"(F), "={s[76:91]}"(goff), "={s[56:71]}"(rb), "={s[92:93]}"(base), [t0] "=&v"(t0)
         : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
         : "memory");
     for (int g = 0; g < a.ngroups; ++g)
-        cs16t_step(rec + size_t(g) * 16, goffs + size_t(g + 2) * 16, rsrc, col, base, F, ld, ra, rb, goff, a0, a1,
-                   a2, a3);
+        cs16t_step(rec + size_t(g) * 16, goffs + size_t(g + 2) * 16, rsrc, col, base, F, ra, rb, goff, a0, a1, a2,
+                   a3);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
-                 : "+{v[88:103]}"(ld), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff)
+                 : "+{v[8:23]}"(F), "+{s[56:71]}"(rb), "+{s[76:91]}"(goff)
                  :
                  : "memory");
     uint8_t* out = a.dst + local * a.dst_stripe + col;

@@ -90,10 +90,11 @@ def setup(top):
 def thread_kernel(C, ring, r2):
     F, R, A, LD, top = regs(C, ring, r2)
     nb = 4 * C
-    ld = {4: "s_load_dwordx16", 2: "s_load_dwordx8"}[C]
+    ld = {4: "s_load_dwordx16", 3: "s_load_dwordx16", 2: "s_load_dwordx8"}[C]
+    wd = {4: 16, 3: 16, 2: 8}[C]  # record window dwords
     B = setup(top)
     B += ["s_getpc_b64 s[92:93]", "s_add_u32 s92, s92, L_blocks%=-.", "s_addc_u32 s93, s93, 0",
-          "s_mov_b64 s[72:73], %[rec]", f"{ld} s[56:{55 + nb}], s[72:73], 0x0",
+          "s_mov_b64 s[72:73], %[rec]", f"{ld} s[56:{55 + wd}], s[72:73], 0x0",
           f"s_add_u32 s72, s72, {4 * nb}", "s_addc_u32 s73, s73, 0", "s_mov_b32 s94, %[nsteps]"]
     B += loads(LD if ring else F)
     B += ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_memtime %[t0]", "s_waitcnt lgkmcnt(0)", "L_loop%=:"]
@@ -105,7 +106,7 @@ def thread_kernel(C, ring, r2):
     B += ["s_waitcnt lgkmcnt(0)"] + [f"s_mov_b64 s[{40 + 2 * i}:{41 + 2 * i}], s[{56 + 2 * i}:{57 + 2 * i}]" for i in range(nb // 2)]
     if ring:
         B += loads(LD)
-    B += [f"{ld} s[56:{55 + nb}], s[72:73], 0x0", f"s_add_u32 s72, s72, {4 * nb}", "s_addc_u32 s73, s73, 0"]
+    B += [f"{ld} s[56:{55 + wd}], s[72:73], 0x0", f"s_add_u32 s72, s72, {4 * nb}", "s_addc_u32 s73, s73, 0"]
     B += ["s_getpc_b64 s[74:75]", "s_add_u32 s74, s74, L_ret%=-.", "s_addc_u32 s75, s75, 0",
           "s_add_u32 s90, s92, s40", "s_addc_u32 s91, s93, 0", "s_setpc_b64 s[90:91]", "L_ret%=:"]
     if not ring:
@@ -174,7 +175,7 @@ def records(C, r2):
 
 kernels = [idx_kernel()]
 recs, meta = [], []
-for C, ring, r2 in [(4, True, False), (4, False, False), (4, False, True), (2, False, False), (2, False, True), (2, True, True)]:
+for C, ring, r2 in [(4, False, False), (3, False, False), (3, False, True), (2, False, False)]:
     kernels.append(thread_kernel(C, ring, r2))
     rc, blk = records(C, r2)
     recs.append(rc)

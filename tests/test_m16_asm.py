@@ -251,9 +251,10 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
     """k_cs16t's group step (gen_asm.py cs16t): the 16 threaded blocks p = 4c + n named by the record
     (offsets kCs16tOff[(p, nibble n of z_c)]) give acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) for each
     of the wave's 4 syndrome cosets, exactly as cs16a; every block ends in the next record entry's block
-    and the last returns. Meanwhile the next group's inputs load into the ring at lane + slot offset (an
-    offset of 0x80000000 reads zero), the next record into s[56:71], the group after next's offsets into
-    s[76:91]. Every block's code offset is also checked by the assembler at build time."""
+    and the last returns. The next record loads into s[56:71] meanwhile; after the blocks the next
+    group's inputs load into F at lane + slot offset (an offset of 0x80000000 reads zero) and the group
+    after next's offsets into s[76:91]. Every block's code offset is also checked by the assembler at
+    build time."""
     step, head, blocks, off = cs16t_parts(tmp_path)
     assert sorted(blocks) == sorted(off) and len(off) == 256
     for b, o in enumerate(off):  # every block ends in a jump to its successor position, or returns
@@ -281,7 +282,7 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
         acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
         w = Wave(mem, {})
-        w.v[88:104] = f  # this group's inputs, in the load ring
+        w.v[8:24] = f  # this group's inputs, loaded by the previous step
         w.v[24:88] = acc0
         lane = (np.arange(64) * 4 + 512).astype(np.uint32)
         w.v[230] = lane
@@ -291,7 +292,8 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
         w.s[92], w.s[93] = 0, 0  # block base: offsets address the blocks directly
         w.s[76:92] = offs.astype(np.uint64)
-        w.run(text.splitlines(), [])  # up to the jump into block 0
+        lines = text.splitlines()
+        w.run(lines, [])  # up to the jump into block 0
         visited = []
         while True:
             target = int(w.s[72]) | (int(w.s[73]) << 32)
@@ -301,6 +303,7 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
             if blocks[target][-1] == "s_setpc_b64 s[74:75]":
                 break
         assert visited == list(rec), (visited, list(rec))
+        w.run(lines, [], entry="L_cst_ret%=")  # back in the step: the next group's loads
         w.retire(0)
         for c in range(4):
             for t in range(16):
@@ -309,11 +312,10 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
                     if (int(z[c]) >> ((t - a) % 16)) & 1:
                         want ^= f[a]
                 assert np.array_equal(w.v[24 + 16 * c + t], want), (trial, c, t)
-        assert np.array_equal(w.v[8:24], f)
         words = data.view("<u4")
         for a in range(16):
             want = np.zeros(64, np.uint32) if offs[a] == 0x80000000 else words[(offs[a] + lane) // 4]
-            assert np.array_equal(w.v[88 + a], want), (trial, a)
+            assert np.array_equal(w.v[8 + a], want), (trial, a)
         assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
         assert list(w.s[56:72]) == list(nxt_rec)
         assert list(w.s[40:56]) == list(rec)
@@ -321,10 +323,16 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
 
 def test_cs16t_prologue_loads_and_base(tmp_path):
     """k_cs16t's prologue issues group 0's 16 input loads into the ring, loads group 1's slot offsets and
-    group 0's record, and holds all 256 blocks behind a jump (nothing but the base address is executed)."""
+    group 0's record, and holds all 256 blocks behind a jump (nothing but the base address is executed).
+    The blocks read F and write the accumulators only: no block touches another register."""
     step, head, blocks, off = cs16t_parts(tmp_path)
     assert "s_branch L_cst_over%=" in head and head.index("s_getpc_b64 s[92:93]") < head.index("s_branch L_cst_over%=")
     assert sum(1 for ln in head if ln.startswith("buffer_load_dword v")) == 16
     assert {int(re.match(r"buffer_load_dword v(\d+)", ln).group(1)) for ln in head if ln.startswith("buffer_load")} \
-        == set(range(88, 104))
+        == set(range(8, 24))
+    for blk in blocks.values():
+        for ln in blk:
+            if ln.startswith("v_"):
+                regs = [int(x) for x in re.findall(r"\bv(\d+)\b", ln)]
+                assert 24 <= regs[0] < 88 and all(8 <= x < 88 for x in regs), ln
     assert off == sorted(off) and off[0] == 0
