@@ -65,6 +65,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  (default 1 GiB; 0 = at once)
  *   "m16_reenc"    GF(2^16) decodes without repair erasures and t >= 0.9 r by re-encoding: 1 (default), 0
  *   "m16_cs_col"   route kernels' block layout: 256 (default) or 1024 bytes per column unit
+ *   "m16_cs_thread" route syndromes: 1 k_cs16t, threaded code blocks at full VALU rate (default); 0 k_cs16,
+ *                  gpr-indexed subset-table lookups
  * The timing ablations (m8_mode 10-13, 15-17, 19; m16_mode 1; "stamp_buffer") exist only in the
  * diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
  * Returns RS_ERR_INVALID for unknown names or values. */
@@ -142,6 +144,11 @@ int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red);
  * (out = m2 * syndromes). info = {D, ngroups, ntiles, fin_stride, R}; arrays may be NULL. Host only. */
 int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, int32_t* groups,
                    uint8_t* rec, int32_t* fin, int32_t* fin_off, uint16_t* m2);
+/* The same plan as k_cs16t runs it: info = {cw (cosets per tile), ntiles, fin_stride, nblocks}; records
+ * [ntiles][ngroups + 2][4 cw] code-block offsets, finish lists [ntiles][fin_stride] and [ntiles][cw + 1],
+ * and the block table [nblocks] (offset of block (c, n, v) at (4c + n) * 16 + v). Host only. */
+int rsg_route_dump_t(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint32_t* rec,
+                     int32_t* fin, int32_t* fin_off, uint32_t* blocks);
 /* Symbol data from symbol_create of >= 16 KiB (page-aligned whole pages): 1 when symbol_create page-locked
  * and mapped it (hipHostRegister, until symbol_destroy), 0 when that registration was refused (the symbol
  * then goes by the staging path); -1 for any other pointer. */

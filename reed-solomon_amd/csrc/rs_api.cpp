@@ -274,8 +274,13 @@ struct DevPlan {
         int64_t max_slot = 0;       // largest input slot (the loads' byte range)
         int32_t* groups = nullptr;  // [ngroups + 2][16] input slots, -1 = none
         uint32_t* rec = nullptr;
-        uint32_t* rec_t = nullptr;  // k_cs16t's records (kind 0): [ntiles][ngroups + 2][16] block offsets
-        uint64_t valu_t = 0;        // k_cs16t VALU per column unit (sum over tiles and groups of its blocks)
+        // k_cs16t (kind 0): tiles of kCs16tCw cosets, records [ntiles_t][ngroups + 2][4 kCs16tCw] block
+        // offsets, its finish lists, and its VALU per column unit (sum over tiles and groups of its blocks)
+        uint32_t* rec_t = nullptr;
+        int32_t* fin_t = nullptr;
+        int32_t* fin_off_t = nullptr;
+        int ntiles_t = 0, fin_stride_t = 0;
+        uint64_t valu_t = 0;
         int32_t* fin = nullptr;
         int32_t* fin_off = nullptr;
         uint32_t nblog[16] = {};
@@ -775,7 +780,10 @@ struct CsHost {
     int D = 0, ngroups = 0, ntiles = 0, fin_stride = 1;
     std::vector<int32_t> groups, fin, fin_off;
     std::vector<uint8_t> rec;
-    std::vector<uint32_t> rec_t;  // k_cs16t (gen_asm.py cs16t): block p = 4c + n of a step is (c, n, nibble n of z)
+    // k_cs16t (gen_asm.py cs16t): its own tiling (kCs16tCw cosets per tile) and block-offset records
+    int ntiles_t = 0, fin_stride_t = 1;
+    std::vector<int32_t> fin_t, fin_off_t;
+    std::vector<uint32_t> rec_t;
     uint64_t valu_t = 0;
 };
 
@@ -817,54 +825,73 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
             }
         }
     }
-    constexpr int CW = 4;  // syndrome cosets per wave (k_cs16 tile)
-    const int C = int(cs_s.size()), ntiles = (C + CW - 1) / CW, nlead = int(lead.size());
-    int fin_stride = 0;
-    for (int t = 0; t < ntiles; ++t) {
-        int cnt = 0;
-        for (int c = CW * t; c < std::min(C, CW * t + CW); ++c) cnt += int(cs_need[size_t(c)].size());
-        fin_stride = std::max(fin_stride, cnt);
-    }
     const std::vector<uint16_t>& rep = normal_repr_tables()[4];
+    const int C = int(cs_s.size()), nlead = int(lead.size());
+    // finish lists of tiles of cw cosets: entry = local coset | b << 4 | j << 8, coset c's entries at
+    // [fin_off[tile][c], fin_off[tile][c + 1])
+    auto finish_lists = [&](int cw, int& ntiles, int& fin_stride, std::vector<int32_t>& fin, std::vector<int32_t>& fin_off) {
+        ntiles = (C + cw - 1) / cw;
+        fin_stride = 1;
+        for (int t = 0; t < ntiles; ++t) {
+            int cnt = 0;
+            for (int c = cw * t; c < std::min(C, cw * t + cw); ++c) cnt += int(cs_need[size_t(c)].size());
+            fin_stride = std::max(fin_stride, cnt);
+        }
+        fin.assign(size_t(ntiles) * size_t(fin_stride), 0);
+        fin_off.assign(size_t(ntiles) * size_t(cw + 1), 0);
+        for (int t = 0; t < ntiles; ++t) {
+            int e = 0;
+            for (int cl = 0; cl < cw; ++cl) {
+                const int c = cw * t + cl;
+                fin_off[size_t(t) * size_t(cw + 1) + size_t(cl)] = e;
+                if (c < C)
+                    for (auto& bj : cs_need[size_t(c)])
+                        fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (bj.first << 4) | (bj.second << 8);
+            }
+            fin_off[size_t(t) * size_t(cw + 1) + size_t(cw)] = e;
+        }
+    };
+    constexpr int CW = 4;  // syndrome cosets per wave (k_cs16 tile)
+    int ntiles = 0, fin_stride = 0;
+    std::vector<int32_t> fin, fin_off;
+    finish_lists(CW, ntiles, fin_stride, fin, fin_off);
     // records [tile][ng + 2][CW cosets][16 byte indices]; padding groups keep index 0 (table entry 0 = 0)
     std::vector<uint8_t> rec(size_t(ntiles) * size_t(ng + 2) * CW * 16, 0);
-    std::vector<int32_t> fin(size_t(ntiles) * size_t(std::max(fin_stride, 1)), 0),
-        fin_off(size_t(ntiles) * (CW + 1), 0);
-    // k_cs16t records: every entry names a block of its own position p (padding: the empty block v = 0),
-    // so every step's chain runs blocks 0..15 and returns
-    std::vector<uint32_t> rec_t(size_t(ntiles) * size_t(ng + 2) * 16);
-    for (size_t i = 0; i < rec_t.size(); ++i) rec_t[i] = kCs16tOff[(i % 16) * 16];
-    for (int t = 0; t < ntiles; ++t) {
-        int e = 0;
-        for (int cl = 0; cl < CW; ++cl) {
-            const int c = CW * t + cl;
-            fin_off[size_t(t) * (CW + 1) + size_t(cl)] = e;
-            if (c >= C) continue;
-            for (auto& bj : cs_need[size_t(c)])
-                fin[size_t(t) * size_t(fin_stride) + size_t(e++)] = cl | (bj.first << 4) | (bj.second << 8);
+    for (int t = 0; t < ntiles; ++t)
+        for (int cl = 0; cl < CW && CW * t + cl < C; ++cl)
             for (int g = 0; g < nlead; ++g) {
-                const uint32_t z = rep[(uint64_t(cs_s[size_t(c)]) * lead[size_t(g)]) % kN];
+                const uint32_t z = rep[(uint64_t(cs_s[size_t(CW * t + cl)]) * lead[size_t(g)]) % kN];
                 uint8_t* r = rec.data() + ((size_t(t) * size_t(ng + 2) + size_t(g)) * CW + size_t(cl)) * 16;
                 for (int tp = 0; tp < 16; ++tp) {  // bit d of e(t') = bit (t' - d) mod 16 of z
                     uint8_t v = 0;
                     for (int d = 0; d < 4; ++d) v = uint8_t(v | (((z >> ((tp - d + 16) % 16)) & 1u) << d));
                     r[tp] = v;
                 }
-                uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * 16;
+            }
+    // k_cs16t (gen_asm.py cs16t): tiles of kCs16tCw cosets, records [tile][ng + 2][4 kCs16tCw] block
+    // offsets, entry p = 4c + n the block (c, n, nibble n of z). Every entry names a block of its own
+    // position (padding: the empty block v = 0), so every step's chain runs all its blocks and returns.
+    constexpr int CWT = kCs16tCw, NBT = 4 * kCs16tCw;
+    CsHost h;
+    finish_lists(CWT, h.ntiles_t, h.fin_stride_t, h.fin_t, h.fin_off_t);
+    std::vector<uint32_t> rec_t(size_t(h.ntiles_t) * size_t(ng + 2) * NBT);
+    for (size_t i = 0; i < rec_t.size(); ++i) rec_t[i] = kCs16tOff[(i % NBT) * 16];
+    for (int t = 0; t < h.ntiles_t; ++t)
+        for (int cl = 0; cl < CWT && CWT * t + cl < C; ++cl)
+            for (int g = 0; g < nlead; ++g) {
+                const uint32_t z = rep[(uint64_t(cs_s[size_t(CWT * t + cl)]) * lead[size_t(g)]) % kN];
+                uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * NBT;
                 for (int nb = 0; nb < 4; ++nb) rt[4 * cl + nb] = kCs16tOff[(4 * cl + nb) * 16 + ((z >> (4 * nb)) & 15u)];
             }
-        }
-        fin_off[size_t(t) * (CW + 1) + CW] = e;
-    }
-    uint64_t valu_t = 0;  // moves + address adds (32) and the blocks' VALU, every step of every tile
-    std::vector<uint32_t> off_valu(kCs16tOff[255] + 1, 0);
-    for (int b = 0; b < 256; ++b) off_valu[kCs16tOff[b]] = kCs16tValu[b];
-    for (int t = 0; t < ntiles; ++t)
+    uint64_t valu_t = 0;  // address adds (16) and the blocks' VALU, every step of every tile
+    constexpr int NBLK = int(sizeof(kCs16tOff) / sizeof(kCs16tOff[0]));
+    std::unordered_map<uint32_t, uint32_t> off_valu;
+    for (int b = 0; b < NBLK; ++b) off_valu[kCs16tOff[b]] = kCs16tValu[b];
+    for (int t = 0; t < h.ntiles_t; ++t)
         for (int g = 0; g < ng; ++g) {
-            valu_t += 32;
-            for (int p = 0; p < 16; ++p) valu_t += off_valu[rec_t[(size_t(t) * size_t(ng + 2) + size_t(g)) * 16 + size_t(p)]];
+            valu_t += 16;
+            for (int p = 0; p < NBT; ++p) valu_t += off_valu[rec_t[(size_t(t) * size_t(ng + 2) + size_t(g)) * NBT + size_t(p)]];
         }
-    CsHost h;
     h.rec_t = std::move(rec_t);
     h.valu_t = valu_t;
     h.D = D;
@@ -889,7 +916,10 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
     PlanBlob blob;  // groups, records and finish lists in the plan's one allocation
     const size_t o_g = blob.add(h.groups.data(), h.groups.size() * 4), o_r = blob.add(h.rec.data(), h.rec.size());
     const size_t o_f = blob.add(h.fin.data(), h.fin.size() * 4), o_fo = blob.add(h.fin_off.data(), h.fin_off.size() * 4);
-    const size_t o_t = h.rec_t.empty() ? 0 : blob.add(h.rec_t.data(), h.rec_t.size() * 4);
+    const bool thr = !h.rec_t.empty();
+    const size_t o_t = thr ? blob.add(h.rec_t.data(), h.rec_t.size() * 4) : 0;
+    const size_t o_ft = thr ? blob.add(h.fin_t.data(), h.fin_t.size() * 4) : 0;
+    const size_t o_fot = thr ? blob.add(h.fin_off_t.data(), h.fin_off_t.size() * 4) : 0;
     if (int rc = blob.upload(p, st)) return rc;
     if (int rc = PlanBlob::finish(p)) return rc;
     auto cs = std::make_unique<DevPlan::Cs>();
@@ -901,7 +931,13 @@ static int upload_cs(DevPlan& p, const CsHost& h, int kind, const std::vector<in
     cs->groups = PlanBlob::at<int32_t>(p, o_g);
     cs->h_groups = h.groups;
     cs->rec = PlanBlob::at<uint32_t>(p, o_r);
-    if (!h.rec_t.empty()) cs->rec_t = PlanBlob::at<uint32_t>(p, o_t);
+    if (thr) {
+        cs->rec_t = PlanBlob::at<uint32_t>(p, o_t);
+        cs->fin_t = PlanBlob::at<int32_t>(p, o_ft);
+        cs->fin_off_t = PlanBlob::at<int32_t>(p, o_fot);
+        cs->ntiles_t = h.ntiles_t;
+        cs->fin_stride_t = h.fin_stride_t;
+    }
     cs->valu_t = h.valu_t;
     cs->fin = PlanBlob::at<int32_t>(p, o_f);
     cs->fin_off = PlanBlob::at<int32_t>(p, o_fo);
@@ -1371,6 +1407,14 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         return scratch_release(c, st);
     }
     const bool thr = c->m16_cs_thread && cs.rec_t;
+    if (thr) {  // k_cs16t's own tiling
+        a.rec = cs.rec_t;
+        a.fin = cs.fin_t;
+        a.fin_off = cs.fin_off_t;
+        a.fin_stride = cs.fin_stride_t;
+        a.ntiles = cs.ntiles_t;
+        a.cw = kCs16tCw;
+    }
     const int64_t per = int64_t(cs.D) * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
     if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
@@ -1382,10 +1426,9 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.dst_stripe = per;
         a.units = cn * a.nchunks;
         if (thr) {
-            a.rec = cs.rec_t;
             HIP_TRY(launch_cs16t(a, st));
             c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
-            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups) * kSalu_cs16t;
+            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSalu_cs16t;
         } else {
             HIP_TRY(launch_cs16(a, st));
             const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
@@ -2214,16 +2257,17 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     ca.in_bytes = uint32_t(cs.max_slot * symbol_stride + int64_t(S));
     const bool thr = c->m16_cs_thread && cs.rec_t;
     ca.rec = thr ? cs.rec_t : cs.rec;
-    ca.fin = cs.fin;
-    ca.fin_off = cs.fin_off;
-    ca.fin_stride = cs.fin_stride;
+    ca.fin = thr ? cs.fin_t : cs.fin;
+    ca.fin_off = thr ? cs.fin_off_t : cs.fin_off;
+    ca.fin_stride = thr ? cs.fin_stride_t : cs.fin_stride;
+    ca.cw = thr ? kCs16tCw : 4;
     ca.dst_stripe = per;
     ca.dst_sym = int64_t(S);
     ca.logt = logt;
     ca.expt = expt;
     for (int q = 0; q < 16; ++q) ca.nblog[q] = cs.nblog[q];
     ca.ngroups = cs.ngroups;
-    ca.ntiles = cs.ntiles;
+    ca.ntiles = thr ? cs.ntiles_t : cs.ntiles;
     ca.colw = c->m16_cs_col == 1024 ? 1024 : 256;
     ca.nchunks = int64_t(S) / ca.colw;
     if (!c->d_ps_in) {  // the apply's shared input list: input j = syndrome j of the stripe (j < r, + padding)
@@ -2257,7 +2301,7 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
         ca.dst = static_cast<uint8_t*>(c->d_cs);
         ca.ids = c->d_ids + c0;
         ca.units = cn * ca.nchunks;
-        const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+        const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(ca.ntiles) * uint64_t(cs.ngroups);
         if (thr) {
             HIP_TRY(launch_cs16t(ca, st));
             c->work_valu += uint64_t(ca.units) * uint64_t(ca.colw / 256) * cs.valu_t;
@@ -3785,6 +3829,32 @@ extern "C" int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint
     if (ok && rec) std::memcpy(rec, h.rec.data(), h.rec.size());
     if (ok && fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
     if (ok && fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);
+    return 0;
+}
+
+// k_cs16t's side of the same plan: info = {cw, ntiles_t, fin_stride_t, block count}; records [ntiles_t]
+// [ngroups + 2][4 cw] block offsets, finish lists [ntiles_t][fin_stride_t] / [ntiles_t][cw + 1], and the
+// block table kCs16tOff ([(4c + n) * 16 + v]). Host only.
+extern "C" int rsg_route_dump_t(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint32_t* rec,
+                                int32_t* fin, int32_t* fin_off, uint32_t* blocks) {
+    if (uint32_t(k) + r > kN || (is_erased && t > r)) return RS_ERR_INVALID;
+    const std::vector<uint16_t> pos = code_positions(k, r);
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(pos, k, r, is_erased, targets, emit, sources, in, outs);
+    const CsHost h = cs16_host(pos, in, int(targets.size()));
+    constexpr int NBLK = int(sizeof(kCs16tOff) / sizeof(kCs16tOff[0]));
+    if (info) {
+        info[0] = kCs16tCw;
+        info[1] = h.ntiles_t;
+        info[2] = h.fin_stride_t;
+        info[3] = NBLK;
+    }
+    if (rec) std::memcpy(rec, h.rec_t.data(), h.rec_t.size() * 4);
+    if (fin) std::memcpy(fin, h.fin_t.data(), h.fin_t.size() * 4);
+    if (fin_off) std::memcpy(fin_off, h.fin_off_t.data(), h.fin_off_t.size() * 4);
+    if (blocks) std::memcpy(blocks, kCs16tOff, sizeof(kCs16tOff));
     return 0;
 }
 

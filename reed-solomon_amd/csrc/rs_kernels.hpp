@@ -154,7 +154,8 @@ struct Cs16Args {
     uint32_t in_bytes;        // inputs' byte range past the stripe base (< 2^31; the V#'s num_records)
     const uint32_t* rec;      // [ntiles][ngroups + 2][16] packed gpr-index records (gen_asm.py cs16a/b)
     const int32_t* fin;       // [ntiles][fin_stride] needed syndromes: local coset | b << 4 | j << 8
-    const int32_t* fin_off;   // [ntiles][5] entries of local coset c: [fin_off[c], fin_off[c + 1])
+    const int32_t* fin_off;   // [ntiles][cw + 1] entries of local coset c: [fin_off[c], fin_off[c + 1])
+    int32_t cw = 4;           // syndrome cosets per tile (k_cs16 / k_bs16: 4; k_cs16t: kCs16tCw)
     int32_t fin_stride;
     uint8_t* dst;             // syndrome j of launch-local stripe s at dst + s * dst_stripe + j * dst_sym
     int64_t dst_stripe, dst_sym;
@@ -169,8 +170,8 @@ struct Cs16Args {
     const int32_t* ids;       // optional [n_stripes] stripe indices (inputs only)
 };
 hipError_t launch_cs16(const Cs16Args& a, hipStream_t st);
-// the same syndromes by threaded code blocks (k_cs16t): records [ntiles][ngroups + 2][16] uint32 block
-// offsets (gen/cs16t_off.h), one group per step (ngroups need not be even)
+// the same syndromes by threaded code blocks (k_cs16t): tiles of cw = kCs16tCw cosets, records
+// [ntiles][ngroups + 2][4 cw] uint32 block offsets (gen/cs16t_off.h), one group per step
 hipError_t launch_cs16t(const Cs16Args& a, hipStream_t st);
 // binary accumulation with per-accumulator indices (k_bs16): records [ntiles][ngroups + 2][4][64] bytes,
 // finish entries' j = output slot, written at dst + stripe * dst_stripe + j * dst_sym

@@ -93,6 +93,7 @@ _sig("rsg_coding_matrix", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
 _sig("rsg_jit_precompile", ctypes.c_int, u16, u16, P, u16)
 _sig("rsg_gamma_tables", ctypes.c_int, P, P, P)
 _sig("rsg_route_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P, P)
+_sig("rsg_route_dump_t", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
 _sig("rsg_bs16_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P)
 _sig("rsg_symbol_registered", ctypes.c_int, P)
 _sig("rsg_version", ctypes.c_char_p)
@@ -166,6 +167,27 @@ def route_dump(k, r, is_erased=None):
     if rc:
         raise RSError(rc, "rsg_route_dump")
     return dict(D=D, groups=groups, rec=rec, fin=fin, fin_off=fin_off, m2=m2)
+
+
+def route_dump_t(k, r, is_erased=None):
+    """k_cs16t's side of the syndrome route plan (host only): dict with cw, rec [ntiles][ngroups + 2][4 cw]
+    block offsets, fin [ntiles][fin_stride], fin_off [ntiles][cw + 1], blocks [(4c + n) * 16 + v] offsets."""
+    er = None if is_erased is None else np.ascontiguousarray(is_erased, dtype=np.bool_)
+    t = 0 if er is None else int(er.sum())
+    info = np.zeros(4, np.int32)
+    rc = _lib.rsg_route_dump_t(k, r, _np_ptr(er), t, _np_ptr(info), None, None, None, None)
+    if rc:
+        raise RSError(rc, "rsg_route_dump_t")
+    cw, nt, fs, nblk = (int(v) for v in info)
+    ng = route_dump(k, r, is_erased)["groups"].shape[0]
+    rec = np.zeros((nt, ng + 2, 4 * cw), np.uint32)
+    fin = np.zeros((nt, fs), np.int32)
+    fin_off = np.zeros((nt, cw + 1), np.int32)
+    blocks = np.zeros(nblk, np.uint32)
+    rc = _lib.rsg_route_dump_t(k, r, _np_ptr(er), t, None, _np_ptr(rec), _np_ptr(fin), _np_ptr(fin_off), _np_ptr(blocks))
+    if rc:
+        raise RSError(rc, "rsg_route_dump_t")
+    return dict(cw=cw, rec=rec, fin=fin, fin_off=fin_off, blocks=blocks)
 
 
 def symbol_registered(arr):

@@ -229,64 +229,69 @@ def test_bs16_step_binary_accumulation(tmp_path):
 def cs16t_parts(tmp_path):
     """(step lines, prologue lines before the blocks, {offset: block lines}, offset table) of k_cs16t."""
     d = str(tmp_path)
-    for v, f in (("cs16t", "t.inc"), ("cs16t_pro", "p.inc"), ("cs16t_off", "off.h")):
+    for v, f in (("cs16t", "t.inc"), ("cs16t_kernel", "k.inc"), ("cs16t_off", "off.h")):
         subprocess.check_call([sys.executable, GEN, os.path.join(d, f), v])
     rd = lambda f: [re.match(r'^"(.*)\\n\\t"$', ln.strip()).group(1) for ln in open(os.path.join(d, f))
                     if ln.startswith('"')]
-    step, pro = rd("t.inc"), rd("p.inc")
-    head = pro[:pro.index("L_cst_blk%=:")]
+    step, kern = rd("t.inc"), rd("k.inc")
+    head = kern[:kern.index("L_cst_blk%=:")]
     blocks, cur = {}, None
-    for ln in pro[pro.index("L_cst_blk%=:") + 1:pro.index("L_cst_over%=:")]:
+    for ln in kern[kern.index("L_cst_blk%=:") + 1:kern.index("L_cst_over%=:")]:
         m = re.match(r"\.if \. - L_cst_blk%= - (\d+)$", ln)
         if m:
             cur = blocks.setdefault(int(m.group(1)), [])
         elif not ln.startswith((".error", ".endif")):
             cur.append(ln)
     txt = open(os.path.join(d, "off.h")).read()
-    off = [int(x) for x in re.search(r"kCs16tOff\[256\] = \{([^}]*)\}", txt).group(1).split(",")]
-    return step, head, blocks, off
+    cw = int(re.search(r"kCs16tCw = (\d+);", txt).group(1))
+    off = [int(x) for x in re.search(r"kCs16tOff\[\d+\] = \{([^}]*)\}", txt).group(1).split(",")]
+    assert len(off) == 64 * cw
+    return step, head, blocks, off, cw, head + kern[kern.index("L_cst_over%=:"):]
 
 
 def test_cs16t_threaded_step_circulant_xor(tmp_path):
-    """k_cs16t's group step (gen_asm.py cs16t): the 16 threaded blocks p = 4c + n named by the record
+    """k_cs16t's group step (gen_asm.py cs16t): the 4 cw threaded blocks p = 4c + n named by the record
     (offsets kCs16tOff[(p, nibble n of z_c)]) give acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) for each
-    of the wave's 4 syndrome cosets, exactly as cs16a; every block ends in the next record entry's block
-    and the last returns. The next record loads into s[56:71] meanwhile; after the blocks the next
+    of the wave's cw syndrome cosets, exactly as cs16a; every block ends in the next record entry's block
+    and the last returns. The next record loads into s[56:] meanwhile; after the blocks the next
     group's inputs load into F at lane + slot offset (an offset of 0x80000000 reads zero) and the group
     after next's offsets into s[76:91]. Every block's code offset is also checked by the assembler at
     build time."""
-    step, head, blocks, off = cs16t_parts(tmp_path)
-    assert sorted(blocks) == sorted(off) and len(off) == 256
+    step, head, blocks, off, cw, _ = cs16t_parts(tmp_path)
+    nb = 4 * cw
+    assert sorted(blocks) == sorted(off)
     for b, o in enumerate(off):  # every block ends in a jump to its successor position, or returns
-        assert blocks[o][-1] == ("s_setpc_b64 s[74:75]" if b // 16 == 15 else "s_setpc_b64 s[72:73]"), b
-        if b // 16 < 15:
+        assert blocks[o][-1] == ("s_setpc_b64 s[74:75]" if b // 16 == nb - 1 else "s_setpc_b64 s[72:73]"), b
+        if b // 16 < nb - 1:
             assert blocks[o][-3] == f"s_add_u32 s72, s92, s{41 + b // 16}", b
     rng = np.random.default_rng(1618)
     text = "\n".join(step)
     text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[94:95]").replace("%[rsrc]", "s[96:99]")
             .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
     for trial in range(4):
-        z = rng.integers(0, 65536, 4)
+        z = rng.integers(0, 65536, cw)
         if trial == 0:
-            z[:] = [0, 0xFFFF, 1, 0x8000]
-        rec = np.array([off[(4 * c + n) * 16 + ((int(z[c]) >> (4 * n)) & 15)] for c in range(4) for n in range(4)],
+            z[:2] = [0, 0xFFFF]
+        if trial == 1:
+            z[:2] = [1, 0x8000]
+        rec = np.array([off[(4 * c + n) * 16 + ((int(z[c]) >> (4 * n)) & 15)] for c in range(cw) for n in range(4)],
                        np.uint32)
         mem = Memory(1 << 16)
-        nxt_rec = rng.integers(0, 2 ** 32, 16, dtype=np.uint64).astype(np.uint32)
-        mem.b[1024 + 64:1024 + 128] = nxt_rec.astype("<u4").view(np.uint8)  # the next group's record
+        nxt_rec = rng.integers(0, 2 ** 32, nb, dtype=np.uint64).astype(np.uint32)
+        mem.b[1024 + 4 * nb:1024 + 8 * nb] = nxt_rec.astype("<u4").view(np.uint8)  # the next group's record
         data = rng.integers(0, 256, 16384, dtype=np.uint8)
         mem.b[32768:32768 + 16384] = data
         offs = np.array([1024 * ((a * 5) % 16) for a in range(16)], np.uint32)
         offs[7] = 0x80000000  # an empty slot
         mem.b[4160:4224] = rng.integers(0, 2 ** 31, 16).astype("<u4").view(np.uint8)  # the group after next
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
-        acc0 = rng.integers(0, 2 ** 32, (64, 64), dtype=np.uint64).astype(np.uint32)
+        acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
         w = Wave(mem, {})
         w.v[8:24] = f  # this group's inputs, loaded by the previous step
-        w.v[24:88] = acc0
+        w.v[24:24 + 16 * cw] = acc0
         lane = (np.arange(64) * 4 + 512).astype(np.uint32)
         w.v[230] = lane
-        w.s[56:72] = rec.astype(np.uint64)  # this record, prefetched by the previous step
+        w.s[56:56 + nb] = rec.astype(np.uint64)  # this record, prefetched by the previous step
         w.s[100], w.s[101] = 1024, 0
         w.s[94], w.s[95] = 4160, 0
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
@@ -298,14 +303,14 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         while True:
             target = int(w.s[72]) | (int(w.s[73]) << 32)
             visited.append(target)
-            assert target in blocks and len(visited) <= 16, visited
+            assert target in blocks and len(visited) <= nb, visited
             w.run(blocks[target], [])
             if blocks[target][-1] == "s_setpc_b64 s[74:75]":
                 break
         assert visited == list(rec), (visited, list(rec))
         w.run(lines, [], entry="L_cst_ret%=")  # back in the step: the next group's loads
         w.retire(0)
-        for c in range(4):
+        for c in range(cw):
             for t in range(16):
                 want = acc0[16 * c + t].copy()
                 for a in range(16):
@@ -317,15 +322,15 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
             want = np.zeros(64, np.uint32) if offs[a] == 0x80000000 else words[(offs[a] + lane) // 4]
             assert np.array_equal(w.v[8 + a], want), (trial, a)
         assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
-        assert list(w.s[56:72]) == list(nxt_rec)
-        assert list(w.s[40:56]) == list(rec)
+        assert list(w.s[56:56 + nb]) == list(nxt_rec)
+        assert list(w.s[40:40 + nb]) == list(rec)
 
 
 def test_cs16t_prologue_loads_and_base(tmp_path):
-    """k_cs16t's prologue issues group 0's 16 input loads into the ring, loads group 1's slot offsets and
-    group 0's record, and holds all 256 blocks behind a jump (nothing but the base address is executed).
+    """k_cs16t's prologue issues group 0's 16 input loads into F, loads group 1's slot offsets and
+    group 0's record, and holds all 64 cw blocks behind a jump (nothing but the base address is executed).
     The blocks read F and write the accumulators only: no block touches another register."""
-    step, head, blocks, off = cs16t_parts(tmp_path)
+    step, head, blocks, off, cw, _ = cs16t_parts(tmp_path)
     assert "s_branch L_cst_over%=" in head and head.index("s_getpc_b64 s[92:93]") < head.index("s_branch L_cst_over%=")
     assert sum(1 for ln in head if ln.startswith("buffer_load_dword v")) == 16
     assert {int(re.match(r"buffer_load_dword v(\d+)", ln).group(1)) for ln in head if ln.startswith("buffer_load")} \
@@ -334,5 +339,67 @@ def test_cs16t_prologue_loads_and_base(tmp_path):
         for ln in blk:
             if ln.startswith("v_"):
                 regs = [int(x) for x in re.findall(r"\bv(\d+)\b", ln)]
-                assert 24 <= regs[0] < 88 and all(8 <= x < 88 for x in regs), ln
+                assert 24 <= regs[0] < 24 + 16 * cw and all(8 <= x < 24 + 16 * cw for x in regs), ln
     assert off == sorted(off) and off[0] == 0
+
+
+def test_cs16t_kernel_loop_over_groups(tmp_path):
+    """The whole k_cs16t group loop (gen_asm.py cs16t_kernel, one asm statement) in the emulator over
+    several groups: the prologue's loads, every step's record / slot-offset prefetches and threaded
+    blocks, the loop count and the final wait. The accumulators equal the circulant sums over all
+    groups' inputs (empty slots read zero); a zero group count runs no step."""
+    step, head, blocks, off, cw, main = cs16t_parts(tmp_path)
+    nb = 4 * cw
+    rng = np.random.default_rng(16016)
+    text = "\n".join(main)
+    text = (text.replace("%[g0]", "s[94:95]").replace("%[g2]", "s[98:99]").replace("%[r0]", "s[100:101]")
+            .replace("%[ng]", "s102").replace("%[rsrc]", "s[104:107]").replace("%[lane]", "v230")
+            .replace("%[t0]", "v231").replace("%[t1]", "v232"))
+    lines = text.splitlines()
+    for ng in (5, 0):
+        z = rng.integers(0, 65536, (ng, cw))
+        mem = Memory(1 << 17)
+        G0, R0, DATA = 4096, 8192, 65536
+        offs = (1024 * rng.integers(0, 32, (ng + 3, 16))).astype(np.uint32)
+        offs[rng.random((ng + 3, 16)) < 0.2] = 0x80000000  # empty slots
+        mem.b[G0:G0 + offs.size * 4] = offs.astype("<u4").view(np.uint8).reshape(-1)
+        rec = np.array([[off[(4 * c + n) * 16 + ((int(z[g, c]) >> (4 * n)) & 15)] for c in range(cw) for n in range(4)]
+                        for g in range(ng)] + [[off[p * 16] for p in range(nb)]] * 2, np.uint32)
+        mem.b[R0:R0 + rec.size * 4] = rec.astype("<u4").view(np.uint8).reshape(-1)
+        data = rng.integers(0, 256, 32768, dtype=np.uint8)
+        mem.b[DATA:DATA + 32768] = data
+        w = Wave(mem, {})
+        lane = (np.arange(64) * 4 + 256).astype(np.uint32)
+        w.v[230] = lane
+        acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
+        w.v[24:24 + 16 * cw] = acc0
+        w.s[94], w.s[95] = G0, 0
+        w.s[98], w.s[99] = G0 + 128, 0
+        w.s[100], w.s[101] = R0, 0
+        w.s[102] = ng
+        w.s[104], w.s[105], w.s[106], w.s[107] = DATA, 0, 32768, 0x20000
+        w.run(lines, [])
+        steps = 0
+        while w.setpc == "s[72:73]":  # into a step's blocks
+            visited = 0
+            while True:
+                target = int(w.s[72]) - (int(w.s[92]) | (int(w.s[93]) << 32))
+                w.run(blocks[target], [])
+                visited += 1
+                if w.setpc == "s[74:75]":
+                    break
+                assert w.setpc == "s[72:73]" and visited < nb
+            assert visited == nb
+            steps += 1
+            w.run(lines, [], entry="L_cst_ret%=")
+        assert w.setpc is None and steps == ng
+        words = data.view("<u4")
+        want = acc0.copy()
+        for g in range(ng):
+            f = [np.zeros(64, np.uint32) if offs[g, a] == 0x80000000 else words[(offs[g, a] + lane) // 4] for a in range(16)]
+            for c in range(cw):
+                for t in range(16):
+                    for a in range(16):
+                        if (int(z[g, c]) >> ((t - a) % 16)) & 1:
+                            want[16 * c + t] ^= f[a]
+        assert np.array_equal(w.v[24:24 + 16 * cw], want), ng

@@ -103,6 +103,61 @@ def test_cs16_plan_model_gives_the_syndromes(kind, k, r, t):
     assert sorted(set(np.concatenate([d["groups"].ravel(), [-1]]))) == [-1] + srcs  # each source in one group slot
 
 
+def _model_syndromes_t(d, dt, X, nb):
+    """k_cs16t's arithmetic on CPU: the record entry p = 4c + n of a (tile, group) names block (c', n', v)
+    through the block table; that block XORs f_((t - 4n' - dd) mod 16) for the set bits dd of v into
+    accumulator t of local coset c' (gen_asm.py cs16t); the finish as k_cs16's."""
+    exp, log = gf_tables()
+    cw, rec, fin, fin_off = dt["cw"], dt["rec"], dt["fin"], dt["fin_off"]
+    where = {int(o): divmod(b, 16) for b, o in enumerate(dt["blocks"])}  # offset -> (p, v)
+    assert len(where) == len(dt["blocks"])  # distinct offsets
+    groups = d["groups"]
+    nt, W = rec.shape[0], X.shape[1]
+    S = np.zeros((d["D"], W), np.int64)
+    for tile in range(nt):
+        acc = np.zeros((cw, 16, W), np.int64)
+        for g in range(groups.shape[0]):
+            f = np.array([X[s] if s >= 0 else np.zeros(W, np.int64) for s in groups[g]])
+            for p in range(4 * cw):
+                pb, v = where[int(rec[tile, g, p])]
+                assert pb == p  # every entry names a block of its own position: the chain stays in order
+                c, n = divmod(p, 4)
+                for t in range(16):
+                    for dd in range(4):
+                        if v >> dd & 1:
+                            acc[c, t] ^= f[(t - 4 * n - dd) % 16]
+        for c in range(cw):
+            for e in range(fin_off[tile, c], fin_off[tile, c + 1]):
+                ent = int(fin[tile, e])
+                assert ent & 15 == c
+                b, j = (ent >> 4) & 15, ent >> 8
+                v = np.zeros(W, np.int64)
+                for t in range(16):
+                    u = acc[c, t]
+                    nz = u != 0
+                    v ^= np.where(nz, exp[(log[u] + log[nb[(t + b) % 16]]) % 65535], 0)
+                S[j] = v
+    for tile in range(nt):  # the padding records (groups past the last, the two prefetched) are valid too
+        for g in range(groups.shape[0], rec.shape[1]):
+            assert all(where[int(rec[tile, g, p])][0] == p for p in range(4 * cw))
+    return S
+
+
+@pytest.mark.parametrize("kind,k,r,t", [CASES[0], CASES[1], ("dec", 60, 40, 40), ("dec_bench", 512, 128, 128)])
+def test_cs16t_plan_model_gives_the_syndromes(kind, k, r, t):
+    """The threaded kernel's records (rsg_route_dump_t) reproduce H * X through a numpy model of its
+    blocks, with its own tiling of cosets and finish lists."""
+    exp, _ = gf_tables()
+    er = _pattern(kind, k, r, t, seed=7)
+    d = rs_amd.route_dump(k, r, er)
+    dt = rs_amd.route_dump_t(k, r, er)
+    pos, srcs, _ = _lists(k, r, er)
+    X = np.random.default_rng(k * r).integers(0, 65536, (k + r, 2)).astype(np.int64)
+    got = _model_syndromes_t(d, dt, X, normal_basis(16))
+    H = exp[(np.arange(d["D"], dtype=np.int64)[:, None] * pos[srcs][None, :]) % 65535].astype(np.uint16)
+    assert np.array_equal(got.astype(np.uint16), gf_apply(H, X[srcs].astype(np.uint16)))
+
+
 def _model_bs16(d, Syn, nb):
     """k_bs16's arithmetic on CPU: syndromes Syn [D][W] -> {output slot: words}. Per (tile, group of 16
     syndromes) four subset tables over syndromes 4q .. 4q + 3; record byte 16q + t of a local coset is the

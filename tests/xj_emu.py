@@ -100,6 +100,7 @@ class Wave:
         blocks' return); labels, s_branch / s_cbranch_scc0/1 jumps within `lines`."""
         labels = {ln[:-1]: i for i, ln in enumerate(lines) if ln.endswith(":")}
         pc = labels[entry] if entry else 0
+        self.setpc = None  # the target pair of the s_setpc_b64 that ended this run, if one did
         while pc < len(lines):
             ln = lines[pc]
             pc += 1
@@ -114,6 +115,7 @@ class Wave:
                 continue
             self.check_vgprs(ln)
             if op == "s_setpc_b64":
+                self.setpc = a[0]
                 return
             if op == "s_branch":
                 if entry is None and a[0] in labels:  # the role code's own jumps (the finish is entered by call)
@@ -123,9 +125,9 @@ class Wave:
                 if (self.scc != 0) == (op == "s_cbranch_scc1"):
                     pc = labels[a[0]]
                 continue
-            if op in ("s_cmp_gt_u32", "s_cmp_lg_u32"):
+            if op in ("s_cmp_gt_u32", "s_cmp_lg_u32", "s_cmp_eq_u32"):
                 x, y = self.val(a[0]), self.val(a[1])
-                self.scc = int(x > y) if op == "s_cmp_gt_u32" else int(x != y)
+                self.scc = int(x > y) if op == "s_cmp_gt_u32" else int(x != y) if op == "s_cmp_lg_u32" else int(x == y)
                 continue
             if op == "s_sub_u32":
                 t = self.val(a[1]) - self.val(a[2])
@@ -149,12 +151,13 @@ class Wave:
                 # only a VGPR src0 is offset; constants and SGPRs in src0 are not
                 if re.fullmatch(r"v\d+", a[1]):
                     a[1] = f"v{_vreg(a[1]) + self.gpr_idx}"
-            if op == "s_load_dwordx16":
+            if op in ("s_load_dwordx16", "s_load_dwordx8", "s_load_dwordx4"):
                 m = re.match(r"s\[(\d+):(\d+)\]", a[0])
-                lo = int(m.group(1))
+                lo, cnt = int(m.group(1)), int(op[len("s_load_dwordx"):])
+                assert int(m.group(2)) - lo + 1 == cnt, ln
                 addr = self.pair(a[1]) + int(a[2], 0)
-                words = self.mem.load32(np.uint64(addr) + 4 * np.arange(16, dtype=np.uint64))
-                for w in range(16):
+                words = self.mem.load32(np.uint64(addr) + 4 * np.arange(cnt, dtype=np.uint64))
+                for w in range(cnt):
                     self.s[lo + w] = np.uint64(int(words[w]))
                 continue
             if op == "v_sub_u32":
