@@ -821,14 +821,14 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
 // k_cs16t: k_cs16 without gpr-indexed VALU (gen_asm.py cs16t_kernel). The circulant of each (group,
 // syndrome coset) is run as four code blocks chosen by z's nibbles, XORing raw inputs into fixed
 // accumulator registers at full rate; the blocks are threaded by code offsets in the records
-// ([tile][ngroups + 2][8] uint32, block p = 4c + n of the step). Tiles of kCs16tCw = 2 cosets: 16
-// inputs + 32 accumulators, at most 64 VGPRs, 8 waves per SIMD to cover each wave's jumps and loads.
-// The whole group loop is one asm statement: between steps, scalar and vector loads are still filling
-// the record, slot-offset and input registers, which compiler-visible code must never copy. Same block
-// layout and finish as k_cs16.
-static_assert(kCs16tCw == 2, "k_cs16t's register operands hold two cosets");
+// ([tile][ngroups + 2][16] uint32, block p = 4c + n of the step). Tiles of kCs16tCw = 4 cosets, no
+// subset tables and no load ring: 16 inputs + 64 accumulators, at most 96 VGPRs, 5 waves per SIMD to
+// cover each wave's jumps and loads. The whole group loop is one asm statement: between steps, scalar
+// and vector loads are still filling the record, slot-offset and input registers, which
+// compiler-visible code must never copy. Same block layout and finish as k_cs16.
+static_assert(kCs16tCw == 4, "k_cs16t's register operands hold four cosets");
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k_cs16t(Cs16Args a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_cs16t(Cs16Args a) {
     int tile;
     int64_t local;
     uint32_t col;
@@ -836,21 +836,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
     const int64_t stripe = RS_STRIPE(a.ids, local);
     const uint64_t sbase = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
     const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
-    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 8;  // [tile][ngroups + 2][8]
-    const uint32_t* goffs = a.goff;                                          // [ngroups + 3][16]
-    u32x16 a0 = 0, a1 = 0;
+    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 16;  // [tile][ngroups + 2][16]
+    const uint32_t* goffs = a.goff;                                           // [ngroups + 3][16]
+    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint32_t t0, t1;
     asm volatile(
 #include "gen/m8_idx_asm_cs16t_kernel.inc"
-        : "+{v[24:39]}"(a0), "+{v[40:55]}"(a1), [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : "+{v[24:39]}"(a0), "+{v[40:55]}"(a1), "+{v[56:71]}"(a2), "+{v[72:87]}"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1)
         : [g0] "s"(goffs), [g2] "s"(goffs + 32), [r0] "s"(rec), [ng] "s"(a.ngroups), [rsrc] "s"(rsrc), [lane] "v"(col)
         : "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23",
-          "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s56", "s57",
-          "s58", "s59", "s60", "s61", "s62", "s63", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80",
-          "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "scc", "memory");
+          "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55",
+          "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
+          "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
+          "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "scc", "memory");
     uint8_t* out = a.dst + local * a.dst_stripe + col;
     cs16_finish(a, a0, 0, tile, out);
     cs16_finish(a, a1, 1, tile, out);
+    cs16_finish(a, a2, 2, tile, out);
+    cs16_finish(a, a3, 3, tile, out);
 }
 
 // m = 16 binary accumulation (k_bs16, gen_asm.py bs16): the syndrome route's encode second stage. Same
