@@ -37,21 +37,24 @@ SEED = 0x5EED
 METRIC = "encode+decode GB/s (device-resident) at k/r/symbol_len; % HBM roofline"  # BASELINE.json
 
 
-def measured_traffic(kernel, cfg, with_source=False):
+def measured_traffic(kernel, cfg, with_source=False, leg=None):
     """HBM bytes per launch of `kernel` measured with rocprofv3 PMC counters on this configuration
     (profiles/traffic.json, written by scripts/traffic.py), or None when no measurement matches: the
     exact kernel name for JIT kernels (content-addressed), name + source hash for compiled ones.
     traffic.json holds one record per (kernel, config). The value is a lookup of an EARLIER rocprofv3
     run of the same kernel bytes, not a counter read in this run; `with_source` also returns where it
-    came from."""
+    came from. `leg` ("encode" / "decode") picks that leg's record when both legs run kernels of the same
+    name (the GF(2^16) route: "cs16t+bs16" for both); the newest matching record wins."""
     from srchash import kernel_src_hash
     try:
         with open(TRAFFIC_JSON) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return (None, None) if with_source else None
-    for rec in t.get("records", [t]):
+    for rec in reversed(t.get("records", [t])):
         if rec.get("config") != cfg or rec.get("bench_kernel") != kernel:
+            continue
+        if leg is not None and rec.get("leg", leg) != leg:
             continue
         if "[" not in str(kernel) and rec.get("src_hash") != kernel_src_hash(kernel):
             continue
@@ -572,10 +575,11 @@ def main():
     cpu_group_barrier(group)
 
     # roofline of the dominant kernel (encode and decode move the same algorithmic bytes here)
-    dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, kern_enc) if enc_ms >= dec_ms else (dec_ms, dec_bytes, kern_dec)
+    dom_ms, dom_bytes, dom_name, dom_leg = ((enc_ms, enc_bytes, kern_enc, "encode") if enc_ms >= dec_ms
+                                            else (dec_ms, dec_bytes, kern_dec, "decode"))
     achieved = dom_bytes / (dom_ms / 1e3) / 1e9
     cfg_key = f"k{k}_r{r}_S{S}_n{n}_t{t}"
-    traffic, traffic_src = measured_traffic(dom_name, cfg_key, with_source=True)
+    traffic, traffic_src = measured_traffic(dom_name, cfg_key, with_source=True, leg=dom_leg)
     line = base_line(args, world, n, k, r, S, t, elapsed)
     line["config"]["kernel"] = {"encode": kern_enc, "decode": kern_dec}
     line["rccl_world"] = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
@@ -587,9 +591,9 @@ def main():
         line["roofline"]["compute"] = compute_roofline(work_enc, enc_ms, work_dec, dec_ms)
     # both legs: algorithmic bytes and PMC-measured HBM bytes per launch (null when unmeasured)
     line["per_launch"] = {"encode": {"kernel": kern_enc, "ms": round(enc_ms, 3), "bytes": enc_bytes,
-                                     "traffic": measured_traffic(kern_enc, cfg_key)},
+                                     "traffic": measured_traffic(kern_enc, cfg_key, leg="encode")},
                           "decode": {"kernel": kern_dec, "ms": round(dec_ms, 3), "bytes": dec_bytes,
-                                     "traffic": measured_traffic(kern_dec, cfg_key)}}
+                                     "traffic": measured_traffic(kern_dec, cfg_key, leg="decode")}}
     line["event_steps"] = {"sampled": len(ev), "stride": stride}  # steps carrying the per-launch HIP events
     line["encode_ms"] = round(enc_ms, 3)
     line["decode_ms"] = round(dec_ms, 3)

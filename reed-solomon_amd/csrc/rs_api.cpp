@@ -1352,6 +1352,9 @@ static int scratch_acquire(rsg_codec_t* c, hipStream_t st);
 static int scratch_release(rsg_codec_t* c, hipStream_t st);
 
 constexpr uint64_t kJitMinBytes = uint64_t(1) << 20;
+// SALU per k_cs16t step: the step's own (asm_counts.h) + the block tails (3 each, 1 for the last) + the
+// loop's pointer / count updates (7)
+constexpr uint64_t kSaluStepCs16t = uint64_t(kSalu_cs16t) + 3 * (4 * kCs16tCw - 1) + 1 + 7;
 
 // Syndrome route launch (p.cs): k_cs16 writes the D syndromes of a chunk of stripes to scratch, then the
 // second stage applies the D x R matrix from there into the outputs.
@@ -1428,7 +1431,7 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         if (thr) {
             HIP_TRY(launch_cs16t(a, st));
             c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
-            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSalu_cs16t;
+            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSaluStepCs16t;
         } else {
             HIP_TRY(launch_cs16(a, st));
             const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
@@ -2305,7 +2308,7 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
         if (thr) {
             HIP_TRY(launch_cs16t(ca, st));
             c->work_valu += uint64_t(ca.units) * uint64_t(ca.colw / 256) * cs.valu_t;
-            c->work_salu += steps * kSalu_cs16t;
+            c->work_salu += steps * kSaluStepCs16t;
         } else {
             HIP_TRY(launch_cs16(ca, st));
             c->work_valu += steps * kValu_cs16a;

@@ -275,3 +275,23 @@ def test_symbol_create_pages_and_pool():
     small = rs_amd.Seq(3, 4096)  # below 16 KiB: calloc, not tracked
     assert all(rs_amd.symbol_registered(x) == -1 for x in small.symbols)
     small.close()
+
+
+def test_bench_traffic_lookup_is_per_leg(tmp_path, monkeypatch):
+    """bench.py's PMC traffic lookup (profiles/traffic.json) keys records by leg: the GF(2^16) route runs
+    kernels of one name on both legs ("cs16t+bs16"), whose HBM bytes differ; the newest record wins."""
+    import json
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    cfg = "k4096_r1024_S1024_n1024_t1024"
+    name = "kern[route]"  # a bracketed (content-addressed) name: no source-hash check
+    recs = [dict(leg="decode", bench_kernel=name, config=cfg, traffic_bytes=3.0),
+            dict(leg="encode", bench_kernel=name, config=cfg, traffic_bytes=1.0),
+            dict(leg="encode", bench_kernel=name, config=cfg, traffic_bytes=2.0)]
+    path = tmp_path / "traffic.json"
+    path.write_text(json.dumps({"records": recs}))
+    monkeypatch.setattr(bench, "TRAFFIC_JSON", str(path))
+    assert bench.measured_traffic(name, cfg, leg="encode") == 2
+    assert bench.measured_traffic(name, cfg, leg="decode") == 3
+    assert bench.measured_traffic("other[k]", cfg, leg="encode") is None
