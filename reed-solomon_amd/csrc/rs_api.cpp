@@ -883,13 +883,13 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
                 uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * NBT;
                 for (int nb = 0; nb < 4; ++nb) rt[4 * cl + nb] = kCs16tOff[(4 * cl + nb) * 16 + ((z >> (4 * nb)) & 15u)];
             }
-    uint64_t valu_t = 0;  // address adds (16) and the blocks' VALU, every step of every tile
+    uint64_t valu_t = 0;  // the step's own VALU (pair sums, lane, address adds) and its blocks', every step of every tile
     constexpr int NBLK = int(sizeof(kCs16tOff) / sizeof(kCs16tOff[0]));
     std::unordered_map<uint32_t, uint32_t> off_valu;
     for (int b = 0; b < NBLK; ++b) off_valu[kCs16tOff[b]] = kCs16tValu[b];
     for (int t = 0; t < h.ntiles_t; ++t)
         for (int g = 0; g < ng; ++g) {
-            valu_t += 16;
+            valu_t += uint64_t(kValu_cs16t);
             for (int p = 0; p < NBT; ++p) valu_t += off_valu[rec_t[(size_t(t) * size_t(ng + 2) + size_t(g)) * NBT + size_t(p)]];
         }
     h.rec_t = std::move(rec_t);

@@ -822,11 +822,11 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
 // syndrome coset) is run as four code blocks chosen by z's nibbles, XORing raw inputs into fixed
 // accumulator registers at full rate; the blocks are threaded by code offsets in the records
 // ([tile][ngroups + 2][16] uint32, block p = 4c + n of the step). Tiles of kCs16tCw = 4 cosets, no
-// subset tables and no load ring: 16 inputs + 64 accumulators, at most 96 VGPRs, 5 waves per SIMD to
-// cover each wave's jumps and loads. The whole group loop is one asm statement: between steps, scalar
+// subset tables and no load ring: 16 inputs + 16 pair sums + 64 accumulators = v[0:95], 5 waves per
+// SIMD to cover each wave's jumps and loads (the lane's column is recomputed per step from its id). The whole group loop is one asm statement: between steps, scalar
 // and vector loads are still filling the record, slot-offset and input registers, which
 // compiler-visible code must never copy. Same block layout and finish as k_cs16.
-static_assert(kCs16tCw == 4, "k_cs16t's register operands hold four cosets");
+static_assert(kCs16tCw == 4 && kCs16tF == 0 && kCs16tR == 16 && kCs16tAcc == 32, "k_cs16t's register operands");
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_cs16t(Cs16Args a) {
     int tile;
@@ -838,18 +838,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
     const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
     const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 16;  // [tile][ngroups + 2][16]
     const uint32_t* goffs = a.goff;                                           // [ngroups + 3][16]
+    // the wave's byte column (lane 0's); every VGPR is taken inside the loop, so the lanes' columns are
+    // formed there from their ids, and again here after it
+    const uint32_t colbase = __builtin_amdgcn_readfirstlane(col - (threadIdx.x & 63u) * 4u);
     u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    uint32_t t0, t1;
     asm volatile(
 #include "gen/m8_idx_asm_cs16t_kernel.inc"
-        : "+{v[24:39]}"(a0), "+{v[40:55]}"(a1), "+{v[56:71]}"(a2), "+{v[72:87]}"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1)
-        : [g0] "s"(goffs), [g2] "s"(goffs + 32), [r0] "s"(rec), [ng] "s"(a.ngroups), [rsrc] "s"(rsrc), [lane] "v"(col)
-        : "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23",
+        : "+{v[32:47]}"(a0), "+{v[48:63]}"(a1), "+{v[64:79]}"(a2), "+{v[80:95]}"(a3)
+        : [g0] "s"(goffs), [g2] "s"(goffs + 32), [r0] "s"(rec), [ng] "s"(a.ngroups), [rsrc] "s"(rsrc),
+          [colbase] "s"(colbase)
+        : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16",
+          "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31",
           "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55",
-          "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
           "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
           "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "scc", "memory");
-    uint8_t* out = a.dst + local * a.dst_stripe + col;
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    uint8_t* out = a.dst + local * a.dst_stripe + (colbase + lane * 4u);
     cs16_finish(a, a0, 0, tile, out);
     cs16_finish(a, a1, 1, tile, out);
     cs16_finish(a, a2, 2, tile, out);

@@ -227,7 +227,8 @@ def test_bs16_step_binary_accumulation(tmp_path):
 
 
 def cs16t_parts(tmp_path):
-    """(step lines, prologue lines before the blocks, {offset: block lines}, offset table) of k_cs16t."""
+    """(step lines, prologue lines before the blocks, {offset: block lines}, offset table, register bases
+    {cw, F, R, acc}, the whole kernel loop without its blocks) of k_cs16t (gen_asm.py)."""
     d = str(tmp_path)
     for v, f in (("cs16t", "t.inc"), ("cs16t_kernel", "k.inc"), ("cs16t_off", "off.h")):
         subprocess.check_call([sys.executable, GEN, os.path.join(d, f), v])
@@ -243,31 +244,43 @@ def cs16t_parts(tmp_path):
         elif not ln.startswith((".error", ".endif")):
             cur.append(ln)
     txt = open(os.path.join(d, "off.h")).read()
-    cw = int(re.search(r"kCs16tCw = (\d+);", txt).group(1))
+    regs = {k: int(v) for k, v in re.findall(r"kCs16t(Cw|F|R|Acc) = (\d+)", txt)}
     off = [int(x) for x in re.search(r"kCs16tOff\[\d+\] = \{([^}]*)\}", txt).group(1).split(",")]
-    assert len(off) == 64 * cw
-    return step, head, blocks, off, cw, head + kern[kern.index("L_cst_over%=:"):]
+    assert len(off) == 64 * regs["Cw"]
+    return step, head, blocks, off, regs, head + kern[kern.index("L_cst_over%=:"):]
+
+
+def _circulant(acc0, f, z, cw):
+    want = acc0.copy()
+    for c in range(cw):
+        for t in range(16):
+            for a in range(16):
+                if (int(z[c]) >> ((t - a) % 16)) & 1:
+                    want[16 * c + t] ^= f[a]
+    return want
 
 
 def test_cs16t_threaded_step_circulant_xor(tmp_path):
-    """k_cs16t's group step (gen_asm.py cs16t): the 4 cw threaded blocks p = 4c + n named by the record
-    (offsets kCs16tOff[(p, nibble n of z_c)]) give acc_t ^= XOR_a f_a * bit_((t - a) mod 16)(z_c) for each
-    of the wave's cw syndrome cosets, exactly as cs16a; every block ends in the next record entry's block
-    and the last returns. The next record loads into s[56:] meanwhile; after the blocks the next
-    group's inputs load into F at lane + slot offset (an offset of 0x80000000 reads zero) and the group
-    after next's offsets into s[76:91]. Every block's code offset is also checked by the assembler at
-    build time."""
-    step, head, blocks, off, cw, _ = cs16t_parts(tmp_path)
+    """k_cs16t's group step (gen_asm.py cs16t): R2_j = f_j ^ f_(j-1), then the 4 cw threaded blocks
+    p = 4c + n named by the record (offsets kCs16tOff[(p, nibble n of z_c)]) give acc_t ^= XOR_a f_a *
+    bit_((t - a) mod 16)(z_c) for each of the wave's cw syndrome cosets, exactly as cs16a; every block ends
+    in the next record entry's block and the last returns. After the blocks the next group's inputs load
+    into F at the lane's column + slot offset (an offset of 0x80000000 reads zero), the next record into
+    s[40:] and the group after next's offsets into s[76:91]. Every block's code offset is also checked by
+    the assembler at build time."""
+    step, head, blocks, off, regs, _ = cs16t_parts(tmp_path)
+    cw, F, A = regs["Cw"], regs["F"], regs["Acc"]
     nb = 4 * cw
     assert sorted(blocks) == sorted(off)
     for b, o in enumerate(off):  # every block ends in a jump to its successor position, or returns
         assert blocks[o][-1] == ("s_setpc_b64 s[74:75]" if b // 16 == nb - 1 else "s_setpc_b64 s[72:73]"), b
         if b // 16 < nb - 1:
             assert blocks[o][-3] == f"s_add_u32 s72, s92, s{41 + b // 16}", b
+        assert sum(1 for ln in blocks[o] if ln.startswith("v_")) == (0 if b % 16 == 0 else 16), b  # one op each
     rng = np.random.default_rng(1618)
     text = "\n".join(step)
     text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[94:95]").replace("%[rsrc]", "s[96:99]")
-            .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
+            .replace("%[colbase]", "s108"))
     for trial in range(4):
         z = rng.integers(0, 65536, cw)
         if trial == 0:
@@ -287,11 +300,10 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
         acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
         w = Wave(mem, {})
-        w.v[8:24] = f  # this group's inputs, loaded by the previous step
-        w.v[24:24 + 16 * cw] = acc0
-        lane = (np.arange(64) * 4 + 512).astype(np.uint32)
-        w.v[230] = lane
-        w.s[56:56 + nb] = rec.astype(np.uint64)  # this record, prefetched by the previous step
+        w.v[F:F + 16] = f  # this group's inputs, loaded by the previous step
+        w.v[A:A + 16 * cw] = acc0
+        w.s[108] = 512  # the wave's byte column
+        w.s[40:40 + nb] = rec.astype(np.uint64)  # this record, loaded by the previous step
         w.s[100], w.s[101] = 1024, 0
         w.s[94], w.s[95] = 4160, 0
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
@@ -310,51 +322,47 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         assert visited == list(rec), (visited, list(rec))
         w.run(lines, [], entry="L_cst_ret%=")  # back in the step: the next group's loads
         w.retire(0)
-        for c in range(cw):
-            for t in range(16):
-                want = acc0[16 * c + t].copy()
-                for a in range(16):
-                    if (int(z[c]) >> ((t - a) % 16)) & 1:
-                        want ^= f[a]
-                assert np.array_equal(w.v[24 + 16 * c + t], want), (trial, c, t)
+        assert np.array_equal(w.v[A:A + 16 * cw], _circulant(acc0, f, z, cw)), trial
         words = data.view("<u4")
+        lane = (np.arange(64) * 4 + 512).astype(np.uint32)
         for a in range(16):
             want = np.zeros(64, np.uint32) if offs[a] == 0x80000000 else words[(offs[a] + lane) // 4]
-            assert np.array_equal(w.v[8 + a], want), (trial, a)
+            assert np.array_equal(w.v[F + a], want), (trial, a)
         assert list(w.s[76:92]) == list(mem.load32(np.uint64(4160) + 4 * np.arange(16, dtype=np.uint64)))
-        assert list(w.s[56:56 + nb]) == list(nxt_rec)
-        assert list(w.s[40:40 + nb]) == list(rec)
+        assert list(w.s[40:40 + nb]) == list(nxt_rec)
 
 
 def test_cs16t_prologue_loads_and_base(tmp_path):
     """k_cs16t's prologue issues group 0's 16 input loads into F, loads group 1's slot offsets and
     group 0's record, and holds all 64 cw blocks behind a jump (nothing but the base address is executed).
-    The blocks read F and write the accumulators only: no block touches another register."""
-    step, head, blocks, off, cw, _ = cs16t_parts(tmp_path)
+    The blocks read F and R2 and write the accumulators only: no block touches another register."""
+    step, head, blocks, off, regs, _ = cs16t_parts(tmp_path)
+    cw, F, R, A = regs["Cw"], regs["F"], regs["R"], regs["Acc"]
     assert "s_branch L_cst_over%=" in head and head.index("s_getpc_b64 s[92:93]") < head.index("s_branch L_cst_over%=")
     assert sum(1 for ln in head if ln.startswith("buffer_load_dword v")) == 16
     assert {int(re.match(r"buffer_load_dword v(\d+)", ln).group(1)) for ln in head if ln.startswith("buffer_load")} \
-        == set(range(8, 24))
+        == set(range(F, F + 16))
     for blk in blocks.values():
         for ln in blk:
             if ln.startswith("v_"):
-                regs = [int(x) for x in re.findall(r"\bv(\d+)\b", ln)]
-                assert 24 <= regs[0] < 24 + 16 * cw and all(8 <= x < 24 + 16 * cw for x in regs), ln
+                regs_ = [int(x) for x in re.findall(r"\bv(\d+)\b", ln)]
+                assert A <= regs_[0] < A + 16 * cw and regs_[1] == regs_[0], ln
+                assert all(F <= x < F + 16 or R <= x < R + 16 for x in regs_[2:]), ln
     assert off == sorted(off) and off[0] == 0
 
 
 def test_cs16t_kernel_loop_over_groups(tmp_path):
     """The whole k_cs16t group loop (gen_asm.py cs16t_kernel, one asm statement) in the emulator over
-    several groups: the prologue's loads, every step's record / slot-offset prefetches and threaded
-    blocks, the loop count and the final wait. The accumulators equal the circulant sums over all
-    groups' inputs (empty slots read zero); a zero group count runs no step."""
-    step, head, blocks, off, cw, main = cs16t_parts(tmp_path)
+    several groups: the prologue's loads, every step's R2, threaded blocks, record / slot-offset loads,
+    the loop count and the final wait. The accumulators equal the circulant sums over all groups' inputs
+    (empty slots read zero); a zero group count runs no step."""
+    step, head, blocks, off, regs, main = cs16t_parts(tmp_path)
+    cw, F, A = regs["Cw"], regs["F"], regs["Acc"]
     nb = 4 * cw
     rng = np.random.default_rng(16016)
     text = "\n".join(main)
-    text = (text.replace("%[g0]", "s[94:95]").replace("%[g2]", "s[98:99]").replace("%[r0]", "s[100:101]")
-            .replace("%[ng]", "s102").replace("%[rsrc]", "s[104:107]").replace("%[lane]", "v230")
-            .replace("%[t0]", "v231").replace("%[t1]", "v232"))
+    text = (text.replace("%[g0]", "s[102:103]").replace("%[g2]", "s[104:105]").replace("%[r0]", "s[100:101]")
+            .replace("%[ng]", "s109").replace("%[rsrc]", "s[112:115]").replace("%[colbase]", "s108"))
     lines = text.splitlines()
     for ng in (5, 0):
         z = rng.integers(0, 65536, (ng, cw))
@@ -369,15 +377,14 @@ def test_cs16t_kernel_loop_over_groups(tmp_path):
         data = rng.integers(0, 256, 32768, dtype=np.uint8)
         mem.b[DATA:DATA + 32768] = data
         w = Wave(mem, {})
-        lane = (np.arange(64) * 4 + 256).astype(np.uint32)
-        w.v[230] = lane
         acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
-        w.v[24:24 + 16 * cw] = acc0
-        w.s[94], w.s[95] = G0, 0
-        w.s[98], w.s[99] = G0 + 128, 0
+        w.v[A:A + 16 * cw] = acc0
+        w.s[102], w.s[103] = G0, 0
+        w.s[104], w.s[105] = G0 + 128, 0
         w.s[100], w.s[101] = R0, 0
-        w.s[102] = ng
-        w.s[104], w.s[105], w.s[106], w.s[107] = DATA, 0, 32768, 0x20000
+        w.s[109] = ng
+        w.s[108] = 256
+        w.s[112], w.s[113], w.s[114], w.s[115] = DATA, 0, 32768, 0x20000
         w.run(lines, [])
         steps = 0
         while w.setpc == "s[72:73]":  # into a step's blocks
@@ -394,12 +401,9 @@ def test_cs16t_kernel_loop_over_groups(tmp_path):
             w.run(lines, [], entry="L_cst_ret%=")
         assert w.setpc is None and steps == ng
         words = data.view("<u4")
+        lane = (np.arange(64) * 4 + 256).astype(np.uint32)
         want = acc0.copy()
         for g in range(ng):
             f = [np.zeros(64, np.uint32) if offs[g, a] == 0x80000000 else words[(offs[g, a] + lane) // 4] for a in range(16)]
-            for c in range(cw):
-                for t in range(16):
-                    for a in range(16):
-                        if (int(z[g, c]) >> ((t - a) % 16)) & 1:
-                            want[16 * c + t] ^= f[a]
-        assert np.array_equal(w.v[24:24 + 16 * cw], want), ng
+            want = _circulant(want, f, z[g], cw)
+        assert np.array_equal(w.v[A:A + 16 * cw], want), ng

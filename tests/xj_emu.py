@@ -196,6 +196,14 @@ class Wave:
                 self.sset(a[0], t)
             elif op == "v_mov_b32":
                 self.vset(a[0], self.val(a[1]))
+            elif op in ("v_mbcnt_lo_u32_b32", "v_mbcnt_hi_u32_b32"):  # with an all-ones mask: lane id parts
+                assert self.val(a[1]) == 0xFFFFFFFF, ln
+                lanes = np.arange(64, dtype=np.uint64)
+                part = np.minimum(lanes, 32) if op == "v_mbcnt_lo_u32_b32" else np.maximum(lanes, 32) - 32
+                self.vset(a[0], (part + np.asarray(self.val(a[2]), np.uint64)) & np.uint64(0xFFFFFFFF))
+            elif op == "v_lshl_add_u32":
+                x = np.asarray(self.val(a[1]), np.uint64) << np.uint64(self.val(a[2]) & 31)
+                self.vset(a[0], (x + np.asarray(self.val(a[3]), np.uint64)) & np.uint64(0xFFFFFFFF))
             elif op == "v_add_u32":
                 self.vset(a[0], (np.asarray(self.val(a[1]), np.uint64) + np.asarray(self.val(a[2]), np.uint64))
                           & np.uint64(0xFFFFFFFF))
