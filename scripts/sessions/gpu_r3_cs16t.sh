@@ -15,6 +15,5 @@ echo "thr=$thr"; tail -1 gpurun_out/t_c5_$thr.log | cut -c1-200
 done
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/t_prof_c5 -o run -- python3 bench.py --k 4096 --r 1024 --symbol 1024 --stripes 1024 --steps 10 --no-cpu > gpurun_out/t_prof_c5.log 2>&1 || exit 1
 find gpurun_out/t_prof_c5 -name "*kernel_stats.csv" -exec head -8 {} \;
-# group-step designs with their loads at 1..8 waves per SIMD (scripts/ubench/gen_thread2.py)
-timeout -k 10 120 ./scripts/ubench/bin/thread2_bench > gpurun_out/t_thread2.log 2>&1 || { cat gpurun_out/t_thread2.log; exit 1; }
-cat gpurun_out/t_thread2.log
+timeout -k 10 300 python -u scripts/bench_patterns_c5.py 1024 > gpurun_out/t_patterns_c5.log 2>&1 || { tail -5 gpurun_out/t_patterns_c5.log; exit 1; }
+cat gpurun_out/t_patterns_c5.log
