@@ -295,3 +295,60 @@ def test_bench_traffic_lookup_is_per_leg(tmp_path, monkeypatch):
     assert bench.measured_traffic(name, cfg, leg="encode") == 2
     assert bench.measured_traffic(name, cfg, leg="decode") == 3
     assert bench.measured_traffic("other[k]", cfg, leg="encode") is None
+
+
+def _regs(tok):
+    """Register numbers named by an operand: ('s', {..}) / ('v', {..}) or None."""
+    m = re.fullmatch(r"([sv])(\d+)", tok)
+    if m:
+        return m.group(1), {int(m.group(2))}
+    m = re.fullmatch(r"([sv])\[(\d+):(\d+)\]", tok)
+    if m:
+        return m.group(1), set(range(int(m.group(2)), int(m.group(3)) + 1))
+    return None
+
+
+def test_no_compiler_code_touches_in_flight_load_registers(tmp_path):
+    """k_cs16 / k_bs16 issue scalar and vector loads inside one step's asm statement that land in
+    registers the NEXT step reads (records, slot offsets, inputs); k_cs16t keeps its whole loop in one
+    statement. Compiler-generated code between the asm statements must never read or write a register a
+    load issued by an earlier statement may still be filling (the round-3 k_cs16t bug: slot offsets copied
+    before their s_load landed). Loads and waits are tracked through the asm text of the gfx950 assembly
+    of rs_kernels.hip (s_waitcnt lgkmcnt(0) / vmcnt(0) retire the scalar / vector loads)."""
+    import subprocess
+    pkg = os.path.join(REPO, "reed-solomon_amd")
+    out = tmp_path / "k.s"
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+                           "-I../include", "-Icsrc", "--cuda-device-only", "-S", "csrc/rs_kernels.hip", "-o", str(out)],
+                          cwd=pkg, stderr=subprocess.DEVNULL)
+    text = out.read_text().splitlines()
+    for sym in ("_ZN5rsamd6k_cs16ENS_8Cs16ArgsE", "_ZN5rsamd6k_bs16ENS_8Cs16ArgsE", "_ZN5rsamd7k_cs16tENS_8Cs16ArgsE"):
+        start = next(i for i, ln in enumerate(text) if ln.startswith(sym + ":"))
+        end = next(i for i in range(start, len(text)) if "s_endpgm" in text[i])
+        pend = {"s": set(), "v": set()}
+        inside, checked = False, 0
+        for raw in text[start:end]:
+            if ";;#ASMSTART" in raw or ";;#ASMEND" in raw:
+                inside = ";;#ASMSTART" in raw
+                continue
+            ln = raw.split(";")[0].strip()
+            if not ln or ln.endswith(":") or ln.startswith("."):
+                continue
+            op, _, rest = ln.partition(" ")
+            ops = [x.strip().split()[0] for x in re.split(r",\s*(?![^\[]*\])", rest) if x.strip()] if rest else []
+            if inside:  # the asm's own loads and waits
+                if op == "s_waitcnt":
+                    if "lgkmcnt(0)" in rest:
+                        pend["s"].clear()
+                    if "vmcnt(0)" in rest:
+                        pend["v"].clear()
+                elif op.startswith(("s_load_dword", "buffer_load_dword", "global_load_dword")) and ops:
+                    r = _regs(ops[0])
+                    if r:
+                        pend[r[0]] |= r[1]
+                continue
+            checked += 1
+            for tok in ops:
+                r = _regs(tok)
+                assert not (r and r[1] & pend[r[0]]), (sym, raw)
+        assert checked > 0
