@@ -261,9 +261,13 @@ class Wave:
                 self.mem.store32(addr, self.val(a[1]))
                 self.vm.append((None, None))
             elif op == "buffer_load_dword" and ln.endswith(" lds"):
-                # LDS DMA: a[0] = voffset, a[1] = V#, a[2] = "soffset offen lds"
-                addr = self.vsharp(a[1]) + self.val(a[2].split()[0]) + self.val(a[0]).astype(np.uint64)
-                data = self.mem.load32(addr)
+                # LDS DMA: a[0] = voffset, a[1] = V#, a[2] = "soffset offen lds"; raw buffer range check
+                # on the VGPR offset as for VGPR loads (out of range: zero written to LDS)
+                voff = np.asarray(self.val(a[0]), np.uint64)
+                addr = self.vsharp(a[1]) + self.val(a[2].split()[0]) + voff
+                nrec = int(self.s[int(re.match(r"s\[(\d+):", a[1]).group(1)) + 2])
+                inb = voff < np.uint64(nrec)
+                data = np.where(inb, self.mem.load32(np.where(inb, addr, np.uint64(0))), np.uint32(0)).astype(np.uint32)
                 dst = self.m0 + 4 * np.arange(64)
                 idx = dst[:, None] + np.arange(4)[None, :]
                 self.vm.append((("lds", idx.reshape(-1)), data.astype("<u4").view(np.uint8)))  # lands at retire
