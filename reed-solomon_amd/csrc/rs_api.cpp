@@ -883,14 +883,26 @@ static CsHost cs16_host(const std::vector<uint16_t>& pos, const std::vector<int3
                 uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * NBT;
                 for (int nb = 0; nb < 4; ++nb) rt[4 * cl + nb] = kCs16tOff[(4 * cl + nb) * 16 + ((z >> (4 * nb)) & 15u)];
             }
+    // zero nibbles cost no jump: an entry naming the empty block (p, 0) is replaced by entry p + 1, so the
+    // previous block jumps straight to block p + 1 (whose tail reads entry p + 2); the last position
+    // keeps its block, the one that returns. Padding groups become a single jump.
+    for (size_t row = 0; row < rec_t.size() / NBT; ++row) {
+        uint32_t* rt = rec_t.data() + row * NBT;
+        for (int p = NBT - 2; p >= 0; --p)
+            if (rt[p] == kCs16tOff[p * 16]) rt[p] = rt[p + 1];
+    }
     uint64_t valu_t = 0;  // the step's own VALU (pair sums, lane, address adds) and its blocks', every step of every tile
     constexpr int NBLK = int(sizeof(kCs16tOff) / sizeof(kCs16tOff[0]));
-    std::unordered_map<uint32_t, uint32_t> off_valu;
-    for (int b = 0; b < NBLK; ++b) off_valu[kCs16tOff[b]] = kCs16tValu[b];
+    std::unordered_map<uint32_t, int> off_block;  // code offset -> block index (4c + n) * 16 + v
+    for (int b = 0; b < NBLK; ++b) off_block[kCs16tOff[b]] = b;
     for (int t = 0; t < h.ntiles_t; ++t)
         for (int g = 0; g < ng; ++g) {
             valu_t += uint64_t(kValu_cs16t);
-            for (int p = 0; p < NBT; ++p) valu_t += off_valu[rec_t[(size_t(t) * size_t(ng + 2) + size_t(g)) * NBT + size_t(p)]];
+            const uint32_t* rt = rec_t.data() + (size_t(t) * size_t(ng + 2) + size_t(g)) * NBT;
+            for (int b = off_block[rt[0]];; b = off_block[rt[b / 16 + 1]]) {  // the chain the step runs
+                valu_t += kCs16tValu[b];
+                if (b / 16 == NBT - 1) break;
+            }
         }
     h.rec_t = std::move(rec_t);
     h.valu_t = valu_t;

@@ -104,9 +104,11 @@ def test_cs16_plan_model_gives_the_syndromes(kind, k, r, t):
 
 
 def _model_syndromes_t(d, dt, X, nb):
-    """k_cs16t's arithmetic on CPU: the record entry p = 4c + n of a (tile, group) names block (c', n', v)
-    through the block table; that block XORs f_((t - 4n' - dd) mod 16) for the set bits dd of v into
-    accumulator t of local coset c' (gen_asm.py cs16t); the finish as k_cs16's."""
+    """k_cs16t's arithmetic on CPU: a step runs the chain of blocks its record names -- entry 0's block
+    first, then after block (position q) the block entry q + 1 names, until the last position's -- and
+    block (c, n, v) at position 4c + n XORs f_((t - 4n - dd) mod 16) for the set bits dd of v into
+    accumulator t of local coset c (gen_asm.py cs16t; zero nibbles are skipped by the record); the finish
+    as k_cs16's."""
     exp, log = gf_tables()
     cw, rec, fin, fin_off = dt["cw"], dt["rec"], dt["fin"], dt["fin_off"]
     where = {int(o): divmod(b, 16) for b, o in enumerate(dt["blocks"])}  # offset -> (p, v)
@@ -118,9 +120,7 @@ def _model_syndromes_t(d, dt, X, nb):
         acc = np.zeros((cw, 16, W), np.int64)
         for g in range(groups.shape[0]):
             f = np.array([X[s] if s >= 0 else np.zeros(W, np.int64) for s in groups[g]])
-            for p in range(4 * cw):
-                pb, v = where[int(rec[tile, g, p])]
-                assert pb == p  # every entry names a block of its own position: the chain stays in order
+            for p, v in _chain(rec[tile, g], where, 4 * cw):
                 c, n = divmod(p, 4)
                 for t in range(16):
                     for dd in range(4):
@@ -139,8 +139,21 @@ def _model_syndromes_t(d, dt, X, nb):
                 S[j] = v
     for tile in range(nt):  # the padding records (groups past the last, the two prefetched) are valid too
         for g in range(groups.shape[0], rec.shape[1]):
-            assert all(where[int(rec[tile, g, p])][0] == p for p in range(4 * cw))
+            assert all(v == 0 for _, v in _chain(rec[tile, g], where, 4 * cw))
     return S
+
+
+def _chain(row, where, nb):
+    """[(position, v)] of the blocks a step runs for record row: positions strictly increase and end at
+    the last one (the block that returns)."""
+    out, p = [], -1
+    while True:
+        q, v = where[int(row[p + 1])]
+        assert q > p, (q, p)
+        out.append((q, v))
+        if q == nb - 1:
+            return out
+        p = q
 
 
 @pytest.mark.parametrize("kind,k,r,t", [CASES[0], CASES[1], ("dec", 60, 40, 40), ("dec_bench", 512, 128, 128)])
