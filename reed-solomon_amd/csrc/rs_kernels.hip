@@ -826,9 +826,15 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
 // SIMD to cover each wave's jumps and loads (the lane's column is recomputed per step from its id). The whole group loop is one asm statement: between steps, scalar
 // and vector loads are still filling the record, slot-offset and input registers, which
 // compiler-visible code must never copy. Same block layout and finish as k_cs16.
+#if RS_CS16T_R2
 static_assert(kCs16tCw == 4 && kCs16tF == 0 && kCs16tR == 16 && kCs16tAcc == 32, "k_cs16t's register operands");
+#define RS_CS16T_WAVES 5
+#else  // raw inputs only: 16 inputs + 64 accumulators = v[0:79], 6 waves per SIMD
+static_assert(kCs16tCw == 4 && kCs16tF == 0 && kCs16tAcc == 16, "k_cs16t's register operands");
+#define RS_CS16T_WAVES 6
+#endif
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_cs16t(Cs16Args a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_CS16T_WAVES))) k_cs16t(Cs16Args a) {
     int tile;
     int64_t local;
     uint32_t col;
@@ -844,11 +850,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k
     u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     asm volatile(
 #include "gen/m8_idx_asm_cs16t_kernel.inc"
+#if RS_CS16T_R2
         : "+{v[32:47]}"(a0), "+{v[48:63]}"(a1), "+{v[64:79]}"(a2), "+{v[80:95]}"(a3)
+#else
+        : "+{v[16:31]}"(a0), "+{v[32:47]}"(a1), "+{v[48:63]}"(a2), "+{v[64:79]}"(a3)
+#endif
         : [g0] "s"(goffs), [g2] "s"(goffs + 32), [r0] "s"(rec), [ng] "s"(a.ngroups), [rsrc] "s"(rsrc),
           [colbase] "s"(colbase)
-        : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16",
-          "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31",
+        : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+#if RS_CS16T_R2
+          "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31",
+#endif
           "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55",
           "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87",
           "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "scc", "memory");
