@@ -826,9 +826,12 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
 // SIMD to cover each wave's jumps and loads (the lane's column is recomputed per step from its id). The whole group loop is one asm statement: between steps, scalar
 // and vector loads are still filling the record, slot-offset and input registers, which
 // compiler-visible code must never copy. Same block layout and finish as k_cs16.
-#if RS_CS16T_R2
-static_assert(kCs16tCw == 4 && kCs16tF == 0 && kCs16tR == 16 && kCs16tAcc == 32, "k_cs16t's register operands");
+#if RS_CS16T_R2 && RS_CS16T_CW == 4
+static_assert(kCs16tF == 0 && kCs16tR == 16 && kCs16tAcc == 32, "k_cs16t's register operands");
 #define RS_CS16T_WAVES 5
+#elif RS_CS16T_R2 && RS_CS16T_CW == 3  // inputs + pair sums + 48 accumulators = v[0:79], 6 waves
+static_assert(kCs16tF == 0 && kCs16tR == 16 && kCs16tAcc == 32, "k_cs16t's register operands");
+#define RS_CS16T_WAVES 6
 #else  // raw inputs only: 16 inputs + 64 accumulators = v[0:79], 6 waves per SIMD
 static_assert(kCs16tCw == 4 && kCs16tF == 0 && kCs16tAcc == 16, "k_cs16t's register operands");
 #define RS_CS16T_WAVES 6
@@ -842,16 +845,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_CS1
     const int64_t stripe = RS_STRIPE(a.ids, local);
     const uint64_t sbase = uint64_t(reinterpret_cast<uintptr_t>(a.src + stripe * a.src_stripe));
     const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, a.in_bytes, 0x20000u};
-    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * 16;  // [tile][ngroups + 2][16]
-    const uint32_t* goffs = a.goff;                                           // [ngroups + 3][16]
+    const uint32_t* rec = a.rec + size_t(tile) * size_t(a.ngroups + 2) * (4 * kCs16tCw);  // [tile][ngroups + 2][4 cw]
+    const uint32_t* goffs = a.goff;                                                      // [ngroups + 3][16]
     // the wave's byte column (lane 0's); every VGPR is taken inside the loop, so the lanes' columns are
     // formed there from their ids, and again here after it
     const uint32_t colbase = __builtin_amdgcn_readfirstlane(col - (threadIdx.x & 63u) * 4u);
-    u32x16 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    u32x16 a0 = 0, a1 = 0, a2 = 0;
+#if RS_CS16T_CW == 4
+    u32x16 a3 = 0;
+#endif
     asm volatile(
 #include "gen/m8_idx_asm_cs16t_kernel.inc"
-#if RS_CS16T_R2
+#if RS_CS16T_R2 && RS_CS16T_CW == 4
         : "+{v[32:47]}"(a0), "+{v[48:63]}"(a1), "+{v[64:79]}"(a2), "+{v[80:95]}"(a3)
+#elif RS_CS16T_R2
+        : "+{v[32:47]}"(a0), "+{v[48:63]}"(a1), "+{v[64:79]}"(a2)
 #else
         : "+{v[16:31]}"(a0), "+{v[32:47]}"(a1), "+{v[48:63]}"(a2), "+{v[64:79]}"(a3)
 #endif
@@ -869,7 +877,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RS_CS1
     cs16_finish(a, a0, 0, tile, out);
     cs16_finish(a, a1, 1, tile, out);
     cs16_finish(a, a2, 2, tile, out);
+#if RS_CS16T_CW == 4
     cs16_finish(a, a3, 3, tile, out);
+#endif
 }
 
 // m = 16 binary accumulation (k_bs16, gen_asm.py bs16): the syndrome route's encode second stage. Same
