@@ -2136,6 +2136,36 @@ static int batch_plan_m16(rsg_codec_t* c, const bool* er, int slot, hipStream_t 
 // first t syndromes by k_apply_m16_v1 in per-stripe mode. Erased information slots are zeroed first (the
 // syndromes read every slot); garbage in an erased repair slot only shifts that slot's own unknown,
 // which is never written.
+// Nonzero bytes of [p, p + len): an erasure pattern's set entries (a bool is erased when nonzero, as in
+// reed_solomon.c's `if (is_erased[i])`). Vectorises; the 32-bit partial sums cannot overflow.
+static size_t count_nonzero(const uint8_t* p, size_t len) {
+    size_t c = 0;
+    for (size_t i0 = 0; i0 < len; i0 += 4096) {
+        const size_t e = std::min(len, i0 + 4096);
+        uint32_t cc = 0;
+        for (size_t i = i0; i < e; ++i) cc += p[i] != 0;
+        c += cc;
+    }
+    return c;
+}
+
+// 64-bit hash of [p, p + len) (four independent multiply-xor lanes over 8-byte words, then the tail)
+static uint64_t hash_bytes(const uint8_t* p, size_t len) {
+    constexpr uint64_t kM = 0x9E3779B97F4A7C15ull;
+    uint64_t h[4] = {len, kM, ~len, kM ^ len};
+    size_t i = 0;
+    for (; i + 32 <= len; i += 32)
+        for (int l = 0; l < 4; ++l) {
+            uint64_t w;
+            std::memcpy(&w, p + i + 8 * l, 8);
+            h[l] = (h[l] ^ w) * kM;
+            h[l] ^= h[l] >> 29;
+        }
+    uint64_t r = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
+    for (; i < len; ++i) r = (r ^ p[i]) * kM;
+    return r ^ (r >> 31);
+}
+
 static bool ps16_eligible(const rsg_codec_t* c, uint64_t S, int64_t stripe_stride, int64_t symbol_stride,
                           const void* base) {
     const int64_t n = int64_t(c->k) + c->r;
@@ -2176,24 +2206,30 @@ static int ps16_syn_plan(rsg_codec_t* c, int D, hipStream_t st, DevPlan** out) {
     return 0;
 }
 
+// tr: per stripe, t (erasures) and R (erased information slots), counted by rsg_decode_batch
 static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
-                               uint64_t n_stripes, uint64_t S, const bool* is_erased, hipStream_t st) {
+                               uint64_t n_stripes, uint64_t S, const bool* is_erased, const int32_t* tr,
+                               hipStream_t st) {
     const size_t n = size_t(c->k) + c->r;
     std::vector<int32_t> ids;
     std::vector<uint8_t> masks;
     int tmax = 0, rmax = 0;
-    masks.reserve(size_t(n_stripes) * n);
     for (uint64_t s = 0; s < n_stripes; ++s) {
-        const bool* e = is_erased + s * n;
-        const int R = int(std::count(e, e + c->k, true));
+        const int t = tr[2 * s], R = tr[2 * s + 1];
         if (!R) continue;
-        const int t = R + int(std::count(e + c->k, e + n, true));
         tmax = std::max(tmax, t);
         rmax = std::max(rmax, R);
         ids.push_back(int32_t(s));
-        masks.insert(masks.end(), reinterpret_cast<const uint8_t*>(e), reinterpret_cast<const uint8_t*>(e) + n);
     }
     if (ids.empty()) return 0;
+    // the selected stripes' masks: the caller's array itself when every stripe is selected
+    const uint8_t* mask_src = reinterpret_cast<const uint8_t*>(is_erased);
+    if (ids.size() != n_stripes) {
+        masks.resize(ids.size() * n);
+        for (size_t i = 0; i < ids.size(); ++i)
+            std::memcpy(masks.data() + i * n, is_erased + size_t(ids[i]) * n, n);
+        mask_src = masks.data();
+    }
     int rc = scratch_acquire(c, st);
     if (rc) return rc;
     const uint16_t *logt = nullptr, *expt = nullptr;
@@ -2233,7 +2269,7 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
     c->ids_cap = ids_bytes / 4;
     if (rc) return rc;
-    if ((rc = grow(&c->d_masks, c->masks_cap, masks.size()))) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, ids.size() * n))) return rc;
     if ((rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per)))) return rc;
     // two sets of plan buffers: chunk i + 1's plans are built on the side stream while chunk i runs
     const int64_t rec_set = al(chunk * rec_stride * 4);
@@ -2247,7 +2283,7 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     if ((rc = grow(&c->d_goff[0], c->goff_cap[0], size_t(ngo) * 4))) return rc;
     // the host lists must outlive the copies: upload on the caller's stream, then wait once
     HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_masks, mask_src, ids.size() * n, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[0]), ngo, symbol_stride, st));
     HIP_TRY(hipStreamSynchronize(st));
     Ps16Args pa{};
@@ -2358,19 +2394,31 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
     const size_t n = size_t(c->k) + c->r;
     // validate every stripe first (nothing is written when one pattern cannot be restored), then group
-    // the stripes that share a pattern: one plan and one launch (over a stripe-id list) per pattern
-    std::map<std::vector<uint8_t>, std::vector<int32_t>> groups;
+    // the stripes that share a pattern: one plan and one launch (over a stripe-id list) per pattern.
+    // Patterns are keyed by a hash and compared byte for byte; groups keep first-occurrence order.
+    struct Group {
+        const uint8_t* key;
+        std::vector<int32_t> ids;
+    };
+    std::vector<Group> groups;
+    std::unordered_map<uint64_t, std::vector<size_t>> by_hash;
+    std::vector<int32_t> tr(size_t(n_stripes) * 2);  // per stripe: t, R
     for (uint64_t s = 0; s < n_stripes; ++s) {
-        const bool* e = is_erased + s * n;
-        size_t t = 0;
-        bool info = false;
-        for (size_t i = 0; i < n; ++i)
-            if (e[i]) ++t, info |= i < c->k;
+        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
+        const size_t R = count_nonzero(e, c->k), t = R + count_nonzero(e + c->k, c->r);
         if (t > c->r) return RS_ERR_CANNOT_RESTORE;
-        if (!info) continue;  // nothing to restore (erased repair slots are never written)
+        tr[2 * s] = int32_t(t);
+        tr[2 * s + 1] = int32_t(R);
+        if (!R) continue;  // nothing to restore (erased repair slots are never written)
         if (s > uint64_t(INT32_MAX)) return RS_ERR_INVALID;
-        std::vector<uint8_t> key(e, e + n);
-        groups[key].push_back(int32_t(s));
+        std::vector<size_t>& cand = by_hash[hash_bytes(e, n)];
+        size_t g = 0;
+        while (g < cand.size() && std::memcmp(groups[cand[g]].key, e, n)) ++g;
+        if (g == cand.size()) {
+            cand.push_back(groups.size());
+            groups.push_back(Group{e, {}});
+        }
+        groups[cand[g]].ids.push_back(int32_t(s));
     }
     if (groups.empty() || !symbol_size) return 0;
     HIP_TRY(hipSetDevice(c->device));
@@ -2383,12 +2431,12 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     if (c->m > 8 && (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > 1)) &&
         ps16_eligible(c, symbol_size, int64_t(stripe_stride), int64_t(symbol_stride), d_rcv))
         return decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride), int64_t(symbol_stride),
-                                   n_stripes, symbol_size, is_erased, st);
+                                   n_stripes, symbol_size, is_erased, tr.data(), st);
     std::vector<int32_t> ids;
     std::vector<size_t> first;
     for (auto& g : groups) {
         first.push_back(ids.size());
-        ids.insert(ids.end(), g.second.begin(), g.second.end());
+        ids.insert(ids.end(), g.ids.begin(), g.ids.end());
     }
     if (int rc = scratch_acquire(c, st)) return rc;
     if (ids.size() > c->ids_cap) {
@@ -2409,15 +2457,15 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     for (auto& g : groups) {
         std::unique_ptr<bool[]> er(new bool[n]);
         uint16_t t = 0;
-        for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.first[i] != 0));
+        for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.key[i] != 0));
         DevPlan* p = nullptr;
         int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
         if (rc) return rc;
         // a pattern shared by every stripe, in order: no stripe-id list (the GF(2^16) route and the re-encode
         // decode cover only that form)
-        const bool all = g.second.size() == n_stripes && g.second.front() == 0 && g.second.back() == int32_t(n_stripes - 1);
+        const bool all = g.ids.size() == n_stripes && g.ids.front() == 0 && g.ids.back() == int32_t(n_stripes - 1);
         rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
-                      int64_t(symbol_stride), g.second.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
+                      int64_t(symbol_stride), g.ids.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
         if (rc) return rc;
         ++gi;
     }
