@@ -1700,18 +1700,25 @@ __global__ void __launch_bounds__(256) k_plan16_ps(Ps16Args a) {
 // tile), one lane per row p. ld = log prod_{e != p} (X_p + X_e); then the synthetic division of P by
 // (x + X_p) from the top, q_{t-1} = 1, q_{i-1} = cf_i + X_p q_i, emits W[p][i] = q_i / prod for i = t-1 .. 0;
 // the wave packs the 64 rows' index bytes of input i in LDS and stores the 256-byte record.
+// Both products of q_i (by X_p and by 1 / prod) come from one set of per-lane nibble tables in LDS, a
+// dword per entry (low half X_p * v, high half v / prod; lane-contiguous, so conflict-free): four LDS
+// reads and three XORs a step instead of dependent log / exp gathers from L2.
 __global__ void __launch_bounds__(256) k_plan16_ps_rec(Ps16Args a) {
     __shared__ uint32_t buf[4][2][64];
+    __shared__ uint32_t tab[4][64][64];  // [wave][16 * nibble position + nibble value][lane]
+    __shared__ uint16_t cfl[kPs16MaxR + 1];
     constexpr uint32_t N = 65535u;
     const int64_t s = blockIdx.x / a.tblocks;
     const int wave = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
     const int tile = int(blockIdx.x - s * a.tblocks) * 4 + wave;
     const int t = a.kr[2 * s], R = a.kr[2 * s + 1];
+    const uint16_t* cf = a.cf + s * (int64_t(a.r) + 1);
+    for (int i = int(threadIdx.x); i <= t; i += 256) cfl[i] = cf[i];
+    __syncthreads();  // the only block barrier: waves without rows leave after it
     if (tile * 64 >= R) return;
     const int row = tile * 64 + lane;
     const bool live = row < R;
     const uint16_t* ee = a.ee + s * a.r;
-    const uint16_t* cf = a.cf + s * (int64_t(a.r) + 1);
     const uint32_t xp = live ? a.pe[s * a.out_stride + row] : 0u;
     uint32_t ld = 0;
     if (live) {
@@ -1721,23 +1728,42 @@ __global__ void __launch_bounds__(256) k_plan16_ps_rec(Ps16Args a) {
         }
         ld %= N;
     }
-    const uint32_t lxp = a.logt[xp];
+    const uint32_t inv = live ? uint32_t(a.expt[(N - ld) % N]) : 0u;
+    // tables: base_b = X_p alpha^b | (alpha^b / prod) << 16 (both halves times alpha per bit), entry (j, v)
+    // = XOR of base_{4j + bit} over the set bits of v
+    uint32_t* tw = &tab[wave][0][0];
+    uint32_t base = xp | (inv << 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t b4[4];
+#pragma unroll
+        for (int bit = 0; bit < 4; ++bit) {
+            b4[bit] = base;
+            base = ((base << 1) & 0xFFFEFFFEu) ^ (((base >> 15) & 0x10001u) * 0x2Du);
+        }
+        uint32_t e[16];
+        e[0] = 0;
+#pragma unroll
+        for (int v = 1; v < 16; ++v) e[v] = e[v & (v - 1)] ^ b4[__builtin_ctz(v)];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) tw[(16 * j + v) * 64 + lane] = e[v];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t* tl = tw + lane;
     uint32_t* rec = a.rec + s * a.rec_stride + size_t(tile) * size_t(t + 1) * 64;
     uint8_t* lb = reinterpret_cast<uint8_t*>(&buf[wave][0][0]);
     const int slot0 = 4 * (2 * (lane >> 3) + (lane & 1)) + ((lane & 7) >> 1);  // byte of plane 0
     uint32_t q = 1;
     for (int i = t - 1; i >= 0; --i) {
-        uint32_t c = 0, lq = 0;
-        if (live && q) {
-            lq = a.logt[q];
-            c = a.expt[(lq + N - ld) % N];
-        }
+        const uint32_t pr = tl[(q & 15u) * 64] ^ tl[(16 + ((q >> 4) & 15u)) * 64] ^ tl[(32 + ((q >> 8) & 15u)) * 64] ^
+                            tl[(48 + (q >> 12)) * 64];
+        const uint32_t c = pr >> 16;  // q_i / prod
         uint8_t* b = lb + (i & 1) * 256;
 #pragma unroll
         for (int n = 0; n < 4; ++n) b[64 * n + slot0] = uint8_t(16 * n + ((c >> (4 * n)) & 15u));
         __builtin_amdgcn_wave_barrier();
         rec[size_t(i) * 64 + lane] = reinterpret_cast<const uint32_t*>(b)[lane];
-        if (i > 0) q = uint32_t(cf[i]) ^ (q ? uint32_t(a.expt[(lxp + lq) % N]) : 0u);
+        if (i > 0) q = uint32_t(cfl[i]) ^ (pr & 0xFFFFu);
     }
 }
 

@@ -4,7 +4,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-D=gpurun_out/grouping
+D=gpurun_out/${1:-grouping}
 mkdir -p $D
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread \
   -k "decode_batch or golden_batch or edge_empty or drop_in" > $D/tests.log 2>&1
