@@ -630,8 +630,10 @@ struct rsg_codec {
     void *d_ps_rec = nullptr, *d_ps_small = nullptr;  // per-stripe records / lists of decode_batch_m16_ps
     int32_t* d_ps_in = nullptr;                       // its shared input list 0 .. r + 15
     hipStream_t ps_side = nullptr;                    // plan kernels of the next chunk run here
+    hipStream_t ps_synst = nullptr;                   // option m16_ps_overlap: the syndrome passes run here
     hipEvent_t ps_ev_entry = nullptr, ps_ev_zero[2] = {nullptr, nullptr}, ps_ev_plan[2] = {nullptr, nullptr},
-               ps_ev_used[2] = {nullptr, nullptr};
+               ps_ev_used[2] = {nullptr, nullptr}, ps_ev_syn[2] = {nullptr, nullptr};
+    int ps_overlap = 1;  // 1: chunk i + 1's syndrome pass beside chunk i's solve (two syndrome buffers)
     int64_t ps_chunk = 0;   // option m16_ps_chunk: max stripes per chunk (0 = by ps_rec_mib)
     int64_t ps_rec_mib = 1024;  // records per chunk (MiB); larger chunks keep k_cs16 busier (measured 48-1024)
     size_t ps_rec_cap = 0, ps_small_cap = 0;
@@ -682,8 +684,9 @@ struct rsg_codec {
         (void)hipSetDevice(device);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
         if (ps_side) (void)hipStreamSynchronize(ps_side), (void)hipStreamDestroy(ps_side);
+        if (ps_synst) (void)hipStreamSynchronize(ps_synst), (void)hipStreamDestroy(ps_synst);
         for (hipEvent_t e : {ps_ev_entry, ps_ev_zero[0], ps_ev_zero[1], ps_ev_plan[0], ps_ev_plan[1], ps_ev_used[0],
-                             ps_ev_used[1]})
+                             ps_ev_used[1], ps_ev_syn[0], ps_ev_syn[1]})
             if (e) (void)hipEventDestroy(e);
         if (bp16) bp16->d_idx = nullptr;  // d_bp16_rec, freed below
         for (int i = 0; i < 2; ++i) {
@@ -1326,6 +1329,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!std::strcmp(name, "m16_ps")) {  // rsg_decode_batch of GF(2^16) codes: per-stripe route plans
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->m16_ps = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m16_ps_overlap")) {  // its syndrome pass of the next chunk beside this chunk's solve
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->ps_overlap = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m16_ps_chunk")) {  // its stripes per chunk (0 = sized by m16_ps_rec_mib)
@@ -2270,14 +2278,16 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     c->ids_cap = ids_bytes / 4;
     if (rc) return rc;
     if ((rc = grow(&c->d_masks, c->masks_cap, ids.size() * n))) return rc;
-    if ((rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per)))) return rc;
+    const bool ovl = c->ps_overlap && nchunk > 1;
+    if ((rc = grow(&c->d_cs, c->cs_cap, size_t((ovl ? 2 : 1) * chunk * per)))) return rc;
     // two sets of plan buffers: chunk i + 1's plans are built on the side stream while chunk i runs
     const int64_t rec_set = al(chunk * rec_stride * 4);
     if ((rc = grow(&c->d_ps_rec, c->ps_rec_cap, size_t(2 * rec_set)))) return rc;
     if ((rc = grow(&c->d_ps_small, c->ps_small_cap, size_t(2 * small)))) return rc;
     if (!c->ps_side) HIP_TRY(hipStreamCreateWithFlags(&c->ps_side, hipStreamNonBlocking));
+    if (ovl && !c->ps_synst) HIP_TRY(hipStreamCreateWithFlags(&c->ps_synst, hipStreamNonBlocking));
     for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1],
-                          &c->ps_ev_used[0], &c->ps_ev_used[1]})
+                          &c->ps_ev_used[0], &c->ps_ev_used[1], &c->ps_ev_syn[0], &c->ps_ev_syn[1]})
         if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     const int ngo = (cs.ngroups + 3) * 16;
     if ((rc = grow(&c->d_goff[0], c->goff_cap[0], size_t(ngo) * 4))) return rc;
@@ -2329,6 +2339,10 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
     // the side stream starts after the caller's earlier work on st (the plans zero erased slots)
     HIP_TRY(hipEventRecord(c->ps_ev_entry, st));
     HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_entry, 0));
+    // overlap: the syndrome passes on their own stream into two buffers, chunk ci's after chunk ci - 2's solve
+    // has read the same buffer; the solve of chunk ci waits for its syndromes and its records
+    hipStream_t sy = ovl ? c->ps_synst : st;
+    if (ovl) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
     for (int64_t c0 = 0, ci = 0; c0 < nsel; c0 += chunk, ++ci) {
         const int64_t cn = std::min(chunk, nsel - c0);
         const int set = int(ci & 1);
@@ -2348,23 +2362,29 @@ static int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_str
         HIP_TRY(launch_plan16_ps_rec(pa, cn, c->ps_side));  // runs beside this chunk's syndrome pass
         HIP_TRY(hipEventRecord(c->ps_ev_plan[set], c->ps_side));
         // syndromes (after the zeroing: they read every slot), then the apply (after the records)
-        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_zero[set], 0));
-        ca.dst = static_cast<uint8_t*>(c->d_cs);
+        HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_zero[set], 0));
+        if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));
+        uint8_t* csb = static_cast<uint8_t*>(c->d_cs) + (ovl ? set * chunk * per : 0);
+        ca.dst = csb;
         ca.ids = c->d_ids + c0;
         ca.units = cn * ca.nchunks;
         const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(ca.ntiles) * uint64_t(cs.ngroups);
         if (thr) {
-            HIP_TRY(launch_cs16t(ca, st));
+            HIP_TRY(launch_cs16t(ca, sy));
             c->work_valu += uint64_t(ca.units) * uint64_t(ca.colw / 256) * cs.valu_t;
             c->work_salu += steps * kSaluStepCs16t;
         } else {
-            HIP_TRY(launch_cs16(ca, st));
+            HIP_TRY(launch_cs16(ca, sy));
             c->work_valu += steps * kValu_cs16a;
             c->work_salu += steps * kSalu_cs16a;
         }
+        if (ovl) {
+            HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
+            HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+        }
         HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
         V1Args v{};
-        v.src = static_cast<const uint8_t*>(c->d_cs);
+        v.src = csb;
         v.src_stripe = per;
         v.src_sym = int64_t(S);
         v.src_local = 1;

@@ -42,7 +42,9 @@ orig = dev.clone()  # the codewords: erased repair slots stay zero after a decod
 mask = torch.from_numpy(pats).to("cuda")
 old = rs_amd.Codec(k, r)
 old.set_option("m16_ps", 0)
-runs = [("distinct_patterns_ps16_route", codec)]
+serial = rs_amd.Codec(k, r)
+serial.set_option("m16_ps_overlap", 0)
+runs = [("distinct_patterns_ps16_route", codec), ("distinct_patterns_ps16_route_no_overlap", serial)]
 for mib in [int(x) for x in os.environ.get("PS_REC_MIB", "").split(",") if x]:  # chunk-size sweep
     cm = rs_amd.Codec(k, r)
     cm.set_option("m16_ps_rec_mib", mib)

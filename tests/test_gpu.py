@@ -459,6 +459,43 @@ def test_decode_batch_m16_per_stripe_route(k, r, S, n):
     assert np.array_equal(dev.cpu().numpy()[:, :k], got[:, :k])
 
 
+@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("chunk", [1, 3, 7])
+def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
+    """The per-stripe route in several chunks (m16_ps_chunk): double-buffered plans, and with m16_ps_overlap
+    the next chunk's syndrome pass on its own stream into the other syndrome buffer; byte-identical to the
+    one-chunk decode, stripes without erased information (skipped) mixed in."""
+    k, r, S, n = 700, 120, 1024, 17
+    rng = np.random.default_rng(chunk * 10 + overlap)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0xC4)
+    one = rs_amd.Codec(k, r)
+    one.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    pats[2, :] = False
+    pats[2, k:k + 5] = True  # repair erasures only: not restored, not in the chunks
+    host = full.copy()
+    host[pats] = rng.integers(0, 256, (int(pats.sum()), S), dtype=np.uint8)
+    dev.copy_(torch.from_numpy(host))
+    assert one.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    want = dev.cpu().numpy()
+    assert np.array_equal(want[:, :k], full[:, :k])
+    cdc = rs_amd.Codec(k, r)
+    cdc.set_option("m16_ps_chunk", chunk)
+    cdc.set_option("m16_ps_overlap", overlap)
+    for _ in range(2):  # the second call reuses the streams, events and buffers
+        dev.copy_(torch.from_numpy(host))
+        assert cdc.decode_batch(dev, pats) == 0
+        torch.cuda.synchronize()
+        assert cdc.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", cdc.last_kernel
+        assert np.array_equal(dev.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("route", [0, 1])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030)])
