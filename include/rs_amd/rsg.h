@@ -57,6 +57,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m16_ps_chunk" / "m16_ps_rec_mib"  stripes / record MiB per chunk of that path (0 / 1024 defaults)
  *   "m16_ps_overlap" 1 (default) the next chunk's syndrome pass runs on a codec stream beside this chunk's
  *                  solve (two syndrome buffers); 0 both on the caller's stream
+ *   "m16_cs_overlap" 1 the one-pattern syndrome route runs >= 16 stripes in 4 chunks, each chunk's
+ *                  syndromes on that codec stream beside the previous chunk's second stage; 0 serial (default)
  *   "m16_mode"     GF(2^16) dense kernels: 0 hand-scheduled gpr-index kernel for > 32 outputs (default),
  *                  2 the compiled kernel
  *   "m16_plans"    GF(2^16) dense matrices: 0 built on the host, 1 on the device, 2 on the device from 64K

@@ -634,6 +634,9 @@ struct rsg_codec {
     hipEvent_t ps_ev_entry = nullptr, ps_ev_zero[2] = {nullptr, nullptr}, ps_ev_plan[2] = {nullptr, nullptr},
                ps_ev_used[2] = {nullptr, nullptr}, ps_ev_syn[2] = {nullptr, nullptr};
     int ps_overlap = 1;  // 1: chunk i + 1's syndrome pass beside chunk i's solve (two syndrome buffers)
+    // option m16_cs_overlap: the same for the one-pattern syndrome route (run_cs); off by default: C5 in four
+    // overlapped chunks measured 77.5-78.3 GB/s against 80.6-80.7 serial (profiles/r3_cs_overlap_ab.log)
+    int cs_overlap = 0;
     int64_t ps_chunk = 0;   // option m16_ps_chunk: max stripes per chunk (0 = by ps_rec_mib)
     int64_t ps_rec_mib = 1024;  // records per chunk (MiB); larger chunks keep k_cs16 busier (measured 48-1024)
     size_t ps_rec_cap = 0, ps_small_cap = 0;
@@ -1336,6 +1339,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->ps_overlap = int(value);
         return 0;
     }
+    if (!std::strcmp(name, "m16_cs_overlap")) {  // one-pattern syndrome route: syndromes beside the second stage
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->cs_overlap = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "m16_ps_chunk")) {  // its stripes per chunk (0 = sized by m16_ps_rec_mib)
         if (value < 0 || value > 65535) return RS_ERR_INVALID;
         c->ps_chunk = value;
@@ -1381,6 +1389,16 @@ constexpr uint64_t kSaluStepCs16t = uint64_t(kSalu_cs16t) + 3 * (4 * kCs16tCw - 
 static int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                     int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
                     const int32_t* d_ids = nullptr, bool dst_local = false);
+
+// The codec's syndrome stream and its events (the per-stripe route and m16_cs_overlap)
+static int overlap_objects(rsg_codec_t* c) {
+    if (!c->ps_synst) HIP_TRY(hipStreamCreateWithFlags(&c->ps_synst, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_used[0], &c->ps_ev_used[1], &c->ps_ev_syn[0], &c->ps_ev_syn[1]})
+        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return 0;
+}
+
+constexpr int64_t kCsOverlapChunks = 4, kCsOverlapMinStripes = 16;
 
 static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
                   int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
@@ -1439,28 +1457,47 @@ static int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
         a.cw = kCs16tCw;
     }
     const int64_t per = int64_t(cs.D) * int64_t(S);
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
-    if (int rc = grow(&c->d_cs, c->cs_cap, size_t(chunk * per))) return rc;
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
+    // option m16_cs_overlap: at least kCsOverlapChunks chunks, chunk i + 1's syndromes on the codec's
+    // syndrome stream (other buffer) beside chunk i's second stage on st
+    const bool ovl = c->cs_overlap && int64_t(n_stripes) >= kCsOverlapMinStripes;
+    if (ovl) chunk = std::min<int64_t>(chunk, (int64_t(n_stripes) + kCsOverlapChunks - 1) / kCsOverlapChunks);
+    if (int rc = grow(&c->d_cs, c->cs_cap, size_t((ovl ? 2 : 1) * chunk * per))) return rc;
+    hipStream_t sy = st;
+    if (ovl) {
+        if (int rc = overlap_objects(c)) return rc;
+        sy = c->ps_synst;
+        HIP_TRY(hipEventRecord(c->ps_ev_entry, st));  // after the d_goff upload above
+        HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
+    }
     std::string second;
-    for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
+    for (int64_t c0 = 0, ci = 0; c0 < int64_t(n_stripes); c0 += chunk, ++ci) {
         const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
+        const int set = int(ci & 1);
+        uint8_t* csb = static_cast<uint8_t*>(c->d_cs) + (ovl ? set * chunk * per : 0);
+        if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));  // buffer read by chunk ci - 2
         a.src = src + c0 * src_stripe;
-        a.dst = static_cast<uint8_t*>(c->d_cs);
+        a.dst = csb;
         a.dst_stripe = per;
         a.units = cn * a.nchunks;
         if (thr) {
-            HIP_TRY(launch_cs16t(a, st));
+            HIP_TRY(launch_cs16t(a, sy));
             c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
             c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSaluStepCs16t;
         } else {
-            HIP_TRY(launch_cs16(a, st));
+            HIP_TRY(launch_cs16(a, sy));
             const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
             c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
             c->work_salu += steps * kSalu_cs16a;
         }
-        if (int rc = run_plan(c, *p.second, static_cast<uint8_t*>(c->d_cs), per, int64_t(S), dst + c0 * dst_stripe,
-                              dst_stripe, dst_sym, uint64_t(cn), S, st))
+        if (ovl) {
+            HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
+            HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+        }
+        if (int rc = run_plan(c, *p.second, csb, per, int64_t(S), dst + c0 * dst_stripe, dst_stripe, dst_sym,
+                              uint64_t(cn), S, st))
             return rc;
+        if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         second = c->last_kernel;
     }
     c->last_kernel = (thr ? "cs16t+" : "cs16+") + second;

@@ -672,6 +672,46 @@ def test_cs16_threaded_matches_indexed(k, r, S, n):
         assert np.array_equal(outs[1][0][0, k:], want[k:])
 
 
+@pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 37), (300, 64, 3072, 16)])
+def test_cs16_overlapped_chunks_match_serial(k, r, S, n):
+    """m16_cs_overlap = 1 (off by default): the one-pattern syndrome route in four chunks with each chunk's syndromes
+    on the codec's syndrome stream beside the previous chunk's second stage (two syndrome buffers) gives
+    the same repair symbols and restores as the serial route (0, default), for the bench pattern (k_bs16 second
+    stage), a random information pattern and a mixed pattern (dense second stage); twice per codec."""
+    outs = {}
+    for ovl in (1, 0):
+        dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+        rs_amd.fill_info(dev, k, seed=0x0C5)
+        codec = rs_amd.Codec(k, r)
+        codec.set_option("m16_cs_overlap", ovl)
+        codec.set_option("m16_route_min_bytes", 0)
+        res = []
+        for _ in range(2):
+            dev[:, k:] = 0
+            codec.encode(dev)
+            torch.cuda.synchronize()
+            assert codec.last_kernel.startswith(CS_DEFAULT + "+"), codec.last_kernel
+            full = dev.cpu().numpy()
+            res.append(full[:, k:].copy())
+            pats = [rs_amd.bench_pattern(k, r), np.zeros(k + r, bool), np.zeros(k + r, bool)]
+            pats[1][np.random.default_rng(k).choice(k, r, replace=False)] = True
+            pats[2][np.random.default_rng(r).choice(k + r, r, replace=False)] = True
+            for er in pats:
+                dev.copy_(torch.from_numpy(full))
+                dev[:, torch.from_numpy(er)] = 0
+                assert codec.decode(dev, er) == 0
+                torch.cuda.synchronize()
+                got = dev.cpu().numpy()
+                assert np.array_equal(got[:, :k], full[:, :k]), (ovl, codec.last_kernel)
+                res.append(got.copy())
+        outs[ovl] = (full, res)
+    for a, b in zip(outs[1][1], outs[0][1]):
+        assert np.array_equal(a, b)
+    want = outs[1][0][n - 1].copy()
+    assert oracle_encode(k, r, want) == 0
+    assert np.array_equal(outs[1][0][n - 1, k:], want[k:])
+
+
 def test_m16_route_encode_then_decode_on_two_streams():
     """A GF(2^16) route encode on stream A and a route decode on stream B issued back to back with one
     codec: the decode rewrites the codec's slot-offset scratch (d_goff) that A's k_cs16 may still be
