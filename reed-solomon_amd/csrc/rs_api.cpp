@@ -1815,6 +1815,36 @@ static bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
     return true;
 }
 
+// Nonzero bytes of [p, p + len): an erasure pattern's set entries (a bool is erased when nonzero, as in
+// reed_solomon.c's `if (is_erased[i])`). Vectorises; the 32-bit partial sums cannot overflow.
+static size_t count_nonzero(const uint8_t* p, size_t len) {
+    size_t c = 0;
+    for (size_t i0 = 0; i0 < len; i0 += 4096) {
+        const size_t e = std::min(len, i0 + 4096);
+        uint32_t cc = 0;
+        for (size_t i = i0; i < e; ++i) cc += p[i] != 0;
+        c += cc;
+    }
+    return c;
+}
+
+// 64-bit hash of [p, p + len) (four independent multiply-xor lanes over 8-byte words, then the tail)
+static uint64_t hash_bytes(const uint8_t* p, size_t len) {
+    constexpr uint64_t kM = 0x9E3779B97F4A7C15ull;
+    uint64_t h[4] = {len, kM, ~len, kM ^ len};
+    size_t i = 0;
+    for (; i + 32 <= len; i += 32)
+        for (int l = 0; l < 4; ++l) {
+            uint64_t w;
+            std::memcpy(&w, p + i + 8 * l, 8);
+            h[l] = (h[l] ^ w) * kM;
+            h[l] ^= h[l] >> 29;
+        }
+    uint64_t r = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
+    for (; i < len; ++i) r = (r ^ p[i]) * kM;
+    return r ^ (r >> 31);
+}
+
 // rsg_decode_batch for m <= 8 codes with device-built plans: k_plan_m8 turns each selected stripe's
 // erasure mask into its decode matrix (nibble records of the V = 1 kernel), then one V = 1 launch (+
 // the tail kernel) applies every stripe's own plan. Stripes without erased information slots are
@@ -1825,13 +1855,14 @@ static int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stri
     if ((S & 1) || (uintptr_t(base) % 8) || (stripe_stride % 8) || (symbol_stride % 8)) return RS_ERR_INVALID;
     std::vector<int32_t> ids;
     std::vector<uint8_t> masks;
+    masks.reserve(size_t(n_stripes) * n);
     for (uint64_t s = 0; s < n_stripes; ++s) {
-        const bool* e = is_erased + s * n;
-        bool info = false;
-        for (size_t i = 0; i < c->k; ++i) info |= e[i];
-        if (!info) continue;
+        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
+        if (!count_nonzero(e, c->k)) continue;
         ids.push_back(int32_t(s));
-        for (size_t i = 0; i < n; ++i) masks.push_back(e[i] ? 1 : 0);
+        const size_t o = masks.size();
+        masks.resize(o + n);
+        for (size_t i = 0; i < n; ++i) masks[o + i] = e[i] != 0;
     }
     if (ids.empty()) return 0;
     int rc = scratch_acquire(c, st);
@@ -2181,36 +2212,6 @@ static int batch_plan_m16(rsg_codec_t* c, const bool* er, int slot, hipStream_t 
 // first t syndromes by k_apply_m16_v1 in per-stripe mode. Erased information slots are zeroed first (the
 // syndromes read every slot); garbage in an erased repair slot only shifts that slot's own unknown,
 // which is never written.
-// Nonzero bytes of [p, p + len): an erasure pattern's set entries (a bool is erased when nonzero, as in
-// reed_solomon.c's `if (is_erased[i])`). Vectorises; the 32-bit partial sums cannot overflow.
-static size_t count_nonzero(const uint8_t* p, size_t len) {
-    size_t c = 0;
-    for (size_t i0 = 0; i0 < len; i0 += 4096) {
-        const size_t e = std::min(len, i0 + 4096);
-        uint32_t cc = 0;
-        for (size_t i = i0; i < e; ++i) cc += p[i] != 0;
-        c += cc;
-    }
-    return c;
-}
-
-// 64-bit hash of [p, p + len) (four independent multiply-xor lanes over 8-byte words, then the tail)
-static uint64_t hash_bytes(const uint8_t* p, size_t len) {
-    constexpr uint64_t kM = 0x9E3779B97F4A7C15ull;
-    uint64_t h[4] = {len, kM, ~len, kM ^ len};
-    size_t i = 0;
-    for (; i + 32 <= len; i += 32)
-        for (int l = 0; l < 4; ++l) {
-            uint64_t w;
-            std::memcpy(&w, p + i + 8 * l, 8);
-            h[l] = (h[l] ^ w) * kM;
-            h[l] ^= h[l] >> 29;
-        }
-    uint64_t r = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
-    for (; i < len; ++i) r = (r ^ p[i]) * kM;
-    return r ^ (r >> 31);
-}
-
 static bool ps16_eligible(const rsg_codec_t* c, uint64_t S, int64_t stripe_stride, int64_t symbol_stride,
                           const void* base) {
     const int64_t n = int64_t(c->k) + c->r;
