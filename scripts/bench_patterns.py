@@ -16,6 +16,7 @@ import rs_amd  # noqa: E402
 k, r, S = 128, 32, 65536
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 mode = sys.argv[2] if len(sys.argv) > 2 else "t32info"
+only = set(sys.argv[3].split(",")) if len(sys.argv) > 3 else None  # case labels to run (profiling)
 rng = np.random.default_rng(5)
 pats = np.zeros((n, k + r), bool)
 for s in range(n):
@@ -44,6 +45,8 @@ mask = torch.from_numpy(pats).to("cuda")
 
 
 def run(codec, label, reps):
+    if only is not None and label not in only:
+        return
     times = []
     for _ in range(reps):
         dev.masked_fill_(mask[:, :, None], 0)
@@ -63,11 +66,14 @@ run(syn, "device_plans_syndrome", 5)
 sur = rs_amd.Codec(k, r, batch_plans=1)
 sur.set_option("syn_route", 0)
 run(sur, "device_plans_survivor", 5)
-run(rs_amd.Codec(k, r, batch_plans=0), "host_plans", 2)
+if only is None or "host_plans" in only:
+    run(rs_amd.Codec(k, r, batch_plans=0), "host_plans", 2)
 # the same bytes with one shared pattern (t = r information erasures): generic and specialised kernels
 one = np.zeros(k + r, bool)
 one[np.arange(r) * (k // r)] = True
 for label, kw in (("one_pattern_generic", dict(jit=0)), ("one_pattern_xj", dict())):
+    if only is not None and label not in only:
+        continue
     c = rs_amd.Codec(k, r, **kw)
     times = []
     for _ in range(4):
