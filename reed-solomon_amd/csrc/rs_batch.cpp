@@ -1,0 +1,643 @@
+// rs_batch.cpp -- rsg_decode_batch: one erasure pattern per stripe (SURVEY f-2).
+// Stripes sharing a pattern share a plan and a launch; past kHostPlanGroups patterns the decode
+// matrices are built on the device (GF(256): the syndrome route or survivor plans; GF(2^16): the
+// per-stripe syndrome route or one plan rebuilt on the stream per pattern).
+#include "rs_core.hpp"
+
+using namespace rsamd;
+
+namespace rsamd {
+
+// Distinct patterns beyond which rsg_decode_batch builds the decode matrices on the device (the
+// host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
+constexpr size_t kHostPlanGroups = 16;
+
+// Syndrome route eligibility: the r x (k + r) syndrome matrix H[j][i] = X_i^j runs on its bit-plane XOR
+// kernel (built once per codec), which covers whole 2 KiB column blocks only.
+bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
+    const int n = int(c->k) + c->r;
+    if (!c->syn_route || c->syn_failed || !c->xj || c->jit == 0 || c->m > 8 || S % 2048 || !xj_supported(8, n, c->r) ||
+        int64_t(n) * symbol_stride >= (int64_t(1) << 31) || int64_t(c->r) * int64_t(S) >= (int64_t(1) << 31))
+        return false;
+    if (!c->syn) {
+        const Field& F = field();
+        std::vector<uint16_t> H(size_t(c->r) * n);
+        for (int j = 0; j < c->r; ++j)
+            for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(c->positions[i]) * j) % kN];
+        std::vector<int32_t> in(n), out(c->r);
+        for (int i = 0; i < n; ++i) in[size_t(i)] = i;
+        for (int j = 0; j < c->r; ++j) out[size_t(j)] = j;
+        std::unique_ptr<DevPlan> p;
+        if (build_plan(c->device, 8, std::move(H), n, c->r, std::move(in), std::move(out), p, nullptr) || !p ||
+            hipStreamSynchronize(nullptr) != hipSuccess) {
+            c->syn_failed = true;
+            return false;
+        }
+        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj) || !p->xj) {
+            std::fprintf(stderr, "librs_amd: syndrome XOR kernel unavailable; per-stripe survivor plans\n");
+            c->syn_failed = true;
+            return false;
+        }
+        c->syn = std::move(p);
+    }
+    return true;
+}
+
+// Nonzero bytes of [p, p + len): an erasure pattern's set entries (a bool is erased when nonzero, as in
+// reed_solomon.c's `if (is_erased[i])`). Vectorises; the 32-bit partial sums cannot overflow.
+size_t count_nonzero(const uint8_t* p, size_t len) {
+    size_t c = 0;
+    for (size_t i0 = 0; i0 < len; i0 += 4096) {
+        const size_t e = std::min(len, i0 + 4096);
+        uint32_t cc = 0;
+        for (size_t i = i0; i < e; ++i) cc += p[i] != 0;
+        c += cc;
+    }
+    return c;
+}
+
+// 64-bit hash of [p, p + len) (four independent multiply-xor lanes over 8-byte words, then the tail)
+uint64_t hash_bytes(const uint8_t* p, size_t len) {
+    constexpr uint64_t kM = 0x9E3779B97F4A7C15ull;
+    uint64_t h[4] = {len, kM, ~len, kM ^ len};
+    size_t i = 0;
+    for (; i + 32 <= len; i += 32)
+        for (int l = 0; l < 4; ++l) {
+            uint64_t w;
+            std::memcpy(&w, p + i + 8 * l, 8);
+            h[l] = (h[l] ^ w) * kM;
+            h[l] ^= h[l] >> 29;
+        }
+    uint64_t r = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
+    for (; i < len; ++i) r = (r ^ p[i]) * kM;
+    return r ^ (r >> 31);
+}
+
+// rsg_decode_batch for m <= 8 codes with device-built plans: k_plan_m8 turns each selected stripe's
+// erasure mask into its decode matrix (nibble records of the V = 1 kernel), then one V = 1 launch (+
+// the tail kernel) applies every stripe's own plan. Stripes without erased information slots are
+// skipped; the caller has validated every pattern.
+int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                              uint64_t n_stripes, uint64_t S, const bool* is_erased, hipStream_t st) {
+    const size_t n = size_t(c->k) + c->r;
+    if ((S & 1) || (uintptr_t(base) % 8) || (stripe_stride % 8) || (symbol_stride % 8)) return RS_ERR_INVALID;
+    std::vector<int32_t> ids;
+    std::vector<uint8_t> masks;
+    masks.reserve(size_t(n_stripes) * n);
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
+        if (!count_nonzero(e, c->k)) continue;
+        ids.push_back(int32_t(s));
+        const size_t o = masks.size();
+        masks.resize(o + n);
+        for (size_t i = 0; i < n; ++i) masks[o + i] = e[i] != 0;
+    }
+    if (ids.empty()) return 0;
+    int rc = scratch_acquire(c, st);
+    if (rc) return rc;
+    const uint16_t* logt = nullptr;
+    const uint8_t* g8 = nullptr;
+    rc = plan_tables(c->device, &logt, &g8);
+    if (rc) return rc;
+    if (!c->d_elem) {
+        const Field& F = field();
+        std::vector<uint16_t> el(n);
+        for (size_t i = 0; i < n; ++i) el[i] = F.exp[c->positions[i]];
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_elem), el.data(), n * 2))) return rc;
+    }
+    const int64_t nsel = int64_t(ids.size());
+    const int tiles = (std::min<int>(c->k, c->r) + 31) / 32;  // erased information slots <= min(k, r)
+    const int64_t in_stride = int64_t(n) + 16, out_stride = int64_t(tiles) * 32, idx_stride = int64_t(tiles) * n * 64;
+    // plans are built and applied in chunks of stripes: at most 256 MiB of nibble records at a time
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nsel, (int64_t(256) << 20) / (idx_stride * 4)));
+    size_t ids_bytes = c->ids_cap * 4;  // ids_cap counts entries
+    rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
+    c->ids_cap = ids_bytes / 4;
+    if (rc) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, masks.size()))) return rc;
+    if ((rc = grow(&c->d_kr, c->kr_cap, size_t(chunk) * 8))) return rc;
+    if ((rc = grow(&c->d_pin, c->pin_cap, size_t(chunk * in_stride) * 4))) return rc;
+    if ((rc = grow(&c->d_pout, c->pout_cap, size_t(chunk * out_stride) * 4))) return rc;
+    if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(chunk * idx_stride) * 4))) return rc;
+    // the host lists must outlive the copies: upload on the caller's stream, then wait once
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (syn_prepare(c, S, symbol_stride)) {
+        // syndrome route: zero erased information slots + build the t_info x t solves (k_plan_syn_m8),
+        // the r syndromes of every selected stripe into scratch (XOR kernel, dst indexed by the chunk-
+        // local stripe), then the per-stripe solves from the syndromes into the erased information slots
+        const uint16_t* expt = nullptr;
+        if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
+        const int64_t per = int64_t(c->r) * int64_t(S);
+        const int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t(1) << 30) / per));
+        if ((rc = grow(&c->d_syn, c->syn_cap, size_t(sch * per)))) return rc;
+        for (int64_t c0 = 0; c0 < nsel; c0 += sch) {
+            const int64_t cn = std::min(sch, nsel - c0);
+            SynPlanArgs pa{};
+            pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+            pa.elem = c->d_elem;
+            pa.logt = logt;
+            pa.expt = expt;
+            pa.g8 = g8;
+            pa.k = c->k;
+            pa.r = c->r;
+            pa.n = int32_t(n);
+            pa.kr = static_cast<int32_t*>(c->d_kr);
+            pa.pin = static_cast<int32_t*>(c->d_pin);
+            pa.pout = static_cast<int32_t*>(c->d_pout);
+            pa.pidx = static_cast<uint32_t*>(c->d_pidx);
+            pa.in_stride = in_stride;
+            pa.out_stride = out_stride;
+            pa.idx_stride = idx_stride;
+            pa.base = base;
+            pa.stripe_stride = stripe_stride;
+            pa.symbol_stride = symbol_stride;
+            pa.S = int64_t(S);
+            pa.ids = c->d_ids + c0;
+            HIP_TRY(launch_plan_syn_m8(pa, cn, st));
+            uint8_t* syn = static_cast<uint8_t*>(c->d_syn);
+            if ((rc = run_plan(c, *c->syn, base, stripe_stride, symbol_stride, syn, per, int64_t(S), uint64_t(cn), S,
+                               st, c->d_ids + c0, true)))
+                return rc;
+            V1Args v{};
+            v.src = syn;
+            v.src_stripe = 0;  // slots are local * r + j
+            v.src_sym = int64_t(S);
+            v.in_idx = pa.pin;
+            v.dst = base;
+            v.dst_stripe = stripe_stride;
+            v.dst_sym = symbol_stride;
+            v.out_idx = pa.pout;
+            v.ltab = c->d_ltab;
+            v.idx = pa.pidx;
+            v.ids = c->d_ids + c0;
+            v.ps_kr = pa.kr;
+            v.ps_in = in_stride;
+            v.ps_out = out_stride;
+            v.ps_idx = idx_stride;
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+        }
+        c->last_kernel = "syn_xj+apply_m8_v1_ps";
+        return scratch_release(c, st);
+    }
+    for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {
+        const int64_t cn = std::min(chunk, nsel - c0);
+        PlanArgs pa{};
+        pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+        pa.elem = c->d_elem;
+        pa.logt = logt;
+        pa.g8 = g8;
+        pa.k = c->k;
+        pa.r = c->r;
+        pa.n = int32_t(n);
+        pa.kr = static_cast<int32_t*>(c->d_kr);
+        pa.pin = static_cast<int32_t*>(c->d_pin);
+        pa.pout = static_cast<int32_t*>(c->d_pout);
+        pa.pidx = static_cast<uint32_t*>(c->d_pidx);
+        pa.in_stride = in_stride;
+        pa.out_stride = out_stride;
+        pa.idx_stride = idx_stride;
+        HIP_TRY(launch_plan_m8(pa, cn, st));
+        V1Args v{};
+        v.src = base;
+        v.src_stripe = stripe_stride;
+        v.src_sym = symbol_stride;
+        v.in_idx = pa.pin;
+        v.dst = base;
+        v.dst_stripe = stripe_stride;
+        v.dst_sym = symbol_stride;
+        v.out_idx = pa.pout;
+        v.ltab = c->d_ltab;
+        v.idx = pa.pidx;
+        v.ids = c->d_ids + c0;
+        v.ps_kr = pa.kr;
+        v.ps_in = in_stride;
+        v.ps_out = out_stride;
+        v.ps_idx = idx_stride;
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+    }
+    c->last_kernel = "apply_m8_v1_ps";
+    return scratch_release(c, st);
+}
+
+// rsg_decode_batch, GF(2^16) codes past kHostPlanGroups patterns: the codec's one batch plan is rebuilt
+// on the stream for every pattern by k_plan16_sums / k_plan16_fill -- the same evaluation and formats as
+// build_plan_m16_device, so results are identical -- instead of a cached plan per pattern (allocations,
+// synchronous uploads and, past 16 patterns, an eviction that frees device memory). Launches on one
+// stream are ordered, so the plan of the next pattern is written after the previous apply has read it;
+// only the host staging needs a ring (two pinned buffers, each guarded by the event after its copies).
+size_t al16(size_t v) { return (v + 15) & ~size_t(15); }
+
+int batch_plan_m16(rsg_codec_t* c, const bool* er, int slot, hipStream_t st, DevPlan** out) {
+    const Field& F = field();
+    const size_t n = size_t(c->k) + c->r, r = c->r;
+    std::vector<uint16_t> targets, sources;
+    std::vector<int> emit;
+    std::vector<int32_t> in, outs;
+    codec_lists(c->positions, c->k, c->r, er, targets, emit, sources, in, outs);
+    const int K = int(sources.size()), R = int(emit.size()), d = int(targets.size());
+    if (R == 0 || size_t(K) > n || size_t(d) > r) return RS_ERR_INVALID;
+    const size_t o_x = al16(n * 2), o_emit = o_x + al16(r * 2), o_lp = o_emit + al16(r * 4), o_ld = o_lp + al16(n * 4);
+    const size_t dev_bytes = o_ld + al16(r * 4);
+    const size_t o_in = o_lp, o_out = o_in + al16((n + 16) * 4), host_bytes = o_out + al16((r + 64) * 4);
+    const size_t rec_cap = ((r + 63) / 64) * (n + 1) * 256;
+    if (!c->bp16) {
+        auto p = std::make_unique<DevPlan>();
+        p->device = c->device;
+        p->m = 16;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_coef), (r + 64) * n * 2));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_in), (n + 16) * 4));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p->d_out), (r + 64) * 4));
+        if (!c->d_bp16) HIP_TRY(hipMalloc(&c->d_bp16, dev_bytes));
+        if (!c->d_bp16_rec && rec_cap <= (size_t(256) << 20)) HIP_TRY(hipMalloc(&c->d_bp16_rec, rec_cap));
+        for (int i = 0; i < 2; ++i) {
+            if (!c->h_bp16[i])
+                HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_bp16[i]), host_bytes, hipHostMallocDefault));
+            if (!c->bp16_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->bp16_ev[i], hipEventDisableTiming));
+        }
+        c->bp16 = std::move(p);
+    }
+    DevPlan& p = *c->bp16;
+    p.K = K;
+    p.R = R;
+    p.rt = apply_tile_rows(16, R);
+    p.ntiles = (R + p.rt - 1) / p.rt;
+    const size_t coef_bytes = size_t(p.ntiles) * size_t(K) * size_t(p.rt / 2) * 4;
+    const size_t rec_bytes = size_t(p.ntiles) * size_t(K + 1) * 256;
+    const bool records = p.rt == 64 && c->d_bp16_rec && rec_bytes <= (size_t(256) << 20);
+    p.d_idx = records ? static_cast<uint32_t*>(c->d_bp16_rec) : nullptr;
+    p.in_slots = in;
+    p.out_slots = outs;
+    p.out_slots.resize(std::max(size_t(p.ntiles) * p.rt, size_t((R + 31) / 32) * 32), 0);
+    p.uses = 0;
+    // stage the lists (the copies that last used this buffer are complete once its event is)
+    if (c->bp16_rec_pending[slot]) HIP_TRY(hipEventSynchronize(c->bp16_ev[slot]));
+    uint8_t* h = c->h_bp16[slot];
+    uint16_t* hy = reinterpret_cast<uint16_t*>(h);
+    uint16_t* hx = reinterpret_cast<uint16_t*>(h + o_x);
+    int32_t* he = reinterpret_cast<int32_t*>(h + o_emit);
+    int32_t* hin = reinterpret_cast<int32_t*>(h + o_in);
+    int32_t* hout = reinterpret_cast<int32_t*>(h + o_out);
+    for (int q = 0; q < K; ++q) hy[q] = F.exp[sources[size_t(q)]];
+    for (int e = 0; e < d; ++e) hx[e] = F.exp[targets[size_t(e)]];
+    for (int j = 0; j < R; ++j) he[j] = emit[size_t(j)];
+    for (int q = 0; q < K + 16; ++q) hin[q] = q < K ? in[size_t(q)] : 0;
+    for (size_t j = 0; j < p.out_slots.size(); ++j) hout[j] = p.out_slots[j];
+    HIP_TRY(hipMemcpyAsync(c->d_bp16, h, o_lp, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p.d_in, hin, size_t(K + 16) * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p.d_out, hout, p.out_slots.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(c->bp16_ev[slot], st));
+    c->bp16_rec_pending[slot] = true;
+    HIP_TRY(hipMemsetAsync(p.d_coef, 0, coef_bytes, st));
+    if (records) HIP_TRY(hipMemsetAsync(p.d_idx, 0, rec_bytes, st));
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if (int rc = plan_tables(c->device, &logt, &g8, &expt)) return rc;
+    uint8_t* dt = static_cast<uint8_t*>(c->d_bp16);
+    Plan16Args a{};
+    a.src_el = reinterpret_cast<const uint16_t*>(dt);
+    a.tgt_el = reinterpret_cast<const uint16_t*>(dt + o_x);
+    a.emit = reinterpret_cast<const int32_t*>(dt + o_emit);
+    a.logt = logt;
+    a.expt = expt;
+    a.lp = reinterpret_cast<uint32_t*>(dt + o_lp);
+    a.ld = reinterpret_cast<uint32_t*>(dt + o_ld);
+    a.coef = p.d_coef;
+    a.rec = records ? reinterpret_cast<uint8_t*>(p.d_idx) : nullptr;
+    a.K = K;
+    a.d = d;
+    a.R = R;
+    a.rt = p.rt;
+    HIP_TRY(launch_plan_m16(a, st));
+    *out = &p;
+    return 0;
+}
+
+// rsg_decode_batch, GF(2^16) codes with per-stripe patterns: the reference's decode split
+// (reed_solomon.c:527-549) into its pattern-independent part -- the syndromes S_j (j < D, D = the largest
+// t of the batch) of all k + r slots of every stripe, one k_cs16 pass with a fixed plan (cached per D) --
+// and the per-pattern part: each stripe's t_info x t solve W (k_plan16_ps / k_plan16_ps_rec build it on
+// the device from the stripe's mask, straight into k_apply_m16_v1 records), applied to that stripe's
+// first t syndromes by k_apply_m16_v1 in per-stripe mode. Erased information slots are zeroed first (the
+// syndromes read every slot); garbage in an erased repair slot only shifts that slot's own unknown,
+// which is never written.
+bool ps16_eligible(const rsg_codec_t* c, uint64_t S, int64_t stripe_stride, int64_t symbol_stride,
+                   const void* base) {
+    const int64_t n = int64_t(c->k) + c->r;
+    return c->m > 8 && c->m16_ps && c->r <= kPs16MaxR && S % 1024 == 0 && int64_t(S) < (int64_t(1) << 31) &&
+           (n - 1) * symbol_stride + int64_t(S) < (int64_t(1) << 31) && int64_t(c->r) * int64_t(S) < (int64_t(1) << 31) &&
+           (stripe_stride % 16) == 0 && (symbol_stride % 16) == 0 && (uintptr_t(base) % 16) == 0 &&
+           symbol_stride >= int64_t(S);
+}
+
+int ps16_syn_plan(rsg_codec_t* c, int D, hipStream_t st, DevPlan** out) {
+    auto it = c->ps_syn.find(D);
+    if (it == c->ps_syn.end()) {
+        if (c->ps_syn.size() >= 4) {  // small LRU: batches usually share a few D values
+            const int old = c->ps_syn_lru.front();
+            c->ps_syn_lru.erase(c->ps_syn_lru.begin());
+            auto o = c->ps_syn.find(old);
+            if (o != c->ps_syn.end()) {
+                o->second->guard_before_release(st);
+                c->ps_syn.erase(o);
+            }
+        }
+        const int n = int(c->k) + c->r;
+        std::vector<int32_t> all(static_cast<size_t>(n));
+        for (int i = 0; i < n; ++i) all[size_t(i)] = i;
+        auto p = std::make_unique<DevPlan>();
+        p->device = c->device;
+        p->m = 16;
+        p->K = n;
+        p->R = D;
+        p->in_slots = all;
+        if (int rc = build_cs16(*p, c->positions, all, D, st)) return rc;
+        it = c->ps_syn.emplace(D, std::move(p)).first;
+    } else {
+        c->ps_syn_lru.erase(std::find(c->ps_syn_lru.begin(), c->ps_syn_lru.end(), D));
+    }
+    c->ps_syn_lru.push_back(D);
+    *out = it->second.get();
+    return 0;
+}
+
+// tr: per stripe, t (erasures) and R (erased information slots), counted by rsg_decode_batch
+int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                        uint64_t n_stripes, uint64_t S, const bool* is_erased, const int32_t* tr,
+                        hipStream_t st) {
+    const size_t n = size_t(c->k) + c->r;
+    std::vector<int32_t> ids;
+    std::vector<uint8_t> masks;
+    int tmax = 0, rmax = 0;
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const int t = tr[2 * s], R = tr[2 * s + 1];
+        if (!R) continue;
+        tmax = std::max(tmax, t);
+        rmax = std::max(rmax, R);
+        ids.push_back(int32_t(s));
+    }
+    if (ids.empty()) return 0;
+    // the selected stripes' masks: the caller's array itself when every stripe is selected
+    const uint8_t* mask_src = reinterpret_cast<const uint8_t*>(is_erased);
+    if (ids.size() != n_stripes) {
+        masks.resize(ids.size() * n);
+        for (size_t i = 0; i < ids.size(); ++i)
+            std::memcpy(masks.data() + i * n, is_erased + size_t(ids[i]) * n, n);
+        mask_src = masks.data();
+    }
+    int rc = scratch_acquire(c, st);
+    if (rc) return rc;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
+    if (!c->d_elem) {
+        const Field& F = field();
+        std::vector<uint16_t> el(n);
+        for (size_t i = 0; i < n; ++i) el[i] = F.exp[c->positions[i]];
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_elem), el.data(), n * 2))) return rc;
+    }
+    // D: the batch's largest t rounded up to a multiple of 32 (fewer distinct cached syndrome plans)
+    const int D = std::min<int>(c->r, (tmax + 31) / 32 * 32);
+    DevPlan* syn = nullptr;
+    if ((rc = ps16_syn_plan(c, D, st, &syn))) return rc;
+    if ((rc = syn->order_after_build(st))) return rc;
+    const DevPlan::Cs& cs = *syn->cs;
+    const int64_t nsel = int64_t(ids.size());
+    const int tiles = (rmax + 63) / 64;
+    const int64_t out_stride = int64_t(tiles) * 64;
+    const int64_t rec_stride = int64_t(tiles) * (D + 1) * 64;  // dwords
+    const int64_t per = int64_t(D) * int64_t(S);                // syndrome bytes per stripe
+    // chunks of stripes, at most m16_ps_rec_mib of records each: larger chunks measured faster (C5, 256
+    // stripes: 48 MiB 0.260, 160 MiB 0.204, 1024 MiB 0.184 ms a stripe; option m16_ps_chunk caps it)
+    int64_t chunk = std::max<int64_t>(
+        1, std::min<int64_t>({nsel, (int64_t(1) << 30) / per, (int64_t(c->ps_rec_mib) << 20) / (rec_stride * 4), 65535}));
+    if (c->ps_chunk > 0) chunk = std::min<int64_t>(chunk, c->ps_chunk);
+    const int64_t nchunk = (nsel + chunk - 1) / chunk;
+    chunk = (nsel + nchunk - 1) / nchunk;  // even chunks (no small tail chunk)
+    // small per-stripe arrays in one buffer: kr [2] i32, ee [r] u16, pe [out_stride] u16, pout
+    // [out_stride] i32, cf [r + 1] u16 (each part 256-byte aligned)
+    auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+    const int64_t o_kr = 0, o_ee = al(chunk * 8), o_pe = o_ee + al(chunk * c->r * 2),
+                  o_po = o_pe + al(chunk * out_stride * 2), o_cf = o_po + al(chunk * out_stride * 4),
+                  small = o_cf + al(chunk * (int64_t(c->r) + 1) * 2);
+    size_t ids_bytes = c->ids_cap * 4;
+    rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
+    c->ids_cap = ids_bytes / 4;
+    if (rc) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, ids.size() * n))) return rc;
+    const bool ovl = c->ps_overlap && nchunk > 1;
+    if ((rc = grow(&c->d_cs, c->cs_cap, size_t((ovl ? 2 : 1) * chunk * per)))) return rc;
+    // two sets of plan buffers: chunk i + 1's plans are built on the side stream while chunk i runs
+    const int64_t rec_set = al(chunk * rec_stride * 4);
+    if ((rc = grow(&c->d_ps_rec, c->ps_rec_cap, size_t(2 * rec_set)))) return rc;
+    if ((rc = grow(&c->d_ps_small, c->ps_small_cap, size_t(2 * small)))) return rc;
+    if (!c->ps_side) HIP_TRY(hipStreamCreateWithFlags(&c->ps_side, hipStreamNonBlocking));
+    if (ovl && !c->ps_synst) HIP_TRY(hipStreamCreateWithFlags(&c->ps_synst, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1],
+                          &c->ps_ev_used[0], &c->ps_ev_used[1], &c->ps_ev_syn[0], &c->ps_ev_syn[1]})
+        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    const int ngo = (cs.ngroups + 3) * 16;
+    if ((rc = grow(&c->d_goff[0], c->goff_cap[0], size_t(ngo) * 4))) return rc;
+    // the host lists must outlive the copies: upload on the caller's stream, then wait once
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_masks, mask_src, ids.size() * n, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[0]), ngo, symbol_stride, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    Ps16Args pa{};
+    pa.elem = c->d_elem;
+    pa.logt = logt;
+    pa.expt = expt;
+    pa.k = c->k;
+    pa.r = c->r;
+    pa.n = int32_t(n);
+    pa.out_stride = out_stride;
+    pa.rec_stride = rec_stride;
+    pa.tblocks = (tiles + 3) / 4;
+    pa.base = base;
+    pa.stripe_stride = stripe_stride;
+    pa.symbol_stride = symbol_stride;
+    pa.S = int64_t(S);
+    Cs16Args ca{};
+    ca.src = base;
+    ca.src_stripe = stripe_stride;
+    ca.src_sym = symbol_stride;
+    ca.goff = static_cast<const uint32_t*>(c->d_goff[0]);
+    ca.in_bytes = uint32_t(cs.max_slot * symbol_stride + int64_t(S));
+    const bool thr = c->m16_cs_thread && cs.rec_t;
+    ca.rec = thr ? cs.rec_t : cs.rec;
+    ca.fin = thr ? cs.fin_t : cs.fin;
+    ca.fin_off = thr ? cs.fin_off_t : cs.fin_off;
+    ca.fin_stride = thr ? cs.fin_stride_t : cs.fin_stride;
+    ca.cw = thr ? kCs16tCw : 4;
+    ca.dst_stripe = per;
+    ca.dst_sym = int64_t(S);
+    ca.logt = logt;
+    ca.expt = expt;
+    for (int q = 0; q < 16; ++q) ca.nblog[q] = cs.nblog[q];
+    ca.ngroups = cs.ngroups;
+    ca.ntiles = thr ? cs.ntiles_t : cs.ntiles;
+    ca.colw = c->m16_cs_col == 1024 ? 1024 : 256;
+    ca.nchunks = int64_t(S) / ca.colw;
+    if (!c->d_ps_in) {  // the apply's shared input list: input j = syndrome j of the stripe (j < r, + padding)
+        std::vector<int32_t> in_list(size_t(c->r) + 16);
+        for (size_t j = 0; j < in_list.size(); ++j) in_list[j] = int32_t(j);
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_ps_in), in_list.data(), in_list.size() * 4))) return rc;
+    }
+    // the side stream starts after the caller's earlier work on st (the plans zero erased slots)
+    HIP_TRY(hipEventRecord(c->ps_ev_entry, st));
+    HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_entry, 0));
+    // overlap: the syndrome passes on their own stream into two buffers, chunk ci's after chunk ci - 2's solve
+    // has read the same buffer; the solve of chunk ci waits for its syndromes and its records
+    hipStream_t sy = ovl ? c->ps_synst : st;
+    if (ovl) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
+    for (int64_t c0 = 0, ci = 0; c0 < nsel; c0 += chunk, ++ci) {
+        const int64_t cn = std::min(chunk, nsel - c0);
+        const int set = int(ci & 1);
+        uint8_t* sm = static_cast<uint8_t*>(c->d_ps_small) + set * small;
+        pa.kr = reinterpret_cast<int32_t*>(sm + o_kr);
+        pa.ee = reinterpret_cast<uint16_t*>(sm + o_ee);
+        pa.pe = reinterpret_cast<uint16_t*>(sm + o_pe);
+        pa.pout = reinterpret_cast<int32_t*>(sm + o_po);
+        pa.cf = reinterpret_cast<uint16_t*>(sm + o_cf);
+        pa.rec = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_ps_rec) + set * rec_set);
+        pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
+        pa.ids = c->d_ids + c0;
+        // plans of this chunk on the side stream, once chunk ci - 2 (same buffer set) has been applied
+        if (ci >= 2) HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_used[set], 0));
+        HIP_TRY(launch_plan16_ps(pa, cn, c->ps_side));
+        HIP_TRY(hipEventRecord(c->ps_ev_zero[set], c->ps_side));
+        HIP_TRY(launch_plan16_ps_rec(pa, cn, c->ps_side));  // runs beside this chunk's syndrome pass
+        HIP_TRY(hipEventRecord(c->ps_ev_plan[set], c->ps_side));
+        // syndromes (after the zeroing: they read every slot), then the apply (after the records)
+        HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_zero[set], 0));
+        if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));
+        uint8_t* csb = static_cast<uint8_t*>(c->d_cs) + (ovl ? set * chunk * per : 0);
+        ca.dst = csb;
+        ca.ids = c->d_ids + c0;
+        ca.units = cn * ca.nchunks;
+        const uint64_t steps = uint64_t(ca.units) * uint64_t(ca.colw / 256) * uint64_t(ca.ntiles) * uint64_t(cs.ngroups);
+        if (thr) {
+            HIP_TRY(launch_cs16t(ca, sy));
+            c->work_valu += uint64_t(ca.units) * uint64_t(ca.colw / 256) * cs.valu_t;
+            c->work_salu += steps * kSaluStepCs16t;
+        } else {
+            HIP_TRY(launch_cs16(ca, sy));
+            c->work_valu += steps * kValu_cs16a;
+            c->work_salu += steps * kSalu_cs16a;
+        }
+        if (ovl) {
+            HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
+            HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+        }
+        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
+        V1Args v{};
+        v.src = csb;
+        v.src_stripe = per;
+        v.src_sym = int64_t(S);
+        v.src_local = 1;
+        v.in_idx = c->d_ps_in;
+        v.dst = base;
+        v.dst_stripe = stripe_stride;
+        v.dst_sym = symbol_stride;
+        v.out_idx = pa.pout;
+        v.idx = pa.rec;
+        v.ids = c->d_ids + c0;
+        v.ps_kr = pa.kr;
+        v.ps_in = 0;
+        v.ps_out = out_stride;
+        v.ps_idx = rec_stride;
+        v.K = D;
+        v.R = rmax;
+        HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
+        HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
+    }
+    if ((rc = syn->note_use(st))) return rc;
+    c->last_kernel = thr ? "ps16+cs16t+apply_m16_v1_ps" : "ps16+cs16+apply_m16_v1_ps";
+    return scratch_release(c, st);
+}
+
+}  // namespace rsamd
+
+extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
+                                uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
+    if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
+    const size_t n = size_t(c->k) + c->r;
+    // validate every stripe first (nothing is written when one pattern cannot be restored), then group
+    // the stripes that share a pattern: one plan and one launch (over a stripe-id list) per pattern.
+    // Patterns are keyed by a hash and compared byte for byte; groups keep first-occurrence order.
+    struct Group {
+        const uint8_t* key;
+        std::vector<int32_t> ids;
+    };
+    std::vector<Group> groups;
+    std::unordered_map<uint64_t, std::vector<size_t>> by_hash;
+    std::vector<int32_t> tr(size_t(n_stripes) * 2);  // per stripe: t, R
+    for (uint64_t s = 0; s < n_stripes; ++s) {
+        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
+        const size_t R = count_nonzero(e, c->k), t = R + count_nonzero(e + c->k, c->r);
+        if (t > c->r) return RS_ERR_CANNOT_RESTORE;
+        tr[2 * s] = int32_t(t);
+        tr[2 * s + 1] = int32_t(R);
+        if (!R) continue;  // nothing to restore (erased repair slots are never written)
+        if (s > uint64_t(INT32_MAX)) return RS_ERR_INVALID;
+        std::vector<size_t>& cand = by_hash[hash_bytes(e, n)];
+        size_t g = 0;
+        while (g < cand.size() && std::memcmp(groups[cand[g]].key, e, n)) ++g;
+        if (g == cand.size()) {
+            cand.push_back(groups.size());
+            groups.push_back(Group{e, {}});
+        }
+        groups[cand[g]].ids.push_back(int32_t(s));
+    }
+    if (groups.empty() || !symbol_size) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (c->m <= 8 && n <= 256 &&
+        (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups)))
+        return decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
+                                         int64_t(symbol_stride), n_stripes, symbol_size, is_erased, st);
+    // GF(2^16): more than one pattern -> per-stripe plans on the syndrome route (one shared syndrome pass)
+    if (c->m > 8 && (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > 1)) &&
+        ps16_eligible(c, symbol_size, int64_t(stripe_stride), int64_t(symbol_stride), d_rcv))
+        return decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride), int64_t(symbol_stride),
+                                   n_stripes, symbol_size, is_erased, tr.data(), st);
+    std::vector<int32_t> ids;
+    std::vector<size_t> first;
+    for (auto& g : groups) {
+        first.push_back(ids.size());
+        ids.insert(ids.end(), g.ids.begin(), g.ids.end());
+    }
+    if (int rc = scratch_acquire(c, st)) return rc;
+    if (ids.size() > c->ids_cap) {
+        if (c->d_ids) (void)hipFree(c->d_ids);
+        c->d_ids = nullptr;
+        c->ids_cap = 0;
+        HIP_TRY(hipMalloc(&c->d_ids, ids.size() * 4));
+        c->ids_cap = ids.size();
+    }
+    // the list must stay valid until the launches have read it: upload on the caller's stream
+    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint8_t* base = static_cast<uint8_t*>(d_rcv);
+    // GF(2^16) codes with many patterns: one plan rebuilt on the stream per pattern (batch_plan_m16)
+    const bool stream_plans = c->m > 8 && c->m16_plans != 0 &&
+                              (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups));
+    size_t gi = 0;
+    for (auto& g : groups) {
+        std::unique_ptr<bool[]> er(new bool[n]);
+        uint16_t t = 0;
+        for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.key[i] != 0));
+        DevPlan* p = nullptr;
+        int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
+        if (rc) return rc;
+        // a pattern shared by every stripe, in order: no stripe-id list (the GF(2^16) route and the re-encode
+        // decode cover only that form)
+        const bool all = g.ids.size() == n_stripes && g.ids.front() == 0 && g.ids.back() == int32_t(n_stripes - 1);
+        rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
+                      int64_t(symbol_stride), g.ids.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
+        if (rc) return rc;
+        ++gi;
+    }
+    return scratch_release(c, st);
+}
