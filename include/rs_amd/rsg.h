@@ -153,10 +153,33 @@ int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, in
  * and the block table [nblocks] (offset of block (c, n, v) at (4c + n) * 16 + v). Host only. */
 int rsg_route_dump_t(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint32_t* rec,
                      int32_t* fin, int32_t* fin_off, uint32_t* blocks);
-/* Symbol data from symbol_create of >= 16 KiB (page-aligned whole pages): 1 when symbol_create page-locked
- * and mapped it (hipHostRegister, until symbol_destroy), 0 when that registration was refused (the symbol
- * then goes by the staging path); -1 for any other pointer. */
+/* Symbol data from symbol_create of >= 16 KiB (page-aligned whole pages of its own): 1 when it is page-locked
+ * and mapped (hipHostRegister, done by the first rs_* call that moves it; symbol_create itself makes no HIP
+ * call), 0 when it is not (not used yet, or the registration was refused: such symbols go by the staging
+ * path); -1 for any other pointer. */
 int rsg_symbol_registered(const void* data);
+/* Counters of the library-allocated symbol pages since process start (rs_hostmem.cpp). A block whose
+ * registration cannot be undone (hipHostUnregister fails, or the runtime still reports the range) is
+ * "stuck": it stays mapped, out of circulation and counted against the pinned cap. */
+typedef struct rsg_symbol_stats {
+    uint64_t live;                /* symbols in registrable pages, not destroyed */
+    uint64_t live_registered;     /* of those, page-locked and mapped */
+    uint64_t idle_blocks;         /* destroyed blocks parked in the idle pool (registration kept) */
+    uint64_t idle_bytes;
+    uint64_t idle_reuses;         /* symbol_create calls served from the idle pool */
+    uint64_t registrations;       /* successful hipHostRegister calls */
+    uint64_t register_failures;   /* refused by the runtime, range already known, or no device pointer */
+    uint64_t unregistrations;     /* hipHostUnregister succeeded and the runtime forgot the range */
+    uint64_t unregister_failures;
+    uint64_t retired_blocks;      /* memory returned to the OS, address range kept reserved (never reused) */
+    uint64_t stuck_blocks;
+    uint64_t stuck_bytes;
+    uint64_t pinned_bytes;        /* page-locked bytes of arenas, slabs and registered symbols */
+} rsg_symbol_stats_t;
+int rsg_symbol_stats(rsg_symbol_stats_t* out);
+/* Idle-pool cap in bytes (default 1 GiB, RS_AMD_SYM_POOL_MB); bytes < 0 only queries. Returns the previous
+ * cap. Blocks destroyed past the cap are unregistered and retired. */
+int64_t rsg_symbol_pool_cap(int64_t bytes);
 /* The k_bs16 second stage of the GF(2^16) route for the encode (is_erased NULL) or decode matrix, when it
  * applies (encode: the repair cosets; decode: an erased set closed under x -> x^(2^d), d < 16): records
  * [ntiles][ngroups + 2][4][64] bytes, finish lists [ntiles][fin_stride] (local coset | rotation << 4 |

@@ -593,9 +593,9 @@ extern "C" int rsg_coding_matrix(uint16_t k, uint16_t r, const bool* is_erased, 
     codec_matrix(pos, k, r, is_erased, M, in, outs);
     if (rows) *rows = uint32_t(outs.size());
     if (cols) *cols = uint32_t(in.size());
-    if (matrix) std::memcpy(matrix, M.data(), M.size() * 2);
-    if (in_slots) std::memcpy(in_slots, in.data(), in.size() * 4);
-    if (out_slots) std::memcpy(out_slots, outs.data(), outs.size() * 4);
+    copy_out(matrix, M);
+    copy_out(in_slots, in);
+    copy_out(out_slots, outs);
     return 0;
 }
 

@@ -49,6 +49,14 @@ inline int hip_fail(hipError_t e, const char* what) {
 
 inline size_t pad16(size_t s) { return (s + 15) & ~size_t(15); }
 
+// the first n elements (all by default) of a host vector into a caller's array; nothing for none (an
+// empty vector's data() may be null, which memcpy must not be given)
+template <class T>
+inline void copy_out(void* dst, const std::vector<T>& v, size_t n = SIZE_MAX) {
+    n = std::min(n, v.size());
+    if (dst && n) std::memcpy(dst, v.data(), n * sizeof(T));
+}
+
 // ------------------------------------------------------------------ rs_plan.cpp
 int device_tables(int device, const uint32_t** out);
 // log / exp / gamma-byte tables of the device plan builders

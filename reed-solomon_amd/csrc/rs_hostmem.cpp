@@ -166,20 +166,27 @@ const uint8_t* arena_run(symbol_t* const* syms, size_t cnt, size_t S, size_t* pi
     return b;
 }
 
-// Caller-owned symbols outside the arenas (symbol_create; seq_create with RS_AMD_PINNED_SEQ=0): data of
-// kRegMinBytes or more lives in whole pages of its own (sym_va_take), recorded here and page-locked and mapped at
-// creation (hipHostRegister, within the pinned cap). A per-call use then moves such symbols with zero-copy
-// or gather / scatter kernels across PCIe instead of host copies through staging. Only buffers this
-// library allocated are registered: it alone knows when they are freed.
-// A registered range is never handed back to the process for reuse: symbol_destroy parks it, still
-// registered, in an idle pool (later symbol_create calls of a similar size take it back: no second
-// registration), and past the pool's cap unregisters it and leaves its address range reserved with no
-// memory behind it (PROT_NONE). Once-registered addresses reused by other allocations -- pageable torch /
-// numpy buffers that the runtime copies into -- were followed by GPU faults in those copies.
+// Caller-owned symbols outside the arenas (symbol_create; seq_create with RS_AMD_PINNED_SEQ=0). symbol_create
+// stays a host-only allocation, as the reference's calloc (src/memory/symbol.c:25): data of kRegMinBytes or
+// more gets whole pages of its own at increasing addresses of a reserved address range (sym_va_take), and
+// no HIP call is made. The first rs_* call that moves such symbols page-locks and maps them
+// (sym_devptrs -> sym_register, within the pinned cap); from then on calls move them with zero-copy or
+// gather / scatter kernels across PCIe instead of host copies through staging. Only buffers this library
+// allocated are registered: it alone knows when they are freed.
+//
+// An address range that was once registered is never handed to another allocator (DESIGN.md section 9,
+// "registered caller symbols": the round-3 fault). symbol_destroy parks a block, still registered, in an
+// idle pool (later symbol_create calls of a similar size take it back: no second registration); past the
+// pool's cap it unregisters the block and retires the range: its memory goes back to the OS (PROT_NONE,
+// MAP_NORESERVE) but the addresses stay reserved. Every register / unregister result is checked. A block
+// whose registration cannot be undone -- hipHostUnregister fails, or the runtime still reports the range
+// afterwards -- is stuck: it stays mapped, out of circulation and counted against the pinned cap, and the
+// first such event is logged.
 constexpr size_t kPage = 4096;
 struct SymEnt {
-    size_t bytes;         // whole pages
-    uint8_t* dev;         // device-visible address once registered
+    size_t bytes;           // whole pages
+    uint8_t* dev;           // device-visible address once registered
+    bool stuck = false;     // a registration that could not be undone (see above)
 };
 struct SymRegistry {
     std::mutex mu;
@@ -187,30 +194,39 @@ struct SymRegistry {
     size_t idle_bytes = 0;                    // blocks parked in sym_idle()
     uint8_t* va_base = nullptr;               // current address reservation (sym_va_take)
     size_t va_size = 0, va_used = 0;
+    size_t pool_cap = 0;                      // idle pool cap (bytes): RS_AMD_SYM_POOL_MB, default 1 GiB
+    rsg_symbol_stats_t st{};                  // counters (rsg_symbol_stats)
+    std::vector<std::pair<uint8_t*, size_t>> stuck;  // stuck blocks of destroyed symbols
+    bool logged = false;                      // the first failure has been reported
+    SymRegistry() {
+        pool_cap = size_t(1) << 30;
+        if (const char* e = std::getenv("RS_AMD_SYM_POOL_MB")) pool_cap = size_t(std::strtoull(e, nullptr, 10)) << 20;
+    }
 };
 SymRegistry& symreg() {
     static SymRegistry* r = new SymRegistry;  // never destroyed: symbols may outlive static destructors
     return *r;
 }
-size_t sym_pool_cap() {
-    static const size_t cap = [] {
-        if (const char* e = std::getenv("RS_AMD_SYM_POOL_MB")) return size_t(std::strtoull(e, nullptr, 10)) << 20;
-        return size_t(1) << 30;
+
+// address reservation per mmap: 64 GiB, or RS_AMD_SYM_VA_MB (tests: a small value exercises the step to
+// the next reservation)
+size_t sym_va_chunk() {
+    static const size_t v = [] {
+        if (const char* e = std::getenv("RS_AMD_SYM_VA_MB")) return std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        return size_t(64) << 30;
     }();
-    return cap;
+    return v;
 }
 
-bool sym_register(uint8_t* p, SymEnt& e);
-
-// Fresh pages at increasing addresses from a reserved address range (64 GiB per reservation, no memory
-// behind it until used), so consecutive symbol_create calls of one size sit at one stride (the zero-copy
-// kernels' condition) and no address is ever handed out twice except through the idle pool.
+// Fresh pages at increasing addresses from a reserved address range (no memory behind it until used),
+// so consecutive symbol_create calls of one size sit at one stride (the zero-copy kernels' condition)
+// and no address is ever handed out twice except through the idle pool. R.mu held.
 uint8_t* sym_va_take(SymRegistry& R, size_t bytes) {
     if (!R.va_base || R.va_used + bytes > R.va_size) {
-        const size_t sz = std::max(size_t(64) << 30, bytes);
+        const size_t sz = std::max(sym_va_chunk(), bytes);
         void* r = mmap(nullptr, sz, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
         if (r == MAP_FAILED) return nullptr;
-        R.va_base = static_cast<uint8_t*>(r);
+        R.va_base = static_cast<uint8_t*>(r);  // the rest of the previous reservation is never used
         R.va_size = sz;
         R.va_used = 0;
     }
@@ -221,12 +237,13 @@ uint8_t* sym_va_take(SymRegistry& R, size_t bytes) {
     return p;
 }
 
-// back to a reserved range without memory (the address is never reused)
+// memory back to the OS, the address range kept reserved (never reused)
 void sym_va_retire(uint8_t* p, size_t bytes) {
-    (void)mmap(p, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+    if (mmap(p, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0) == MAP_FAILED)
+        std::fprintf(stderr, "librs_amd: retiring a symbol range failed (its memory stays mapped)\n");
 }
 
-// a parked block (registered, or not when the cap or a missing GPU refused it): host address and entry
+// a parked block (registered, or not when it was never registered): host address and entry
 struct IdleBlock {
     uint8_t* host;
     SymEnt e;
@@ -236,91 +253,140 @@ std::multimap<size_t, IdleBlock>& sym_idle() {
     return *m;
 }
 
+void sym_log_once(SymRegistry& R, const char* what, uint8_t* p, size_t bytes, hipError_t e) {
+    if (R.logged) return;
+    R.logged = true;
+    std::fprintf(stderr,
+                 "librs_amd: %s of symbol pages [%p, +%zu) failed (%s); the block stays mapped, out of circulation "
+                 "and counted against the pinned cap (reported once)\n",
+                 what, static_cast<void*>(p), bytes, hipGetErrorString(e));
+}
+
+// true when the runtime knows an address of [p, p + bytes) (first, middle or last byte)
+bool sym_runtime_knows(const uint8_t* p, size_t bytes) {
+    for (const uint8_t* q : {p, p + bytes / 2, p + bytes - 1}) {
+        hipPointerAttribute_t attr{};
+        const bool known = hipPointerGetAttributes(&attr, q) == hipSuccess && attr.type != hipMemoryTypeUnregistered;
+        (void)hipGetLastError();
+        if (known) return true;
+    }
+    return false;
+}
+
+// undoes one of our registrations (R.mu held): true when the runtime returned success and no longer
+// knows the range
+bool sym_unregister(SymRegistry& R, uint8_t* p, size_t bytes) {
+    const hipError_t e = hipHostUnregister(p);
+    (void)hipGetLastError();
+    const bool ok = e == hipSuccess && !sym_runtime_knows(p, bytes);
+    if (ok) {
+        ++R.st.unregistrations;
+        return true;
+    }
+    ++R.st.unregister_failures;
+    sym_log_once(R, e == hipSuccess ? "unregistration (range still known to the runtime)" : "unregistration", p,
+                 bytes, e);
+    return false;
+}
+
 uint8_t* sym_alloc(size_t S) {
     if (S < kRegMinBytes) return nullptr;
     const size_t bytes = (S + kPage - 1) / kPage * kPage;
     SymRegistry& R = symreg();
-    {
-        std::lock_guard<std::mutex> lk(R.mu);
-        auto& idle = sym_idle();
-        auto it = idle.lower_bound(bytes);
-        if (it != idle.end() && it->first <= 2 * bytes) {  // a parked registered block of a similar size
-            IdleBlock b = it->second;
-            idle.erase(it);
-            R.idle_bytes -= b.e.bytes;
-            std::memset(b.host, 0, b.e.bytes);
-            SymEnt& e = R.m[uintptr_t(b.host)] = b.e;
-            (void)sym_register(b.host, e);  // parked unregistered (cap, no GPU then): try again
-            return b.host;
-        }
-    }
     std::lock_guard<std::mutex> lk(R.mu);
+    auto& idle = sym_idle();
+    auto it = idle.lower_bound(bytes);
+    if (it != idle.end() && it->first <= 2 * bytes) {  // a parked block of a similar size, registration kept
+        IdleBlock b = it->second;
+        idle.erase(it);
+        R.idle_bytes -= b.e.bytes;
+        ++R.st.idle_reuses;
+        std::memset(b.host, 0, b.e.bytes);
+        R.m[uintptr_t(b.host)] = b.e;
+        return b.host;
+    }
     uint8_t* p = sym_va_take(R, bytes);
     if (!p) return nullptr;
-    SymEnt& e = R.m[uintptr_t(p)] = SymEnt{bytes, nullptr};
-    // page-lock it now, as seq_create's arenas are (the per-call path then never pays for it); a failure
-    // (no GPU, the pinned cap) leaves it to the first use
-    (void)sym_register(static_cast<uint8_t*>(p), e);
-    return static_cast<uint8_t*>(p);
+    R.m[uintptr_t(p)] = SymEnt{bytes, nullptr};  // registered by the first call that moves it (sym_devptrs)
+    return p;
 }
 
-// page-locks and maps one registry entry (its mutex held); false when the cap or the runtime refuses
-bool sym_register(uint8_t* p, SymEnt& e) {
+// page-locks and maps one registry entry (R.mu held); false when the cap or the runtime refuses
+bool sym_register(SymRegistry& R, uint8_t* p, SymEnt& e) {
     if (e.dev) return true;
+    if (e.stuck) return false;
     ArenaRegistry& A = arenas();
     {
         std::lock_guard<std::mutex> la(A.mu);
         if (A.no_pinning || A.pinned + e.bytes > pinned_cap()) return false;
         A.pinned += e.bytes;
     }
-    // never touch a range the runtime already knows: a failed registration must not be followed by an
-    // unregister, which would remove the owner's mapping
-    hipPointerAttribute_t attr{};
-    const bool known = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type != hipMemoryTypeUnregistered;
-    (void)hipGetLastError();
-    bool ok = !known && hipHostRegister(p, e.bytes, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess;
-    void* dv = nullptr;
-    if (ok && hipHostGetDevicePointer(&dv, p, 0) != hipSuccess) {
-        (void)hipHostUnregister(p);  // ours: registered just above
-        ok = false;
-    }
-    (void)hipGetLastError();
-    if (!ok) {
+    auto unpin = [&] {
         std::lock_guard<std::mutex> la(A.mu);
         A.pinned -= e.bytes;
+    };
+    // never touch a range the runtime already knows: a failed registration must not be followed by an
+    // unregister, which would remove the owner's mapping
+    if (sym_runtime_knows(p, e.bytes)) {
+        ++R.st.register_failures;
+        unpin();
+        return false;
+    }
+    const hipError_t er = hipHostRegister(p, e.bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    (void)hipGetLastError();
+    if (er != hipSuccess) {
+        ++R.st.register_failures;
+        unpin();
+        return false;
+    }
+    ++R.st.registrations;
+    void* dv = nullptr;
+    const hipError_t ed = hipHostGetDevicePointer(&dv, p, 0);
+    (void)hipGetLastError();
+    if (ed != hipSuccess || !dv) {
+        ++R.st.register_failures;
+        if (sym_unregister(R, p, e.bytes)) {
+            unpin();
+        } else {
+            e.stuck = true;  // still registered as far as we know: keep it counted, never register again
+        }
         return false;
     }
     e.dev = static_cast<uint8_t*>(dv);
     return true;
 }
 
-// true (and p parked or released) when p came from sym_alloc
+// a block leaving circulation (R.mu held): unregistered (when registered) and retired, or kept stuck
+void sym_retire_block(SymRegistry& R, uint8_t* p, const SymEnt& e) {
+    if (e.stuck || (e.dev && !sym_unregister(R, p, e.bytes))) {
+        R.stuck.emplace_back(p, e.bytes);  // mapped, out of circulation, still counted as pinned
+        ++R.st.stuck_blocks;
+        R.st.stuck_bytes += e.bytes;
+        return;
+    }
+    sym_va_retire(p, e.bytes);
+    ++R.st.retired_blocks;
+    if (e.dev) {
+        ArenaRegistry& A = arenas();
+        std::lock_guard<std::mutex> la(A.mu);
+        A.pinned -= e.bytes;
+    }
+}
+
+// true (and p parked, retired or kept stuck) when p came from sym_alloc
 bool sym_release(uint8_t* p) {
     SymRegistry& R = symreg();
-    SymEnt e;
-    {
-        std::lock_guard<std::mutex> lk(R.mu);
-        auto it = R.m.find(uintptr_t(p));
-        if (it == R.m.end()) return false;
-        e = it->second;
-        R.m.erase(it);
-        if (R.idle_bytes + e.bytes <= sym_pool_cap()) {
-            sym_idle().emplace(e.bytes, IdleBlock{p, e});
-            R.idle_bytes += e.bytes;
-            return true;
-        }
-        if (!e.dev) {  // never registered
-            sym_va_retire(p, e.bytes);
-            return true;
-        }
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.m.find(uintptr_t(p));
+    if (it == R.m.end()) return false;
+    const SymEnt e = it->second;
+    R.m.erase(it);
+    if (!e.stuck && R.idle_bytes + e.bytes <= R.pool_cap) {
+        sym_idle().emplace(e.bytes, IdleBlock{p, e});
+        R.idle_bytes += e.bytes;
+        return true;
     }
-    // over the pool's cap: unregister, then keep the address range reserved without memory behind it
-    (void)hipHostUnregister(p);
-    (void)hipGetLastError();
-    sym_va_retire(p, e.bytes);
-    ArenaRegistry& A = arenas();
-    std::lock_guard<std::mutex> lk(A.mu);
-    A.pinned -= e.bytes;
+    sym_retire_block(R, p, e);
     return true;
 }
 
@@ -333,7 +399,7 @@ bool sym_devptrs(symbol_t* const* syms, size_t cnt, size_t S, uint64_t* out) {
         if (!syms[i]) return false;
         auto it = R.m.find(uintptr_t(syms[i]->data));
         if (it == R.m.end() || it->second.bytes < S) return false;
-        if (!it->second.dev && !sym_register(syms[i]->data, it->second)) return false;
+        if (!it->second.dev && !sym_register(R, syms[i]->data, it->second)) return false;
         out[i] = uint64_t(reinterpret_cast<uintptr_t>(it->second.dev));
     }
     return true;
@@ -461,4 +527,37 @@ extern "C" int rsg_symbol_registered(const void* data) {
     std::lock_guard<std::mutex> lk(R.mu);
     auto it = R.m.find(uintptr_t(data));
     return it == R.m.end() ? -1 : (it->second.dev ? 1 : 0);
+}
+
+extern "C" int rsg_symbol_stats(rsg_symbol_stats_t* out) {
+    if (!out) return RS_ERR_INVALID;
+    SymRegistry& R = symreg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    *out = R.st;
+    out->live = R.m.size();
+    out->live_registered = 0;
+    for (const auto& kv : R.m) out->live_registered += kv.second.dev ? 1 : 0;
+    out->idle_blocks = sym_idle().size();
+    out->idle_bytes = R.idle_bytes;
+    ArenaRegistry& A = arenas();
+    std::lock_guard<std::mutex> la(A.mu);
+    out->pinned_bytes = A.pinned;
+    return 0;
+}
+
+extern "C" int64_t rsg_symbol_pool_cap(int64_t bytes) {
+    SymRegistry& R = symreg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    const int64_t prev = int64_t(R.pool_cap);
+    if (bytes < 0) return prev;
+    R.pool_cap = size_t(bytes);
+    auto& idle = sym_idle();
+    while (R.idle_bytes > R.pool_cap && !idle.empty()) {  // a lowered cap: the largest parked blocks leave now
+        auto it = std::prev(idle.end());
+        const IdleBlock b = it->second;
+        idle.erase(it);
+        R.idle_bytes -= b.e.bytes;
+        sym_retire_block(R, b.host, b.e);
+    }
+    return prev;
 }

@@ -635,9 +635,9 @@ extern "C" int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint
         info[4] = ok ? h.fin_stride : 0;
         info[5] = d;
     }
-    if (ok && rec) std::memcpy(rec, h.rec.data(), h.rec.size());
-    if (ok && fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
-    if (ok && fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);
+    if (ok) copy_out(rec, h.rec);
+    if (ok) copy_out(fin, h.fin);
+    if (ok) copy_out(fin_off, h.fin_off);
     return 0;
 }
 
@@ -660,9 +660,9 @@ extern "C" int rsg_route_dump_t(uint16_t k, uint16_t r, const bool* is_erased, u
         info[2] = h.fin_stride_t;
         info[3] = NBLK;
     }
-    if (rec) std::memcpy(rec, h.rec_t.data(), h.rec_t.size() * 4);
-    if (fin) std::memcpy(fin, h.fin_t.data(), h.fin_t.size() * 4);
-    if (fin_off) std::memcpy(fin_off, h.fin_off_t.data(), h.fin_off_t.size() * 4);
+    copy_out(rec, h.rec_t);
+    copy_out(fin, h.fin_t);
+    copy_out(fin_off, h.fin_off_t);
     if (blocks) std::memcpy(blocks, kCs16tOff, sizeof(kCs16tOff));
     return 0;
 }
@@ -686,13 +686,13 @@ extern "C" int rsg_route_dump(uint16_t k, uint16_t r, const bool* is_erased, uin
         info[3] = h.fin_stride;
         info[4] = int32_t(outs.size());
     }
-    if (groups) std::memcpy(groups, h.groups.data(), size_t(h.ngroups) * 16 * 4);  // even count, without the tail
-    if (rec) std::memcpy(rec, h.rec.data(), h.rec.size());
-    if (fin) std::memcpy(fin, h.fin.data(), h.fin.size() * 4);
-    if (fin_off) std::memcpy(fin_off, h.fin_off.data(), h.fin_off.size() * 4);
+    copy_out(groups, h.groups, size_t(h.ngroups) * 16);  // even count, without the tail
+    copy_out(rec, h.rec);
+    copy_out(fin, h.fin);
+    copy_out(fin_off, h.fin_off);
     if (m2) {
         const std::vector<uint16_t> M = syndrome_solve_matrix(targets, emit);
-        std::memcpy(m2, M.data(), M.size() * 2);
+        copy_out(m2, M);
     }
     return 0;
 }

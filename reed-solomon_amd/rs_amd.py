@@ -96,6 +96,17 @@ _sig("rsg_route_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P, P)
 _sig("rsg_route_dump_t", ctypes.c_int, u16, u16, P, u16, P, P, P, P, P)
 _sig("rsg_bs16_dump", ctypes.c_int, u16, u16, P, u16, P, P, P, P)
 _sig("rsg_symbol_registered", ctypes.c_int, P)
+
+
+class SymbolStatsT(ctypes.Structure):  # include/rs_amd/rsg.h rsg_symbol_stats_t
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "live", "live_registered", "idle_blocks", "idle_bytes", "idle_reuses", "registrations",
+        "register_failures", "unregistrations", "unregister_failures", "retired_blocks", "stuck_blocks",
+        "stuck_bytes", "pinned_bytes")]
+
+
+_sig("rsg_symbol_stats", ctypes.c_int, ctypes.POINTER(SymbolStatsT))
+_sig("rsg_symbol_pool_cap", i64, i64)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("gf_create", P)
 _sig("gf_destroy", None, P)
@@ -193,6 +204,20 @@ def route_dump_t(k, r, is_erased=None):
 def symbol_registered(arr):
     """1 / 0: a symbol_create buffer (>= 16 KiB) is / is not yet page-locked for the per-call path; -1: other."""
     return int(_lib.rsg_symbol_registered(ctypes.c_void_p(arr.ctypes.data)))
+
+
+def symbol_stats():
+    """Counters of the library-allocated symbol pages (rsg_symbol_stats) as a dict."""
+    st = SymbolStatsT()
+    rc = _lib.rsg_symbol_stats(ctypes.byref(st))
+    if rc:
+        raise RSError(rc, "rsg_symbol_stats")
+    return {n: int(getattr(st, n)) for n, _ in SymbolStatsT._fields_}
+
+
+def symbol_pool_cap(nbytes=-1):
+    """Sets the idle pool's cap (bytes; < 0 queries) and returns the previous one."""
+    return int(_lib.rsg_symbol_pool_cap(int(nbytes)))
 
 
 def bs16_dump(k, r, is_erased=None):

@@ -126,7 +126,8 @@ _oracle = None
 def oracle():
     global _oracle
     if _oracle is None:
-        so = os.path.join(ORACLE_DIR, "librs_oracle.so")
+        # RS_ORACLE_LIB: another build of the same oracle (the sanitizer build, tests/test_sanitizers.py)
+        so = os.environ.get("RS_ORACLE_LIB") or os.path.join(ORACLE_DIR, "librs_oracle.so")
         if not os.path.exists(so):
             subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         lib = ctypes.CDLL(so)

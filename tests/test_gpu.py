@@ -3,6 +3,7 @@ each kernel variant, plus multi-stripe round trips checked against the CPU oracl
 
 All tests run in one process; they need librs_amd.so built for gfx950 (no CPU fallback exists)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -1025,10 +1026,11 @@ def test_drop_in_pinned_seq(k, r, S, pattern):
             assert pitch == _pad(S), "seq_create did not place the sequence in one arena"
         for i in range(k):
             q.symbols[i][:] = data[i]
-        own = S >= 16384 and flag == "0"  # symbol_create buffers from 16 KiB: page-aligned, page-locked
-        assert all(rs_amd.symbol_registered(x) == (1 if own else -1) for x in q.symbols)
+        own = S >= 16384 and flag == "0"  # symbol_create buffers from 16 KiB: page-aligned, registered on first use
+        assert all(rs_amd.symbol_registered(x) == (0 if own else -1) for x in q.symbols)
         for call in range(4):  # decode calls 3+ of a GF(256) pattern run the specialised plan, 4+ zero-copy
             assert rs.generate_repair_symbols(q, r) == 0
+            assert all(rs_amd.symbol_registered(x) == (1 if own else -1) for x in q.symbols)
             got = np.stack(q.symbols)
             assert np.array_equal(got, want), f"encode pinned={flag} call {call}"
             for i in np.nonzero(er)[0]:
@@ -1042,6 +1044,65 @@ def test_drop_in_pinned_seq(k, r, S, pattern):
     assert np.array_equal(outs[0], outs[1])
     rs.close()
 
+
+
+def test_registered_symbol_retired_past_pool_cap():
+    """The round-3 fault's mechanism, checked once ("registered caller symbols"):
+    symbol_create pages registered by a per-call use and destroyed past the idle pool's cap are
+    unregistered with the result checked (unregistrations + n, no failure, no stuck block), their memory
+    is returned (the pages are PROT_NONE) while the address range stays reserved, later symbols never get
+    those addresses, and a torch D2H copy into fresh pageable memory afterwards is exact."""
+    k, r, S = 10, 4, 65536
+    n = k + r
+    rng = np.random.default_rng(404)
+    data = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    want = np.zeros((n, S), np.uint8)
+    want[:k] = data
+    assert oracle_encode(k, r, want) == 0
+    old_cap = rs_amd.symbol_pool_cap(0)  # nothing parks: every destroyed block is unregistered and retired
+    try:
+        st0 = rs_amd.symbol_stats()
+        os.environ["RS_AMD_PINNED_SEQ"] = "0"
+        try:
+            q = rs_amd.Seq(n, S)
+        finally:
+            os.environ.pop("RS_AMD_PINNED_SEQ")
+        assert all(rs_amd.symbol_registered(x) == 0 for x in q.symbols)  # symbol_create made no HIP call
+        for i in range(k):
+            q.symbols[i][:] = data[i]
+        rs = rs_amd.RS()
+        assert rs.generate_repair_symbols(q, r) == 0
+        assert np.array_equal(np.stack(q.symbols), want)
+        assert all(rs_amd.symbol_registered(x) == 1 for x in q.symbols)
+        addrs = [x.ctypes.data for x in q.symbols]
+        q.close()
+        rs.close()
+        st1 = rs_amd.symbol_stats()
+        assert st1["registrations"] - st0["registrations"] == n
+        assert st1["unregistrations"] - st0["unregistrations"] == n
+        assert st1["unregister_failures"] == st0["unregister_failures"]
+        assert st1["stuck_blocks"] == st0["stuck_blocks"]
+        assert st1["retired_blocks"] - st0["retired_blocks"] == n
+        assert st1["pinned_bytes"] == st0["pinned_bytes"]
+        with open("/proc/self/maps") as f:
+            maps = [(int(a, 16), int(b, 16), perms) for a, b, perms in
+                    ((ln.split()[0].split("-") + [ln.split()[1]]) for ln in f)]
+        for a in addrs:
+            assert any(lo <= a < hi and perms == "---p" for lo, hi, perms in maps), "retired pages still mapped"
+        os.environ["RS_AMD_PINNED_SEQ"] = "0"
+        try:
+            q2 = rs_amd.Seq(n, S)
+        finally:
+            os.environ.pop("RS_AMD_PINNED_SEQ")
+        assert not set(x.ctypes.data for x in q2.symbols) & set(addrs)
+        q2.close()
+        src = torch.randint(0, 256, (8, 1 << 20), dtype=torch.uint8, device="cuda")
+        ref = src.sum(dim=1, dtype=torch.int64).cpu()
+        for _ in range(3):
+            host = src.cpu()  # pageable destination
+            assert torch.equal(host.sum(dim=1, dtype=torch.int64), ref)
+    finally:
+        rs_amd.symbol_pool_cap(old_cap)
 
 
 @pytest.mark.parametrize("k,r,S,n,pinned", [(128, 32, 65536, 30, True), (10, 4, 4096 + 24, 300, False),

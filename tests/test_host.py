@@ -250,11 +250,12 @@ def test_seq_create_without_gpu_falls_back_to_heap():
 
 def test_symbol_create_pages_and_pool():
     """symbol_create from 16 KiB (seq_create with RS_AMD_PINNED_SEQ=0): whole zeroed pages of their own at
-    increasing addresses (consecutive symbols of one size at one stride, the zero-copy condition);
-    symbol_destroy parks them (registered ones stay registered) and the next symbols of that size take
-    the same addresses back, zeroed, so a once-registered address never returns to other allocators.
-    Without a GPU the registration is refused (0), never -1 (unknown pointer)."""
+    increasing addresses (consecutive symbols of one size at one stride, the zero-copy condition), and no
+    HIP call (registration waits for the first rs_* call that moves the symbol: 0, never -1);
+    symbol_destroy parks them in the idle pool and the next symbols of that size take the same addresses
+    back, zeroed, so a once-registered address never returns to other allocators."""
     S = 3 * 4096 + 4096 + 100
+    st0 = rs_amd.symbol_stats()
     os.environ["RS_AMD_PINNED_SEQ"] = "0"
     try:
         q = rs_amd.Seq(6, S)
@@ -262,7 +263,7 @@ def test_symbol_create_pages_and_pool():
         page = (S + 4095) // 4096 * 4096
         assert all(a % 4096 == 0 for a in addrs)
         assert [b - a for a, b in zip(addrs, addrs[1:])] == [page] * 5
-        assert all(rs_amd.symbol_registered(x) in (0, 1) for x in q.symbols)
+        assert all(rs_amd.symbol_registered(x) == 0 for x in q.symbols)
         for x in q.symbols:
             x[:] = 0xA5
         q.close()
@@ -272,9 +273,72 @@ def test_symbol_create_pages_and_pool():
         q2.close()
     finally:
         os.environ.pop("RS_AMD_PINNED_SEQ")
+    st1 = rs_amd.symbol_stats()
+    assert st1["registrations"] == st0["registrations"] and st1["register_failures"] == st0["register_failures"]
+    assert st1["idle_reuses"] - st0["idle_reuses"] == 6
     small = rs_amd.Seq(3, 4096)  # below 16 KiB: calloc, not tracked
     assert all(rs_amd.symbol_registered(x) == -1 for x in small.symbols)
     small.close()
+
+
+def _maps_perms(addr):
+    """Permissions of the /proc/self/maps mapping holding addr (None when unmapped)."""
+    with open("/proc/self/maps") as f:
+        for line in f:
+            lo, hi = (int(v, 16) for v in line.split()[0].split("-"))
+            if lo <= addr < hi:
+                return line.split()[1]
+    return None
+
+
+def test_symbol_churn_pool_cap_and_reservations():
+    """Allocator churn of library-allocated symbol pages (rs_hostmem.cpp), the code of the round-3 fault:
+    random sizes 16 KiB .. 200 KiB, random destroy order, a small idle-pool cap. Live counts return to the
+    baseline, the pool never exceeds its cap, blocks destroyed past it are retired (memory returned:
+    PROT_NONE, address kept reserved) and no retired address is handed out again; a parked address comes
+    back only through the pool. Under tests/test_sanitizers.py (RS_AMD_SYM_VA_MB=1) the churn also
+    crosses many address reservations (sym_va_take)."""
+    rng = np.random.default_rng(11)
+    old_cap = rs_amd.symbol_pool_cap(3 << 20)
+    st0 = rs_amd.symbol_stats()
+    retired, seen = set(), set()
+    live = []
+    os.environ["RS_AMD_PINNED_SEQ"] = "0"
+    try:
+        for it in range(60):
+            n = int(rng.integers(1, 9))
+            S = int(rng.integers(16 << 10, 200 << 10))
+            q = rs_amd.Seq(n, S)
+            for x in q.symbols:
+                a = x.ctypes.data
+                assert a % 4096 == 0 and not x.any()
+                assert a not in retired, "a retired address was handed out again"
+                assert rs_amd.symbol_registered(x) == 0
+                x[:] = it & 0xFF
+                seen.add(a)
+            live.append(q)
+            if len(live) > 4 or rng.integers(0, 2):
+                victim = live.pop(int(rng.integers(0, len(live))))
+                before = rs_amd.symbol_stats()
+                addrs = [x.ctypes.data for x in victim.symbols]
+                victim.close()
+                after = rs_amd.symbol_stats()
+                assert after["idle_bytes"] <= (3 << 20)
+                if after["retired_blocks"] > before["retired_blocks"]:
+                    # every block of the victim not parked was retired: its pages are PROT_NONE now
+                    gone = [a for a in addrs if _maps_perms(a) == "---p"]
+                    assert len(gone) == after["retired_blocks"] - before["retired_blocks"]
+                    retired.update(gone)
+        for q in live:
+            q.close()
+    finally:
+        os.environ.pop("RS_AMD_PINNED_SEQ")
+        rs_amd.symbol_pool_cap(old_cap)
+    st1 = rs_amd.symbol_stats()
+    assert st1["live"] == st0["live"]
+    assert st1["retired_blocks"] > st0["retired_blocks"] and st1["idle_reuses"] > st0["idle_reuses"]
+    assert st1["unregister_failures"] == st0["unregister_failures"] and st1["stuck_blocks"] == st0["stuck_blocks"]
+    assert len(retired) > 0
 
 
 def test_bench_traffic_lookup_is_per_leg(tmp_path, monkeypatch):
