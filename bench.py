@@ -245,6 +245,25 @@ def cpu_cores():
     return avail, quota
 
 
+def port_calibration(k, r, S, gbs):
+    """The port's speed relative to the reference (oracle/calibration.json, measured in the build container
+    by scripts/calibrate_oracle.py: same C driver, one thread, identical inputs) and the reference-equivalent
+    rate of this run's port baseline; None when the configuration was not calibrated."""
+    try:
+        with open(os.path.join(REPO, "oracle", "calibration.json")) as f:
+            cal = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for row in cal.get("rows", []):
+        if (row["k"], row["r"], row["S"]) == (k, r, S):
+            x = float(row["port_over_ref"])
+            return dict(port_over_reference=x, reference_equivalent_value=round(gbs * x, 4),
+                        source=f"oracle/calibration.json ({cal.get('measured')}, {cal.get('host')}): port "
+                               f"{row['port_ms_per_stripe']} ms vs reference {row['ref_ms_per_stripe']} ms per stripe, "
+                               f"bit-exact {row['bitexact']}")
+    return None
+
+
 def cpu_baseline(args, erased, gpu_sample):
     """Times encode + decode of `cpu_stripes` resident stripes with the reference CPU path on a pthread
     pool (oracle/cpu_baseline.c: one context per thread, views built before the clock). Returns
@@ -300,8 +319,11 @@ def cpu_baseline(args, erased, gpu_sample):
     t1 = run(0, 1, 1, c1) + run(1, 1, 1, c1)
     gbs1 = c1 * ((k + r) + (k + t)) * S / t1 / 1e9
     label = kind if kind == "reference" else "port (oracle/_ref/librs_ref.so absent: clean-room restatement timed)"
-    return dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind, cores_available=avail, cpu_quota=quota,
-                single_core=round(gbs1, 4),
+    out = dict(value=round(gbs, 4), unit="GB/s", cores=threads, kind=kind, cores_available=avail, cpu_quota=quota,
+               single_core=round(gbs1, 4))
+    if kind == "port":
+        out["calibration"] = port_calibration(k, r, S, gbs)
+    return dict(out,
                 sample=f"{label}: {n} resident stripes of k={k} r={r} S={S}, {p_enc} encode + {p_dec} decode (t={t}) "
                        f"passes on {threads} pthreads ({avail} cores available, quota {quota}), "
                        f"{t_enc + t_dec:.1f} s; single_core: {c1} stripes, 1 thread, {t1:.2f} s"), parity

@@ -28,7 +28,7 @@ extern "C" {
 /* reference :29 */
 #define RS_ERR_CANNOT_RESTORE 100
 /* additions of this implementation (the reference asserts these preconditions instead) */
-#define RS_ERR_INVALID 2   /* odd symbol size, k + r > N, size mismatch, erasure count != t */
+#define RS_ERR_INVALID 2   /* k + r > N, size mismatch, erasure count != t (rsg_*: also odd symbol sizes) */
 #define RS_ERR_DEVICE 3    /* HIP runtime / kernel error */
 
 /* reference :34-37; the first two members keep the reference's layout */
@@ -42,7 +42,9 @@ typedef struct {
 RS_t* rs_create(void);
 /* reference :51 */
 void rs_destroy(RS_t* rs);
-/* reference :61 -- 0 on success, 1 on allocation failure, RS_ERR_INVALID / RS_ERR_DEVICE */
+/* reference :61 -- 0 on success, 1 on allocation failure, RS_ERR_INVALID / RS_ERR_DEVICE. An odd symbol size
+ * behaves as the reference's Release build: the even prefix is coded and each repair symbol's last byte
+ * is 0 (restores likewise: restored symbols end in a zero byte). */
 int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf_symbols, symbol_seq_t* rep_symbols);
 /* reference :74 -- erased slots must be zero on entry; restores erased information symbols in place
  * (erased repair slots are left untouched, as in the reference). 0, 1, RS_ERR_CANNOT_RESTORE (t > r),

@@ -169,11 +169,12 @@ extern "C" void rs_destroy(RS_t* rs) {
     std::free(rs);
 }
 
-extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, symbol_seq_t* rep) {
-    if (!rs || !rs->impl || !inf || !rep) return RS_ERR_INVALID;
+namespace {
+
+// The per-call encode on an even symbol size (rs_generate_repair_symbols handles odd ones around it).
+int generate_even(RS_t* rs, const symbol_seq_t* inf, symbol_seq_t* rep) {
     Impl& im = *static_cast<Impl*>(rs->impl);
     const size_t S = inf->symbol_size;
-    if (S != rep->symbol_size || (S & 1) || inf->length + rep->length > kN) return RS_ERR_INVALID;
     const uint16_t k = uint16_t(inf->length), r = uint16_t(rep->length);
     if (r == 0 || S == 0) return 0;
     std::lock_guard<std::mutex> lk(im.mu);
@@ -276,13 +277,10 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
     return 0;
 }
 
-extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool* is_erased,
-                                  uint16_t t) {
-    if (r < t) return RS_ERR_CANNOT_RESTORE;  // checked first, as reference reed_solomon.c:467-470
-    if (!rs || !rs->impl || !rcv || !is_erased) return RS_ERR_INVALID;
+// The per-call restore on an even symbol size (rs_restore_symbols handles odd ones around it).
+int restore_even(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool* is_erased, uint16_t t) {
     Impl& im = *static_cast<Impl*>(rs->impl);
     const size_t S = rcv->symbol_size, n = size_t(k) + r;
-    if (rcv->length != n || (S & 1) || n > kN) return RS_ERR_INVALID;
     size_t cnt = 0;
     std::vector<int> keep, lost;  // surviving slots (gathered), erased information slots (scattered)
     for (size_t i = 0; i < n; ++i) {
@@ -439,4 +437,39 @@ extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t
     HIP_TRY(hipEventSynchronize(im.ev[nch - 1]));
     scatter(nch - 1);
     return 0;
+}
+
+}  // namespace
+
+// Odd symbol sizes follow the reference's Release build (-DNDEBUG, the baseline's flags), where the
+// symbol-wide operations cover symbol_size / 2 words (gf65536.c:158-169): the code runs on the even
+// prefix, and every symbol the call writes ends in a zero byte -- fft_partial_transform_cycl memsets each
+// repair symbol first (fft.c:163), _rs_restore_erased each restored one (reed_solomon.c:326). Golden cases
+// odd_* pin both (tests/golden/make_golden.py).
+extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, symbol_seq_t* rep) {
+    if (!rs || !rs->impl || !inf || !rep) return RS_ERR_INVALID;
+    const size_t S = inf->symbol_size;
+    if (S != rep->symbol_size || inf->length + rep->length > kN) return RS_ERR_INVALID;
+    if (!(S & 1)) return generate_even(rs, inf, rep);
+    const symbol_seq_t ie = {inf->length, S - 1, inf->symbols};
+    symbol_seq_t re = {rep->length, S - 1, rep->symbols};
+    const int rc = generate_even(rs, &ie, &re);
+    if (rc == 0)
+        for (size_t j = 0; j < rep->length; ++j) rep->symbols[j]->data[S - 1] = 0;
+    return rc;
+}
+
+extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool* is_erased,
+                                  uint16_t t) {
+    if (r < t) return RS_ERR_CANNOT_RESTORE;  // checked first, as reference reed_solomon.c:467-470
+    if (!rs || !rs->impl || !rcv || !is_erased) return RS_ERR_INVALID;
+    const size_t S = rcv->symbol_size, n = size_t(k) + r;
+    if (rcv->length != n || n > kN) return RS_ERR_INVALID;
+    if (!(S & 1)) return restore_even(rs, k, r, rcv, is_erased, t);
+    symbol_seq_t e = {rcv->length, S - 1, rcv->symbols};
+    const int rc = restore_even(rs, k, r, &e, is_erased, t);
+    if (rc == 0)
+        for (size_t i = 0; i < k; ++i)
+            if (is_erased[i]) rcv->symbols[i]->data[S - 1] = 0;
+    return rc;
 }

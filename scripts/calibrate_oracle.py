@@ -1,7 +1,11 @@
-"""Calibration of the CPU baselines: the reference src/rs compiled from its
-own sources (oracle/_ref/librs_ref.so) and the clean-room restatement (oracle/librs_oracle.so),
-single-threaded on identical inputs; prints the time ratio per configuration and checks that both
-produce the same bytes. TEST INFRASTRUCTURE (no GPU)."""
+"""Calibration of the CPU baselines: the reference src/rs compiled from its own
+sources (oracle/_ref/librs_ref.so) against the clean-room restatement (oracle/librs_oracle.so), timed by
+the same C driver bench.py uses (oracle/cpu_baseline.c, cpub_run: views built before the clock), one
+thread, identical inputs (encode + bench-pattern decode), median of 3 runs; checks that both produce
+the same bytes. With --out FILE it writes the ratios bench.py reports beside a port-timed baseline on the
+GPU box, where the reference never travels (oracle/calibration.json).
+
+TEST INFRASTRUCTURE (no GPU): run here, where /root/reference is."""
 import ctypes
 import json
 import os
@@ -12,48 +16,60 @@ import numpy as np
 
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(REPO, "tests"))
-sys.path.insert(0, REPO)
-from _util import bench_pattern, gen_info, oracle  # noqa: E402
-from bench import _seq  # noqa: E402
+from _util import bench_pattern, gen_info  # noqa: E402
 
-ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "librs_ref.so"))
-ref.rs_create.restype = ctypes.c_void_p
-ref.rs_destroy.argtypes = [ctypes.c_void_p]
-ref.rs_generate_repair_symbols.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-ref.rs_restore_symbols.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_void_p,
-                                   ctypes.c_void_p, ctypes.c_uint16]
-orc = oracle()
+REF = os.path.join(REPO, "oracle", "_ref", "librs_ref.so")
+PORT = os.path.join(REPO, "oracle", "librs_oracle.so")
+drv = ctypes.CDLL(os.path.join(REPO, "oracle", "libcpu_baseline.so"))
+drv.cpub_run.restype = ctypes.c_int
+drv.cpub_run.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p,
+                         ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                         ctypes.POINTER(ctypes.c_double)]
+out_path = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
 
-for k, r, S, n in ((4, 2, 256, 2000), (10, 4, 4096, 200), (128, 32, 65536, 2), (4096, 1024, 1024, 1)):
+
+def timed(lib, port, k, r, S, stripes, er, t, op, passes):
+    sec = ctypes.c_double()
+    rc = drv.cpub_run(lib.encode(), port, k, r, S, stripes.ctypes.data, stripes.shape[0], er.ctypes.data, t, op,
+                      passes, 1, ctypes.byref(sec))
+    assert rc == 0, rc
+    return sec.value
+
+
+def one(k, r, S, n, passes):
     er = np.zeros(k + r, np.bool_)
     er[bench_pattern(k, r)] = True
     t = int(er.sum())
     base = np.zeros((n, k + r, S), np.uint8)
     for s in range(n):
         base[s, :k] = gen_info(0x5EED, s, k * S).reshape(k, S)
-    a, b = base.copy(), base.copy()
-    rs = ref.rs_create()
-    t0 = time.perf_counter()
-    for s in range(n):
-        inf, k1 = _seq(a[s], 0, k, S)
-        rep, k2 = _seq(a[s], k, r, S)
-        assert ref.rs_generate_repair_symbols(rs, ctypes.byref(inf), ctypes.byref(rep)) == 0
-    t_ref_enc = time.perf_counter() - t0
-    a[:, er] = 0
-    t0 = time.perf_counter()
-    for s in range(n):
-        rcv, k3 = _seq(a[s], 0, k + r, S)
-        assert ref.rs_restore_symbols(rs, k, r, ctypes.byref(rcv), er.ctypes.data, t) == 0
-    t_ref_dec = time.perf_counter() - t0
-    ref.rs_destroy(rs)
-    t0 = time.perf_counter()
-    assert orc.orc_encode_many(k, r, S, b.ctypes.data, n, 1) == 0
-    t_orc_enc = time.perf_counter() - t0
-    b[:, er] = 0
-    t0 = time.perf_counter()
-    assert orc.orc_decode_many(k, r, S, b.ctypes.data, n, er.ctypes.data, t, 1) == 0
-    t_orc_dec = time.perf_counter() - t0
-    print(json.dumps({"k": k, "r": r, "S": S, "stripes": n, "bitexact": bool(np.array_equal(a, b)),
-                      "ref_ms_per_stripe": round((t_ref_enc + t_ref_dec) / n * 1e3, 3),
-                      "oracle_ms_per_stripe": round((t_orc_enc + t_orc_dec) / n * 1e3, 3),
-                      "oracle_over_ref": round((t_orc_enc + t_orc_dec) / (t_ref_enc + t_ref_dec), 3)}), flush=True)
+    res = {}
+    for name, lib, port in (("ref", REF, 0), ("port", PORT, 1)):
+        a = base.copy()
+        te = timed(lib, port, k, r, S, a, er, t, 0, passes)
+        enc = a.copy()
+        td = timed(lib, port, k, r, S, a, er, t, 1, passes)
+        res[name] = (te + td) / (n * passes), enc, a
+    same = np.array_equal(res["ref"][1], res["port"][1]) and np.array_equal(res["ref"][2], res["port"][2])
+    return same, res["ref"][0], res["port"][0]
+
+
+rows = []
+for k, r, S, n, passes in ((4, 2, 256, 256, 200), (10, 4, 4096, 64, 20), (128, 32, 65536, 4, 1),
+                           (4096, 1024, 1024, 1, 1)):
+    runs = [one(k, r, S, n, passes) for _ in range(3)]
+    ratio = sorted(p / f for _, f, p in runs)[1]
+    row = {"k": k, "r": r, "S": S, "stripes": n, "passes": passes, "bitexact": all(b for b, _, _ in runs),
+           "ref_ms_per_stripe": round(sorted(f for _, f, _ in runs)[1] * 1e3, 4),
+           "port_ms_per_stripe": round(sorted(p for _, _, p in runs)[1] * 1e3, 4),
+           "port_over_ref": round(ratio, 3)}
+    rows.append(row)
+    print(json.dumps(row), flush=True)
+if out_path:
+    with open(out_path, "w") as f:
+        json.dump({"what": "time of the clean-room CPU port (oracle/librs_oracle.so) over the reference compiled from "
+                           "its own sources (oracle/_ref/librs_ref.so): the same C driver (oracle/cpu_baseline.c), "
+                           "one thread, identical inputs, encode + bench-pattern decode, median of 3 runs "
+                           "(scripts/calibrate_oracle.py)",
+                   "host": "build container (no GPU)", "measured": time.strftime("%Y-%m-%d"), "rows": rows}, f,
+                  indent=1)

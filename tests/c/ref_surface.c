@@ -5,6 +5,12 @@
  * tests/test_gpu.py compares them with tests/golden/. Inputs are regenerated with the fixtures'
  * portable generator (oracle/gen_golden.c:gen_byte / pos_gen).
  *
+ * The codec part follows the reference's own callers, so their coverage does not depend on the
+ * reference's compiled programs (which never travel to the GPU box): src/example.c (a k + r sequence
+ * from seq_create, information / repair views into it, a received copy, erase, restore, seq_eq) on the
+ * ex_* fixtures and the C3-shape c3_* fixtures, and test/src/rs/test_random_data.c's 100 rounds of
+ * random (k, r, t) round trips over 16-byte symbols (self-checked with seq_eq on the information view).
+ *
  * Usage: ref_surface <outdir>
  */
 #include <stdbool.h>
@@ -63,6 +69,76 @@ static symbol_seq_t* gen_seq(size_t len, size_t S, uint64_t stripe) {
     for (size_t i = 0; i < len; ++i)
         for (size_t b = 0; b < S; ++b) q->symbols[i]->data[b] = gen_byte(SEED, stripe, i * S + b);
     return q;
+}
+
+/* src/example.c's call pattern on one golden case: per stripe, encode through views into a seq_create
+ * sequence, then (decode cases) copy to a received sequence, zero the erased slots, restore, and check
+ * the information symbols with seq_eq. Writes the repair rows (encode) or whole stripes (decode). */
+static void codec_case(RS_t* rs, const char* name, uint16_t k, uint16_t r, size_t S, int n, const uint16_t* erased,
+                       uint16_t t, int decode) {
+    const size_t rows = decode ? (size_t)(k + r) : r;
+    uint8_t* out = malloc((size_t)n * rows * S);
+    bool* is_erased = calloc(k + r, sizeof(bool));
+    for (uint16_t e = 0; e < t; ++e) is_erased[erased[e]] = true;
+    for (int s = 0; s < n; ++s) {
+        symbol_seq_t* src = seq_create(k + r, S);
+        for (size_t i = 0; i < k; ++i)
+            for (size_t b = 0; b < S; ++b) src->symbols[i]->data[b] = gen_byte(SEED, (uint64_t)s, i * S + b);
+        symbol_seq_t inf = {k, S, src->symbols}, rep = {r, S, src->symbols + k};
+        check(rs_generate_repair_symbols(rs, &inf, &rep) == 0, name);
+        if (!decode) {
+            for (size_t j = 0; j < r; ++j) memcpy(out + ((size_t)s * rows + j) * S, rep.symbols[j]->data, S);
+        } else {
+            symbol_seq_t* rcv = seq_create(k + r, S);
+            for (size_t i = 0; i < (size_t)(k + r); ++i) memcpy(rcv->symbols[i]->data, src->symbols[i]->data, S);
+            for (size_t i = 0; i < (size_t)(k + r); ++i)
+                if (is_erased[i]) memset(rcv->symbols[i]->data, 0, S);
+            check(t == 0 || !seq_eq(src, rcv), name);
+            check(rs_restore_symbols(rs, k, r, rcv, is_erased, t) == 0, name);
+            symbol_seq_t rinf = {k, S, rcv->symbols};
+            check((S & 1) || seq_eq(&inf, &rinf), name);  /* odd S: restored symbols end in 0 (reference) */
+            for (size_t i = 0; i < rows; ++i) memcpy(out + ((size_t)s * rows + i) * S, rcv->symbols[i]->data, S);
+            seq_destroy(rcv);
+        }
+        seq_destroy(src);
+    }
+    save_raw(name, out, (size_t)n * rows * S);
+    free(is_erased);
+    free(out);
+}
+
+/* test/src/rs/test_random_data.c's call pattern: 100 rounds, symbol size 16, k in [100, 200), r in
+ * [50, 100), t erasures anywhere (half the rounds t in [11, r), half t = r); each round encodes through
+ * views into one sequence, erases a random set in a received copy, restores, and compares the
+ * information views with seq_eq. The random choices come from splitmix, not libc rand(). */
+static void random_data_rounds(RS_t* rs) {
+    uint64_t st = 234546127u;
+    for (int round = 0; round < 100; ++round) {
+        const uint16_t k = (uint16_t)(100 + mix64(++st) % 100), r = (uint16_t)(50 + mix64(++st) % 50);
+        const uint16_t t = round < 50 ? (uint16_t)(11 + mix64(++st) % (uint64_t)(r - 10)) : r;
+        const size_t S = 16;
+        symbol_seq_t* src = seq_create(k + r, S);
+        symbol_seq_t* rcv = seq_create(k + r, S);
+        bool* is_erased = calloc(k + r, sizeof(bool));
+        for (size_t i = 0; i < k; ++i)
+            for (size_t b = 0; b < S; ++b) src->symbols[i]->data[b] = (uint8_t)(mix64(++st) >> 24);
+        symbol_seq_t inf = {k, S, src->symbols}, rep = {r, S, src->symbols + k}, rinf = {k, S, rcv->symbols};
+        check(rs_generate_repair_symbols(rs, &inf, &rep) == 0, "random_data encode");
+        for (size_t i = 0; i < (size_t)(k + r); ++i) memcpy(rcv->symbols[i]->data, src->symbols[i]->data, S);
+        for (uint16_t e = 0; e < t;) {
+            const size_t i = mix64(++st) % (uint64_t)(k + r);
+            if (is_erased[i]) continue;
+            is_erased[i] = true;
+            memset(rcv->symbols[i]->data, 0, S);
+            ++e;
+        }
+        check(!seq_eq(src, rcv), "random_data erase");
+        check(rs_restore_symbols(rs, k, r, rcv, is_erased, t) == 0, "random_data restore");
+        check(seq_eq(&inf, &rinf), "random_data inf_symbols == rcv_inf_symbols");
+        free(is_erased);
+        seq_destroy(rcv);
+        seq_destroy(src);
+    }
 }
 
 int main(int argc, char** argv) {
@@ -163,6 +239,23 @@ int main(int argc, char** argv) {
         seq_destroy(tiny);
         seq_destroy(kept);
         seq_destroy(all);
+        /* src/example.c on its golden pair, the C3-shape fixtures, then test_random_data.c's rounds */
+        const uint16_t ex_er[10] = {2, 8, 11, 13, 19, 30, 38, 50, 61, 92};
+        codec_case(rs, "ex_enc", 100, 10, 10, 1, NULL, 0, 0);
+        codec_case(rs, "ex_dec", 100, 10, 10, 1, ex_er, 10, 1);
+        uint16_t bench[32];
+        for (int i = 0; i < 32; ++i) bench[i] = (uint16_t)(4 * i);
+        const uint16_t rand17[17] = {0, 7, 16, 24, 30, 34, 53, 65, 97, 99, 110, 115, 120, 124, 126, 145, 155};
+        codec_case(rs, "c3_enc", 128, 32, 512, 2, NULL, 0, 0);
+        codec_case(rs, "c3_dec_bench", 128, 32, 512, 2, bench, 32, 1);
+        codec_case(rs, "c3_dec_rand17", 128, 32, 512, 1, rand17, 17, 1);
+        /* odd symbol sizes: the reference's Release semantics (even prefix coded, written symbols end in 0) */
+        const uint16_t odd9[2] = {1, 4}, odd4097[4] = {0, 3, 7, 12};
+        codec_case(rs, "odd_enc_9", 4, 2, 9, 1, NULL, 0, 0);
+        codec_case(rs, "odd_dec_9", 4, 2, 9, 1, odd9, 2, 1);
+        codec_case(rs, "odd_enc_4097", 10, 4, 4097, 2, NULL, 0, 0);
+        codec_case(rs, "odd_dec_4097", 10, 4, 4097, 2, odd4097, 4, 1);
+        random_data_rounds(rs);
         rs_destroy(rs);
     }
     cc_destroy(cc);

@@ -94,6 +94,13 @@ def cases():
     # example.c shape: 10-byte symbols (5 words, not a multiple of 16 B)
     add("ex_enc", "encode", 100, 10, 10, 1)
     add("ex_dec", "decode", 100, 10, 10, 1, 10, rand_pattern(100, 10, 10, 4))
+    # odd symbol sizes: the reference's Release build (-DNDEBUG, the baseline's flags) codes the even
+    # prefix, S / 2 words (gf65536.c:158-169), and the written symbols' last byte is zero (fft.c:163
+    # memsets each repair symbol, reed_solomon.c:326 each restored one)
+    add("odd_enc_9", "encode", 4, 2, 9, 1)
+    add("odd_dec_9", "decode", 4, 2, 9, 1, 2, [1, 4])
+    add("odd_enc_4097", "encode", 10, 4, 4097, 2)
+    add("odd_dec_4097", "decode", 10, 4, 4097, 2, 4, [0, 3, 7, 12])
     # coding matrices via unit vectors (word i of info i = 1)
     add("gmat_4_2", "gmatrix", 4, 2, 8, 1)
     add("gmat_10_4", "gmatrix", 10, 4, 20, 1)

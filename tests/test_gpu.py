@@ -63,13 +63,15 @@ def run_case_gpu(c, variant, options=None):
 
 
 GPU_CASES = [c["name"] for c in manifest()["cases"] if c["op"] not in EXTRA_OPS]
+# odd symbol sizes are a drop-in API case (the reference's Release semantics); rsg_* rejects them
+BATCH_CASES = [n for n in GPU_CASES if not n.startswith("odd_")]
 EXTRA_CASES = [c["name"] for c in manifest()["cases"] if c["op"] in EXTRA_OPS]
 # kernels (rsg_last_kernel) of the production GF(2^16) path over full 1 KiB column chunks
 M16_PRODUCTION = ("apply_m16_v1", "apply_m16_rt16", "apply_m16_rt32")  # R <= 32: the compiled tiles
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
-@pytest.mark.parametrize("name", GPU_CASES)
+@pytest.mark.parametrize("name", BATCH_CASES)
 def test_golden_batch_api(name, variant):
     c = case(name)
     m16 = c["k"] + c["r"] > 255 and c["op"] != "gmatrix"
@@ -93,7 +95,7 @@ def test_golden_batch_api(name, variant):
     check_golden(c, out)
 
 
-DROPIN = [n for n in GPU_CASES if n.startswith(("c1_", "kat_", "ex_", "edge_", "c2_", "m4_", "m8_"))]
+DROPIN = [n for n in GPU_CASES if n.startswith(("c1_", "kat_", "ex_", "edge_", "c2_", "m4_", "m8_", "odd_"))]
 
 
 @pytest.mark.parametrize("name", DROPIN)
@@ -116,6 +118,36 @@ def test_golden_drop_in_api(name):
                     syms[i][:] = 0
             rc = rs.restore_symbols(k, r, syms, er, c["t"])
             outs.append(b"".join(x.tobytes() for x in syms))
+    rs.close()
+    assert rc == c["rc"]
+    check_golden(c, b"".join(outs))
+
+
+@pytest.mark.parametrize("name", [n for n in DROPIN if n.startswith(("odd_", "ex_", "c1_", "c2_"))])
+def test_golden_drop_in_seq_create(name):
+    """The same golden cases on library-allocated sequences (seq_create: page-locked arena stripes at
+    stride pad16(S), zero-copy launches or DMA in place), as the reference's callers allocate them
+    (src/example.c, test_random_data.c); includes the odd symbol sizes."""
+    c = case(name)
+    k, r, n = c["k"], c["r"], c["n"]
+    rs = rs_amd.RS()
+    outs, rc = [], 0
+    for s in range(n):
+        buf, er = case_inputs(c, s)
+        q = rs_amd.Seq(k + r, c["S"])
+        for i in range(k + r):
+            q.symbols[i][:] = buf[i]
+        if c["op"] in ("encode", "encode_iota", "gmatrix"):
+            rc = rs.generate_repair_symbols(q, r)
+            outs.append(b"".join(x.tobytes() for x in q.symbols[k:]))
+        else:
+            if c["op"] == "decode":
+                assert rs.generate_repair_symbols(q, r) == 0
+                for i in np.nonzero(er)[0]:
+                    q.symbols[i][:] = 0
+            rc = rs.restore_symbols(k, r, q, er, c["t"])
+            outs.append(b"".join(x.tobytes() for x in q.symbols))
+        q.close()
     rs.close()
     assert rc == c["rc"]
     check_golden(c, b"".join(outs))
@@ -207,9 +239,12 @@ def test_errors():
     assert codec.decode(dev, er, check=False) == rs_amd.RS_ERR_CANNOT_RESTORE
     assert codec.encode_raw(dev.data_ptr() + 1, 6 * 64, 64, dev.data_ptr() + 256, 6 * 64, 64, 1, 64,
                             torch.cuda.current_stream()) == rs_amd.RS_ERR_INVALID
+    assert codec.encode_raw(dev.data_ptr(), 6 * 64, 64, dev.data_ptr() + 256, 6 * 64, 64, 1, 63,
+                            torch.cuda.current_stream()) == rs_amd.RS_ERR_INVALID  # rsg_*: odd symbol size
     rs = rs_amd.RS()
-    syms = [np.zeros(9, np.uint8) for _ in range(6)]
-    assert rs.generate_repair_symbols(syms[:4], syms[4:]) == rs_amd.RS_ERR_INVALID  # odd symbol size
+    syms = [np.zeros(9, np.uint8) for _ in range(7)]
+    assert rs.generate_repair_symbols(syms[:4], syms[4:7]) == 0  # drop-in: the reference's odd-size semantics
+    assert rs.restore_symbols(4, 2, syms[:5], np.zeros(6, bool), 0) == rs_amd.RS_ERR_INVALID  # length != k + r
 
 
 def test_fingerprint_matches_cpu_port():
@@ -1222,7 +1257,9 @@ def test_symbol_ops_large_and_aliased():
 
 def test_reference_surface_program(tmp_path):
     """tests/c/ref_surface.c calls every function of the reference's rs/ and memory/ headers, built
-    against this repo's headers and linked against librs_amd.so; its outputs equal the goldens."""
+    against this repo's headers and linked against librs_amd.so, including the call patterns of the
+    reference's src/example.c and test_random_data.c (100 self-checked rounds); its outputs equal the
+    goldens (ex_*, c1_*, c3_* and the secondary-surface cases)."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "ref_surface")
@@ -1230,7 +1267,8 @@ def test_reference_surface_program(tmp_path):
     p = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     for name in ("gf_add_64", "gf_mul_c", "gf_madd_c", "fft_t_small", "fft_tc_small", "fft_p_small", "fft_pc_mixed",
-                 "c1_enc", "c1_dec_info_rep"):
+                 "c1_enc", "c1_dec_info_rep", "ex_enc", "ex_dec", "c3_enc", "c3_dec_bench", "c3_dec_rand17",
+                 "odd_enc_9", "odd_dec_9", "odd_enc_4097", "odd_dec_4097"):
         check_golden(case(name), (tmp_path / f"{name}.bin").read_bytes())
 
 

@@ -96,24 +96,32 @@ def _apply_case(c):
     k, r, S = c["k"], c["r"], c["S"]
     outs_all = []
     rc = 0
+    Se = S & ~1  # odd sizes: the reference's Release build codes the even prefix, written symbols end in 0
     for s in range(c["n"]):
         buf, er = case_inputs(c, s)
-        W = buf.view("<u2")
+        W = np.ascontiguousarray(buf[:, :Se]).view("<u2")
         if c["op"] in ("encode", "encode_iota", "gmatrix"):
             if r:
                 M, ins, outs = rs_amd.coding_matrix(k, r)
                 W[k:] = gf_apply(M, W[:k])
+                buf[k:, :Se] = W[k:].view(np.uint8)
+                buf[k:, Se:] = 0
             outs_all.append(buf[k:].tobytes())
             continue
         if c["op"] == "decode":
             M, ins, outs = rs_amd.coding_matrix(k, r)
             W[k:] = gf_apply(M, W[:k])
+            buf[k:, :Se] = W[k:].view(np.uint8)
+            buf[k:, Se:] = 0
             buf[er] = 0
+            W[er] = 0
         if c["t"] > r:
             rc = 100
         elif er[:k].any():
             M, ins, outs = rs_amd.coding_matrix(k, r, er)
             W[outs] = gf_apply(M, W[ins])
+            buf[outs, :Se] = W[outs].view(np.uint8)
+            buf[outs, Se:] = 0
         outs_all.append(buf.tobytes())
     return rc, b"".join(outs_all)
 
