@@ -51,6 +51,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  codes and past one pattern for GF(2^16) codes (default)
  *   "syn_route"    GF(256) device-plan decodes (S a multiple of 2 KiB): 1 syndromes of every slot on the
  *                  bit-plane XOR kernel, then a per-stripe t_info x t solve (default); 0 survivor matrices
+ *   "m8_syn_overlap" that route's plans + syndromes of the next chunk on a codec stream beside this chunk's
+ *                  solve (two buffer sets; 1 default), 0 one stream
  *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
  *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
  *                  0 one plan per pattern rebuilt on the stream

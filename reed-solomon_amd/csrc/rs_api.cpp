@@ -167,6 +167,16 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->dec_lru.clear();
         return 0;
     }
+    if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        c->m8_ps_kernel = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m8_syn_overlap")) {  // GF(256) per-stripe syndrome route: overlapped chunks
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        c->m8_syn_overlap = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "syn_route")) {
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->syn_route = int(value);

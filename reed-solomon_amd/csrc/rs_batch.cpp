@@ -124,16 +124,34 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (syn_prepare(c, S, symbol_stride)) {
-        // syndrome route: zero erased information slots + build the t_info x t solves (k_plan_syn_m8),
-        // the r syndromes of every selected stripe into scratch (XOR kernel, dst indexed by the chunk-
-        // local stripe), then the per-stripe solves from the syndromes into the erased information slots
+        // syndrome route: the t_info x t solves (k_plan_syn_m8), the r syndromes of every selected stripe
+        // into scratch (XOR kernel, dst indexed by the chunk-local stripe), then the per-stripe solves
+        // from the syndromes XORed into the erased information slots (not zeroed first: V1Args::xor_dst).
+        // Option m8_syn_overlap (default): plans and syndromes of chunk i + 1 run on the codec's syndrome
+        // stream beside chunk i's solve on the caller's stream, two buffer sets alternating.
         const uint16_t* expt = nullptr;
         if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
         const int64_t per = int64_t(c->r) * int64_t(S);
-        const int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t(1) << 30) / per));
-        if ((rc = grow(&c->d_syn, c->syn_cap, size_t(sch * per)))) return rc;
-        for (int64_t c0 = 0; c0 < nsel; c0 += sch) {
+        int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t(1) << 30) / per));
+        const bool ovl = c->m8_syn_overlap && nsel > sch / 2;
+        if (ovl) sch = std::max<int64_t>(1, std::min<int64_t>(sch, (nsel + 3) / 4));  // at least 4 chunks
+        const int nset = ovl ? 2 : 1;
+        if ((rc = grow(&c->d_syn, c->syn_cap, size_t(nset * sch * per)))) return rc;
+        if ((rc = grow(&c->d_kr, c->kr_cap, size_t(nset * sch) * 8))) return rc;
+        if ((rc = grow(&c->d_pin, c->pin_cap, size_t(nset * sch * in_stride) * 4))) return rc;
+        if ((rc = grow(&c->d_pout, c->pout_cap, size_t(nset * sch * out_stride) * 4))) return rc;
+        if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
+        hipStream_t sy = st;
+        if (ovl) {
+            if ((rc = overlap_objects(c))) return rc;
+            sy = c->ps_synst;
+            HIP_TRY(hipEventRecord(c->ps_ev_entry, st));  // the stripes' earlier writers on st come first
+            HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
+        }
+        for (int64_t c0 = 0, ci = 0; c0 < nsel; c0 += sch, ++ci) {
             const int64_t cn = std::min(sch, nsel - c0);
+            const int set = ovl ? int(ci & 1) : 0;
+            if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));  // chunk ci - 2's solve read it
             SynPlanArgs pa{};
             pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(c0) * n;
             pa.elem = c->d_elem;
@@ -143,26 +161,25 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             pa.k = c->k;
             pa.r = c->r;
             pa.n = int32_t(n);
-            pa.kr = static_cast<int32_t*>(c->d_kr);
-            pa.pin = static_cast<int32_t*>(c->d_pin);
-            pa.pout = static_cast<int32_t*>(c->d_pout);
-            pa.pidx = static_cast<uint32_t*>(c->d_pidx);
+            pa.kr = static_cast<int32_t*>(c->d_kr) + 2 * set * sch;
+            pa.pin = static_cast<int32_t*>(c->d_pin) + set * sch * in_stride;
+            pa.pout = static_cast<int32_t*>(c->d_pout) + set * sch * out_stride;
+            pa.pidx = static_cast<uint32_t*>(c->d_pidx) + set * sch * idx_stride;
             pa.in_stride = in_stride;
             pa.out_stride = out_stride;
             pa.idx_stride = idx_stride;
-            pa.base = base;
-            pa.stripe_stride = stripe_stride;
-            pa.symbol_stride = symbol_stride;
-            pa.S = int64_t(S);
-            pa.ids = c->d_ids + c0;
-            HIP_TRY(launch_plan_syn_m8(pa, cn, st));
-            uint8_t* syn = static_cast<uint8_t*>(c->d_syn);
+            HIP_TRY(launch_plan_syn_m8(pa, cn, sy));
+            uint8_t* syn = static_cast<uint8_t*>(c->d_syn) + set * sch * per;
             if ((rc = run_plan(c, *c->syn, base, stripe_stride, symbol_stride, syn, per, int64_t(S), uint64_t(cn), S,
-                               st, c->d_ids + c0, true)))
+                               sy, c->d_ids + c0, true)))
                 return rc;
+            if (ovl) {
+                HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
+                HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+            }
             V1Args v{};
             v.src = syn;
-            v.src_stripe = 0;  // slots are local * r + j
+            v.src_stripe = 0;  // input slots of the plan are local * r + j, relative to this set's buffer
             v.src_sym = int64_t(S);
             v.in_idx = pa.pin;
             v.dst = base;
@@ -176,9 +193,11 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_in = in_stride;
             v.ps_out = out_stride;
             v.ps_idx = idx_stride;
-            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+            v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
+            if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
-        c->last_kernel = "syn_xj+apply_m8_v1_ps";
+        c->last_kernel = ovl ? "syn_xj+apply_m8_v1_ps(overlap)" : "syn_xj+apply_m8_v1_ps";
         return scratch_release(c, st);
     }
     for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {
@@ -215,7 +234,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.ps_in = in_stride;
         v.ps_out = out_stride;
         v.ps_idx = idx_stride;
-        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st));
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
     }
     c->last_kernel = "apply_m8_v1_ps";
     return scratch_release(c, st);

@@ -297,6 +297,13 @@ struct rsg_codec {
     // device-plan decodes of m <= 8 codes: 1 = syndrome route (fixed r x (k + r) syndrome matrix on the
     // XOR kernel, then a per-stripe t_info x t solve), 0 = per-stripe survivor matrices (k_plan_m8)
     int syn_route = 1;
+    // option m8_syn_overlap: that route's plans and syndromes of chunk i + 1 on the codec's syndrome stream
+    // beside chunk i's solve (two buffer sets); 0 = one stream
+    int m8_syn_overlap = 1;
+    // option m8_ps_kernel: the per-stripe GF(256) solve's kernel: 0 k_apply_m8_v1 (LDS input ring), 1
+    // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
+    // two dwords per lane)
+    int m8_ps_kernel = 0;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;
     void* d_syn = nullptr;  // [chunk][r][S] syndromes
@@ -383,6 +390,8 @@ int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, i
            const int32_t* groups = nullptr);
 int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_stride, int64_t sym, uint64_t n_stripes,
               uint64_t S, hipStream_t st);
+// the codec's syndrome stream and its events (per-stripe routes, m16_cs_overlap), created on first use
+int overlap_objects(rsg_codec_t* c);
 
 // ------------------------------------------------------------------ rs_hostmem.cpp
 // symbols of at least this many bytes are allocated in whole pages of their own and registrable

@@ -112,6 +112,39 @@ __device__ __forceinline__ void wait_vm() {
 // ------------------------------------------ m <= 8, one dword per lane per input step (V = 1)
 constexpr int V1_LDS_WORDS = 2048 + RING_SLOTS * 256;
 
+// The V = 1 kernels' outputs: row p of the tile (accumulator a0[p] / a1[p - 16], GF(256)^2 coordinates) back
+// to GF(2^16) words and stored to dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst).
+__device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt, uint8_t* dst, const int32_t* out,
+                                            int rows, const u32x16& a0, const u32x16& a1) {
+    if (a.xor_dst) {  // g ^ (W S): the old contents, loaded 8 at a time ahead of their stores
+#pragma unroll
+        for (int p0 = 0; p0 < 32; p0 += 8) {
+            uint32_t old[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                old[q] = p0 + q < rows ? *reinterpret_cast<const uint32_t*>(dst + int64_t(sload(out + p0 + q)) * a.dst_sym)
+                                       : 0u;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int p = p0 + q;
+                if (p < rows) {
+                    const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
+                    *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) =
+                        lds_lookup4(lt + 1024, v) ^ old[q];
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) = lds_lookup4(lt + 1024, v);
+        }
+    }
+}
+
 // Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile
 // blockIdx.y. Per batch of 4 inputs: wave (i % 4) issues input i's DMA RING_B batches ahead; every
 // wave reads its 4 dwords from the ring, maps them to GF(256)^2 coordinates (LDS byte tables) and
@@ -201,13 +234,5 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
             if (p < rows) part[p * cw] = lds_lookup4(lt + 1024, p < 16 ? a0[p & 15] : a1[p & 15]);
         return;
     }
-    uint8_t* dst = a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4;
-#pragma unroll
-    for (int p = 0; p < 32; ++p) {
-        if (p < rows) {
-            const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
-            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out_idx + tile * 32 + p)) * a.dst_sym) =
-                lds_lookup4(lt + 1024, v);
-        }
-    }
+    m8_v1_store(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4, out_idx + tile * 32, rows, a0, a1);
 }

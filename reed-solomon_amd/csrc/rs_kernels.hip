@@ -393,6 +393,133 @@ __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
     });
 }
 
+// Per-stripe V = 1 apply without the LDS input ring, for the short solves of rsg_decode_batch (K = t <= r
+// inputs per stripe; at C3 32). The ring kernel's four waves of a 1 KiB chunk meet at a barrier every 4
+// inputs and wait for DMA bookkeeping: at K = 32 its waves spent a third of their time parked
+// (SQ_WAIT_ANY, profiles/r4/ps8_pmc.txt). Here the four waves of a block share only the coordinate tables:
+// each loads its own 256-byte column of the inputs straight into registers, 8 inputs ahead, and runs the
+// same input step (gen_asm.py v1) and output stage as k_apply_m8_v1.
+__global__ void __launch_bounds__(256) k_apply_m8_ps_w(V1Args a) {
+    __shared__ uint32_t lt[2048];
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+    const int64_t bid = blockIdx.x;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t col = (bid - local * a.nchunks) * 1024 + int64_t(threadIdx.x) * 4;
+    const int tile = blockIdx.y;
+    const int K = sload(a.ps_kr + 2 * local), R = sload(a.ps_kr + 2 * local + 1);
+    if (tile * 32 >= R) return;  // uniform over the block
+    const int32_t* in_idx = a.in_idx + local * a.ps_in;
+    const uint32_t* idxb = a.idx + local * a.ps_idx + size_t(tile) * K * 64;
+    const uint8_t* src = a.src + (a.src_local ? local : stripe) * a.src_stripe + col;
+    auto ld = [&](int i) { return *reinterpret_cast<const uint32_t*>(src + int64_t(sload(in_idx + i)) * a.src_sym); };
+    u32x16 a0 = 0, a1 = 0;
+    uint32_t cur[8], nxt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cur[j] = j < K ? ld(j) : 0u;
+    for (int i0 = 0; i0 < K; i0 += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nxt[j] = i0 + 8 + j < K ? ld(i0 + 8 + j) : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (i0 + j < K) m8_v1_step<0>(lds_lookup4(lt, cur[j]), idxb + size_t(i0 + j) * 64, a0, a1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+    }
+    m8_v1_store(a, lt, a.dst + stripe * a.dst_stripe + col, a.out_idx + local * a.ps_out + tile * 32,
+                min(32, R - tile * 32), a0, a1);
+}
+
+// The same with two dwords per lane (the "split" input step of k_apply_m8_idx / _lds, gen_asm.py): each
+// index switch serves two lookups, half the V = 1 kernel's SALU per byte, at 3 waves per SIMD. A block's
+// four waves cover a 2 KiB column chunk; the last chunk of a symbol may be partial (FULL = false: loads
+// and stores bounded by the symbol size).
+template <bool FULL>
+__device__ __forceinline__ void m8_ps_w2_body(const V1Args& a, const uint32_t* lt, int64_t local, int64_t stripe,
+                                              int64_t col, int tile, int K, int R) {
+    const int64_t avail = FULL ? 8 : a.nchunks - col;  // nchunks carries the symbol size here (see launcher)
+    const int32_t* in_idx = a.in_idx + local * a.ps_in;
+    const uint32_t* idxb = a.idx + local * a.ps_idx + size_t(tile) * K * 64;
+    const uint8_t* src = a.src + (a.src_local ? local : stripe) * a.src_stripe + col;
+    auto ld = [&](uint32_t (&x)[2], int i) {
+        const uint8_t* p = src + int64_t(sload(in_idx + i)) * a.src_sym;
+        if constexpr (FULL) {
+            const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+            x[0] = v.x;
+            x[1] = v.y;
+        } else {
+            load_slice<8>(x, p, avail);
+        }
+    };
+    u32x16 a0l = 0, a0h = 0, a1l = 0, a1h = 0;
+    uint32_t cur[4][2], nxt[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cur[j][0] = cur[j][1] = 0;
+        if (j < K) ld(cur[j], j);
+    }
+    for (int i0 = 0; i0 < K; i0 += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            nxt[j][0] = nxt[j][1] = 0;
+            if (i0 + 4 + j < K) ld(nxt[j], i0 + 4 + j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i0 + j < K) m8_idx_step<0>(lt, cur[j], idxb + size_t(i0 + j) * 64, a0l, a0h, a1l, a1h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j][0] = nxt[j][0], cur[j][1] = nxt[j][1];
+    }
+    uint8_t* dst = a.dst + stripe * a.dst_stripe + col;
+    const int32_t* out = a.out_idx + local * a.ps_out + tile * 32;
+    const int rows = min(32, R - tile * 32);
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        if (p < rows) {
+            uint8_t* d = dst + int64_t(sload(out + p)) * a.dst_sym;
+            uint32_t y[2] = {lds_lookup4(lt + 1024, p < 16 ? a0l[p & 15] : a0h[p & 15]),
+                             lds_lookup4(lt + 1024, p < 16 ? a1l[p & 15] : a1h[p & 15])};
+            if (a.xor_dst) {  // V1Args::xor_dst
+                uint32_t old[2];
+                if constexpr (FULL) {
+                    const u32x2 v = *reinterpret_cast<const u32x2*>(d);
+                    old[0] = v.x;
+                    old[1] = v.y;
+                } else {
+                    load_slice<8>(old, d, avail);
+                }
+                y[0] ^= old[0];
+                y[1] ^= old[1];
+            }
+            if constexpr (FULL)
+                *reinterpret_cast<u32x2*>(d) = (u32x2){y[0], y[1]};
+            else
+                store_slice<8>(d, y, avail);
+        }
+    }
+}
+
+// grid (n_sel * chunks of 2 KiB, tiles); a.nchunks = the symbol size in bytes
+__global__ void __launch_bounds__(256) k_apply_m8_ps_w2(V1Args a) {
+    __shared__ uint32_t lt[2048];
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+    const int64_t S = a.nchunks, nch = (S + 2047) / 2048;
+    const int64_t bid = blockIdx.x;
+    const int64_t local = bid / nch;
+    const int64_t chunk0 = (bid - local * nch) * 2048;
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int tile = blockIdx.y;
+    const int K = sload(a.ps_kr + 2 * local), R = sload(a.ps_kr + 2 * local + 1);
+    if (tile * 32 >= R) return;  // uniform over the block
+    const int64_t col = chunk0 + int64_t(threadIdx.x) * 8;
+    if (chunk0 + 2048 <= S)
+        m8_ps_w2_body<true>(a, lt, local, stripe, col, tile, K, R);
+    else
+        m8_ps_w2_body<false>(a, lt, local, stripe, col, tile, K, R);
+}
+
 template <int ABL, int PD>
 __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t* __restrict__ in_idx) {
     __shared__ uint32_t lt[2048];
@@ -1323,8 +1450,9 @@ __global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
 // the reference's evaluator / Forney steps (reed_solomon.c:186-336) solve the t x t Vandermonde system
 // sum_{e in E} X_e^j d_e = S_j, j < t, over the syndromes of fft_transform_cycl (fft.c:39-100, erased
 // slots read as zero). Its inverse is W[p][j] = q_{p,j} / Q_p(X_p), q_p the coefficients of
-// Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Garbage in
-// erased repair slots only shifts their own (unused) unknowns; erased information slots are zeroed here.
+// Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Erased slots are
+// not zeroed: their old contents g enter the syndromes, the solve yields g + c for the erased information
+// slots, and the apply XORs that into g (V1Args::xor_dst). Erased repair slots only shift their own unknowns.
 __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
     __shared__ uint16_t ee[256], pe[256];
     __shared__ int32_t ps[256];
@@ -1402,13 +1530,6 @@ __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
             for (int i = 0; i < t; ++i) r0[size_t(i) * 64 + jj] = r0[size_t(i) * 64 + 32 + jj] = 0u;
         }
     }
-    // zero the erased information slots of this stripe (8-byte stores; S, bases and strides are 8-aligned)
-    uint8_t* sb = a.base + int64_t(a.ids[s]) * a.stripe_stride;
-    const int64_t words = a.S / 8;
-    for (int p = 0; p < R; ++p) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(sb + int64_t(ps[p]) * a.symbol_stride);
-        for (int64_t x = j; x < words; x += 256) d[x] = 0;
-    }
 }
 
 // Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
@@ -1460,8 +1581,14 @@ __global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0
 #pragma unroll
     for (int p = 0; p < 32; ++p) {
         if (p < rows) {
-            const uint32_t y[1] = {lds_lookup4(lt + 1024, acc[p])};
-            store_slice<4>(dst + int64_t(out_idx[tile * 32 + p]) * a.dst_sym, y, avail);
+            uint8_t* d = dst + int64_t(out_idx[tile * 32 + p]) * a.dst_sym;
+            uint32_t y[1] = {lds_lookup4(lt + 1024, acc[p])};
+            if (a.xor_dst) {  // see V1Args::xor_dst
+                uint32_t old[1];
+                load_slice<4>(old, d, avail);
+                y[0] ^= old[0];
+            }
+            store_slice<4>(d, y, avail);
         }
     }
 }
@@ -1848,13 +1975,23 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st) {
+hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
+    if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch
+        V1Args f = v;
+        f.nchunks = nbytes;
+        hipLaunchKernelGGL(k_apply_m8_ps_w2, dim3(unsigned(n_sel * ((nbytes + 2047) / 2048)), unsigned(tiles)),
+                           dim3(256), 0, st, f);
+        return hipGetLastError();
+    }
     const int64_t full = nbytes / 1024;
     if (full > 0) {
         V1Args f = v;
         f.nchunks = full;
-        hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        if (kernel == 1)
+            hipLaunchKernelGGL(k_apply_m8_ps_w, dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        else
+            hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
     }
     if (nbytes % 1024)
         hipLaunchKernelGGL(k_apply_m8_ps_tail, dim3(unsigned(n_sel), unsigned(tiles)), dim3(256), 0, st, v,

@@ -68,9 +68,6 @@ struct SynPlanArgs {
     int32_t* pout;         // [n_sel][out_stride] erased information slots
     uint32_t* pidx;        // [n_sel][idx_stride] V = 1 nibble records
     int64_t in_stride, out_stride, idx_stride;
-    uint8_t* base;         // stripes (erased information slots are zeroed)
-    int64_t stripe_stride, symbol_stride, S;
-    const int32_t* ids;    // [n_sel] stripe indices
 };
 hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st);
 
@@ -122,7 +119,8 @@ hipError_t launch_plan16_ps_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st
 // k_apply_m16_v1 in per-stripe mode over the full 1 KiB chunks (v.ps_* set, tiles = the largest stripe's)
 hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 // V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
-hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
+hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st,
+                              int kernel = 0);
 
 // dst row j = src row rows[j] for j < nrows, `width` bytes each (16-byte aligned rows, padded pitch)
 hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,

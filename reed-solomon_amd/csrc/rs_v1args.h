@@ -37,6 +37,10 @@ struct V1Args {
     // k_apply_m16_v1 per-stripe mode (ps_kr set): nonzero = inputs come from the launch-local stripe
     // (src + local * src_stripe: a per-stripe scratch, e.g. syndromes), outputs from ids (RS_STRIPE)
     int32_t src_local;
+    // nonzero: each output is XORed into its destination instead of stored (the GF(256) per-stripe
+    // syndrome route: the erased slots still hold their old contents g, the syndromes saw them, and the
+    // solve yields g + c, so g ^ (W S) = c without a pass that zeroes the slots first)
+    int32_t xor_dst;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -62,6 +62,10 @@ def run(codec, label, reps):
 
 
 syn = rs_amd.Codec(k, r, batch_plans=1)
+if os.environ.get("RS_PS8_NO_OVERLAP"):  # A/B of the overlapped chunks (option m8_syn_overlap)
+    syn.set_option("m8_syn_overlap", 0)
+if os.environ.get("RS_PS8_KERNEL"):  # A/B of the per-stripe solve kernel (option m8_ps_kernel)
+    syn.set_option("m8_ps_kernel", int(os.environ["RS_PS8_KERNEL"]))
 run(syn, "device_plans_syndrome", 5)
 sur = rs_amd.Codec(k, r, batch_plans=1)
 sur.set_option("syn_route", 0)

@@ -532,20 +532,29 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
         assert np.array_equal(dev.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("route", [0, 1])
+@pytest.mark.parametrize("route,ovl,kern", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1), (0, 0, 1), (1, 0, 2),
+                                            (1, 1, 2), (0, 0, 2)])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
-                                     (128, 32, 32768, 1030)])
-def test_decode_batch_syndrome_route(k, r, S, n, route):
+                                     (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
+def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
-    the XOR kernel, then each stripe's t_info x t solve) and the survivor-matrix route (0). Erased slots
-    hold garbage, not zeros: information slots come back bit-exact vs the oracle (which reads erased
-    slots as zero), erased repair slots are left as they were. n = 1030 at 32 KiB spans two chunks of
-    the syndrome scratch."""
+    the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
+    first; ovl 1: chunk i + 1's plans and syndromes on the codec's second stream beside chunk i's solve)
+    and the survivor-matrix route (0). Erased slots hold garbage, not zeros: information slots come back
+    bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
+    were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
+    kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
+    LDS-ring kernel. S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
+    ends in a partial column chunk."""
+    if route and S % 2048:
+        pytest.skip("the syndrome route covers whole 2 KiB columns (other sizes take the survivor route)")
     rng = np.random.default_rng(k + 3 * n + route)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xD5)
     codec = rs_amd.Codec(k, r, batch_plans=1)
     codec.set_option("syn_route", route)
+    codec.set_option("m8_syn_overlap", ovl)
+    codec.set_option("m8_ps_kernel", kern)  # 1: the ring-free per-stripe solve kernel (k_apply_m8_ps_w)
     codec.encode(dev)
     pats = np.zeros((n, k + r), bool)
     for s in range(n):
@@ -561,7 +570,8 @@ def test_decode_batch_syndrome_route(k, r, S, n, route):
     poisoned = dev.clone()
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert codec.last_kernel == ("syn_xj+apply_m8_v1_ps" if route else "apply_m8_v1_ps")
+    assert codec.last_kernel == ("apply_m8_v1_ps" if not route else
+                                 "syn_xj+apply_m8_v1_ps(overlap)" if ovl else "syn_xj+apply_m8_v1_ps")
     assert torch.equal(dev[:, :k], full[:, :k])
     rep_er = mask.clone()
     rep_er[:, :k] = False
