@@ -77,6 +77,13 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  * diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
+/* Device scratch of a codec only grows with the launches it serves, and is reused by later calls: the
+ * GF(2^16) per-stripe route of rsg_decode_batch keeps two record sets of up to m16_ps_rec_mib (1 GiB each by
+ * default) and two syndrome buffers of up to 1 GiB; the GF(256) syndrome route two syndrome buffers of up
+ * to 1 GiB; the route / re-encode decodes up to 1 GiB each; the host pipelines two 256 MiB batch buffers.
+ * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it (plans stay cached;
+ * later calls grow it again). */
+int rsg_codec_trim(rsg_codec_t* c);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);
 /* Wave-instructions (VALU, SALU) the hand-scheduled GF(2^16) kernels issued in the last rsg_encode /

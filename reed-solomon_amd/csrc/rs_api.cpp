@@ -190,6 +190,45 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     return RS_ERR_INVALID;
 }
 
+extern "C" int rsg_codec_trim(rsg_codec_t* c) {
+    if (!c) return RS_ERR_INVALID;
+    HIP_TRY(hipSetDevice(c->device));
+    // the launches that may still read the scratch: the last batch / route call's (scratch_ev), the side
+    // and syndrome streams, the host pipelines' streams, the staged list copies
+    if (c->scratch_pending) HIP_TRY(hipEventSynchronize(c->scratch_ev));
+    c->scratch_pending = false;
+    if (c->stage_pending) HIP_TRY(hipEventSynchronize(c->stage_ev));
+    c->stage_pending = false;
+    for (hipStream_t s : {c->ps_side, c->ps_synst, c->hs[0], c->hs[1]})
+        if (s) HIP_TRY(hipStreamSynchronize(s));
+    auto drop = [](void*& p, size_t& cap) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    };
+    drop(c->d_cs, c->cs_cap);
+    drop(c->d_reenc, c->reenc_cap);
+    drop(c->d_syn, c->syn_cap);
+    drop(c->d_ps_rec, c->ps_rec_cap);
+    drop(c->d_ps_small, c->ps_small_cap);
+    drop(c->d_partial, c->partial_cap);
+    drop(c->d_masks, c->masks_cap);
+    drop(c->d_kr, c->kr_cap);
+    drop(c->d_pin, c->pin_cap);
+    drop(c->d_pout, c->pout_cap);
+    drop(c->d_pidx, c->pidx_cap);
+    for (int i = 0; i < 2; ++i) {
+        if (c->hbuf[i]) (void)hipFree(c->hbuf[i]);
+        c->hbuf[i] = nullptr;
+    }
+    c->hbuf_cap = 0;
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->stage_cap = 0;
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 extern "C" const char* rsg_last_kernel(const rsg_codec_t* c) { return c ? c->last_kernel.c_str() : "none"; }
 
 namespace rsamd {
@@ -226,11 +265,11 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
             if (p.route_bytes >= uint64_t(c->route_min_bytes)) {
                 std::unique_ptr<bool[]> er(new bool[p.erased.size()]);
                 for (size_t i = 0; i < p.erased.size(); ++i) er[i] = p.erased[i] != 0;
-                const bool re = reenc_eligible(c, er.get()) && src == dst && src_stripe == dst_stripe &&
-                                src_sym == dst_sym && (c->k + c->r) * src_sym < (int64_t(1) << 31) &&
-                                int64_t(c->r) * int64_t(S) < (int64_t(1) << 31);
-                if (int rc = re ? make_plan_reenc(c, er.get(), p.route, st) : make_plan_cs(c, er.get(), p.route, st))
-                    return rc;
+                // the re-encode decode runs in place (its launch layout) with 31-bit offsets over all slots
+                const bool in_place = src == dst && src_stripe == dst_stripe && src_sym == dst_sym &&
+                                      (c->k + c->r) * src_sym < (int64_t(1) << 31) &&
+                                      int64_t(c->r) * int64_t(S) < (int64_t(1) << 31);
+                if (int rc = make_plan_route(c, er.get(), in_place, p.route, st)) return rc;
             }
         }
         if (fits && p.route)

@@ -8,6 +8,41 @@ using namespace rsamd;
 
 namespace rsamd {
 
+// The host lists of a batch call (stripe ids, erasure masks) reach the device through the codec's pinned
+// staging: one copy per list queued on the caller's stream, and the call returns without waiting for
+// them (it used to synchronise the caller's whole stream). The staging is grow-only and guarded by an event:
+// the next call that overwrites it waits for the previous call's copies only.
+struct ListPart {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+int stage_lists(rsg_codec_t* c, hipStream_t st, std::initializer_list<ListPart> parts) {
+    size_t total = 0;
+    for (const ListPart& q : parts) total += (q.bytes + 255) & ~size_t(255);
+    if (c->stage_pending) HIP_TRY(hipEventSynchronize(c->stage_ev));
+    c->stage_pending = false;
+    if (total > c->stage_cap) {
+        if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->stage_cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), std::max<size_t>(total, 4096), hipHostMallocDefault));
+        c->stage_cap = std::max<size_t>(total, 4096);
+    }
+    if (!c->stage_ev) HIP_TRY(hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming));
+    size_t off = 0;
+    for (const ListPart& q : parts) {
+        if (q.bytes) {
+            std::memcpy(c->h_stage + off, q.src, q.bytes);
+            HIP_TRY(hipMemcpyAsync(q.dst, c->h_stage + off, q.bytes, hipMemcpyHostToDevice, st));
+        }
+        off += (q.bytes + 255) & ~size_t(255);
+    }
+    HIP_TRY(hipEventRecord(c->stage_ev, st));
+    c->stage_pending = true;
+    return 0;
+}
+
 // Distinct patterns beyond which rsg_decode_batch builds the decode matrices on the device (the
 // host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
 constexpr size_t kHostPlanGroups = 16;
@@ -119,10 +154,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     if ((rc = grow(&c->d_pin, c->pin_cap, size_t(chunk * in_stride) * 4))) return rc;
     if ((rc = grow(&c->d_pout, c->pout_cap, size_t(chunk * out_stride) * 4))) return rc;
     if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(chunk * idx_stride) * 4))) return rc;
-    // the host lists must outlive the copies: upload on the caller's stream, then wait once
-    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_masks, masks.data(), masks.size(), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
+        return rc;
     if (syn_prepare(c, S, symbol_stride)) {
         // syndrome route: the t_info x t solves (k_plan_syn_m8), the r syndromes of every selected stripe
         // into scratch (XOR kernel, dst indexed by the chunk-local stripe), then the per-stripe solves
@@ -458,11 +491,9 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
         if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     const int ngo = (cs.ngroups + 3) * 16;
     if ((rc = grow(&c->d_goff[0], c->goff_cap[0], size_t(ngo) * 4))) return rc;
-    // the host lists must outlive the copies: upload on the caller's stream, then wait once
-    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_masks, mask_src, ids.size() * n, hipMemcpyHostToDevice, st));
+    if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, mask_src, ids.size() * n}})))
+        return rc;
     HIP_TRY(launch_cs16_goff(cs.groups, static_cast<uint32_t*>(c->d_goff[0]), ngo, symbol_stride, st));
-    HIP_TRY(hipStreamSynchronize(st));
     Ps16Args pa{};
     pa.elem = c->d_elem;
     pa.logt = logt;
@@ -635,9 +666,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         HIP_TRY(hipMalloc(&c->d_ids, ids.size() * 4));
         c->ids_cap = ids.size();
     }
-    // the list must stay valid until the launches have read it: upload on the caller's stream
-    HIP_TRY(hipMemcpyAsync(c->d_ids, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}})) return rc;
     uint8_t* base = static_cast<uint8_t*>(d_rcv);
     // GF(2^16) codes with many patterns: one plan rebuilt on the stream per pattern (batch_plan_m16)
     const bool stream_plans = c->m > 8 && c->m16_plans != 0 &&

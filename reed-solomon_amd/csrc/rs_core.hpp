@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -326,12 +327,19 @@ struct rsg_codec {
     hipEvent_t scratch_ev = nullptr;
     bool scratch_pending = false;
     hipStream_t scratch_stream = nullptr;
+    // pinned staging of rsg_decode_batch's host lists (stage_lists, rs_batch.cpp), guarded by stage_ev
+    uint8_t* h_stage = nullptr;
+    size_t stage_cap = 0;
+    hipEvent_t stage_ev = nullptr;
+    bool stage_pending = false;
     // rsg_encode_host / rsg_decode_host: two streams, each with its own device batch buffer
     hipStream_t hs[2] = {nullptr, nullptr};
     uint8_t* hbuf[2] = {nullptr, nullptr};
     size_t hbuf_cap = 0;
     ~rsg_codec() {
         (void)hipSetDevice(device);
+        if (stage_ev) (void)hipEventSynchronize(stage_ev), (void)hipEventDestroy(stage_ev);
+        if (h_stage) (void)hipHostFree(h_stage);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
         if (ps_side) (void)hipStreamSynchronize(ps_side), (void)hipStreamDestroy(ps_side);
         if (ps_synst) (void)hipStreamSynchronize(ps_synst), (void)hipStreamDestroy(ps_synst);
@@ -383,6 +391,9 @@ int make_plan_dense(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>
 int make_plan_cs(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st);
 int make_plan_reenc(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st);
 bool reenc_eligible(const rsg_codec_t* c, const bool* erased);
+// the route plan of a decode pattern: the plain route, or the re-encode decode (reenc_ok: the launch allows it)
+int make_plan_route(rsg_codec_t* c, const bool* erased, bool reenc_ok, std::unique_ptr<DevPlan>& out,
+                    hipStream_t st);
 int build_cs16(DevPlan& p, const std::vector<uint16_t>& pos, const std::vector<int32_t>& in_slots, int D,
                hipStream_t st);
 int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,

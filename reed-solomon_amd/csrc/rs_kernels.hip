@@ -701,7 +701,6 @@ __global__ void __launch_bounds__(256) k_apply_m16_v1(V1Args a) {
     wait_mine(mine(1, RING_B - 1));
     asm volatile("s_barrier" ::: "memory");
     // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
-    // records: [tile][K + 1][64] packed table indices (one padding record: the last step prefetches)
     const uint32_t* rec = idxb + (size_t(tile) * (Kp + 1) + i0) * 64;
     u32x16 plane;  // plane 0 of the next step's record, requested one step ahead (s[40:55] in the asm)
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "={s[40:55]}"(plane) : "s"(rec) : "memory");

@@ -384,13 +384,25 @@ bool reenc_eligible(const rsg_codec_t* c, const bool* erased) {
     for (int i = 0; i < c->k; ++i) t += erased[i] ? 1 : 0;
     for (int i = c->k; i < c->k + c->r; ++i)
         if (erased[i]) return false;
-    if (!(t >= 1 && 10 * t >= 9 * c->r && c->k - t >= 64)) return false;
-    // an erased set closed under x -> x^16 (or a smaller Frobenius step) gives the plain route a k_bs16
-    // second stage with orbits of >= 4 rows (bs16_host): cheaper than re-encoding + the dense t x r stage
+    return t >= 1 && 10 * t >= 9 * c->r && c->k - t >= 64;
+}
+
+// The route plan of a decode pattern, built when its dense plan has moved route_min_bytes. Among the
+// re-encode-eligible patterns, one whose erased set is closed under x -> x^(2^d), d <= 4, may give the plain
+// route a k_bs16 second stage over orbits of >= 4 rows -- cheaper than re-encoding plus the dense t x r
+// stage -- but only when bs16_host accepts its rows (orbit runs of at least 2 rows on average): so the plain
+// route is built, and replaced by the re-encode decode when its second stage came out dense (no speed cliff).
+int make_plan_route(rsg_codec_t* c, const bool* erased, bool reenc_ok, std::unique_ptr<DevPlan>& out,
+                    hipStream_t st) {
+    if (!reenc_ok || !reenc_eligible(c, erased)) return make_plan_cs(c, erased, out, st);
     std::vector<uint16_t> pos;
     for (int i = 0; i < c->k; ++i)
         if (erased[i]) pos.push_back(c->positions[size_t(i)]);
-    return orbit_step(pos) > 4;
+    if (orbit_step(pos) > 4) return make_plan_reenc(c, erased, out, st);
+    if (int rc = make_plan_cs(c, erased, out, st)) return rc;
+    if (out->second && out->second->cs && out->second->cs->kind == 1) return 0;  // the k_bs16 orbit stage
+    out.reset();  // never launched: its memory goes back to the pool behind its upload
+    return make_plan_reenc(c, erased, out, st);
 }
 
 int make_plan_reenc(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st) {

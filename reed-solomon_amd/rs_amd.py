@@ -79,6 +79,7 @@ _sig("rs_restore_symbols", ctypes.c_int, P, u16, u16, ctypes.POINTER(SymbolSeqT)
 _sig("rsg_codec_create", ctypes.c_int, ctypes.c_int, u16, u16, ctypes.POINTER(P))
 _sig("rsg_codec_destroy", None, P)
 _sig("rsg_codec_subfield", ctypes.c_int, P)
+_sig("rsg_codec_trim", ctypes.c_int, P)
 _sig("rsg_set_option", ctypes.c_int, P, ctypes.c_char_p, i64)
 _sig("rsg_last_kernel", ctypes.c_char_p, P)
 _sig("rsg_last_work", ctypes.c_int, P, P, P)
@@ -465,6 +466,12 @@ class Codec:
         rc = _lib.rsg_set_option(self._h, name.encode(), int(value))
         if rc:
             raise RSError(rc, f"rsg_set_option({name})")
+
+    def trim(self):
+        """Frees the codec's grow-only device scratch after its outstanding work (rsg_codec_trim)."""
+        rc = _lib.rsg_codec_trim(self._h)
+        if rc:
+            raise RSError(rc, "rsg_codec_trim")
 
     def encode(self, stripes, n_stripes=None, symbol_size=None, stream=None, check=True):
         """Repair symbols of `stripes` ([n, k + r, S] uint8, contiguous, on this device), in place."""

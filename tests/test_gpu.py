@@ -524,7 +524,9 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
     cdc = rs_amd.Codec(k, r)
     cdc.set_option("m16_ps_chunk", chunk)
     cdc.set_option("m16_ps_overlap", overlap)
-    for _ in range(2):  # the second call reuses the streams, events and buffers
+    for it in range(3):  # the second call reuses the streams, events and buffers; the third regrows them
+        if it == 2:
+            cdc.trim()
         dev.copy_(torch.from_numpy(host))
         assert cdc.decode_batch(dev, pats) == 0
         torch.cuda.synchronize()
@@ -953,6 +955,55 @@ def test_m16_reenc_decode(k, r, t, S):
             ref = poisoned[s].copy()
             assert oracle_decode(k, r, ref, er, int(er.sum())) == 0
             assert np.array_equal(outs[0][s], ref)
+
+
+def test_m16_reenc_when_orbit_stage_is_dense():
+    """A re-encode-eligible pattern (information erasures only, t >= 0.9 r) closed under x -> x^16 whose erased
+    slots interleave two orbits per coset (slots a, a + 1, a + 4, a + 5, ... of each 16-slot coset): the orbit
+    rows do not form runs, so k_bs16 cannot take the plain route's second stage. The route plan is then the
+    re-encode decode (rs_route16.cpp:make_plan_route), not the plain route with a dense t x r stage; both
+    bit-exact vs the oracle."""
+    from _util import oracle_positions
+    k, r, S, n = 1000, 256, 1024, 2
+    pos = oracle_positions(k, r).astype(np.int64)
+    runs, i = [], 0
+    while i < k:  # 16-slot cosets among the information slots
+        j = i + 1
+        while j < k + r and j - i < 16 and pos[j] == (2 * pos[j - 1]) % 65535:
+            j += 1
+        if j - i == 16 and j <= k:
+            runs.append(i)
+        i = j
+    er = np.zeros(k + r, bool)
+    for a in runs[:29]:
+        er[[a + d for d in (0, 1, 4, 5, 8, 9, 12, 13)]] = True
+    t = int(er.sum())
+    assert t == 232 and 10 * t >= 9 * r
+    rng = np.random.default_rng(77)
+    host = np.zeros((n, k + r, S), np.uint8)
+    host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_route_min_bytes", 0)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    poisoned = got.copy()
+    poisoned[:, er] = 0
+    for reenc in (1, 0):
+        codec.set_option("m16_reenc", reenc)
+        dev.copy_(torch.from_numpy(poisoned))
+        codec.decode(dev, er)
+        torch.cuda.synchronize()
+        if reenc:
+            assert "+bs16+xor+" in codec.last_kernel, codec.last_kernel
+        else:
+            assert codec.last_kernel.startswith(CS_DEFAULT + "+apply"), codec.last_kernel
+        out = dev.cpu().numpy()
+        for s in range(n):
+            ref = poisoned[s].copy()
+            assert oracle_decode(k, r, ref, er, t) == 0
+            assert np.array_equal(out[s], ref), (reenc, s)
 
 
 def test_drop_in_arena_mixed_layouts():
