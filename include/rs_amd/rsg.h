@@ -49,10 +49,14 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "batch_plans"  rsg_decode_batch: 0 host plans per distinct pattern; 1 device-built plans (GF(256):
  *                  per stripe; GF(2^16): see m16_ps); 2 device plans past 16 distinct patterns for GF(256)
  *                  codes and past one pattern for GF(2^16) codes (default)
- *   "syn_route"    GF(256) device-plan decodes (S a multiple of 2 KiB): 1 syndromes of every slot on the
- *                  bit-plane XOR kernel, then a per-stripe t_info x t solve (default); 0 survivor matrices
- *   "m8_syn_overlap" that route's plans + syndromes of the next chunk on a codec stream beside this chunk's
- *                  solve (two buffer sets; 1 default), 0 one stream
+ *   "syn_route"    GF(256) device-plan decodes (S a multiple of 2 KiB): 2 the re-encode differences
+ *                  [G | I] of every slot on the bit-plane XOR kernel, then a per-stripe t_info x t_info
+ *                  solve from the first t_info surviving repair rows (default); 1 syndromes of every slot
+ *                  on that kernel, then a t_info x t solve; 0 survivor matrices
+ *   "m8_syn_overlap" that route's plans + fixed pass of the next chunk on a codec stream beside this
+ *                  chunk's solve (two buffer sets), 0 one stream (default)
+ *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 1 one dword per lane
+ *                  without the ring, 2 two dwords per lane
  *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
  *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
  *                  0 one plan per pattern rebuilt on the stream

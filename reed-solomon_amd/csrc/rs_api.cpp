@@ -177,8 +177,14 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->m8_syn_overlap = int(value);
         return 0;
     }
-    if (!std::strcmp(name, "syn_route")) {
-        if (value < 0 || value > 1) return RS_ERR_INVALID;
+    if (!std::strcmp(name, "syn_route")) {  // 0 survivor plans, 1 syndromes, 2 re-encode differences
+        if (value < 0 || value > 2) return RS_ERR_INVALID;
+        if (c->syn && int(value) != c->syn_route) {  // the fixed pass's plan changes with it
+            HIP_TRY(hipSetDevice(c->device));
+            HIP_TRY(hipDeviceSynchronize());
+            c->syn.reset();
+            c->syn_failed = false;
+        }
         c->syn_route = int(value);
         return 0;
     }

@@ -55,10 +55,22 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
         int64_t(n) * symbol_stride >= (int64_t(1) << 31) || int64_t(c->r) * int64_t(S) >= (int64_t(1) << 31))
         return false;
     if (!c->syn) {
-        const Field& F = field();
+        // syn_route 1: the r syndromes, H[j][i] = X_i^j over all k + r slots (reed_solomon.c:443-559);
+        // 2: the re-encode differences [G | I] (k_plan_reenc_m8), G = the encode matrix, I on the repair slots
         std::vector<uint16_t> H(size_t(c->r) * n);
-        for (int j = 0; j < c->r; ++j)
-            for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(c->positions[i]) * j) % kN];
+        if (c->syn_route == 2) {
+            std::vector<uint16_t> G;
+            std::vector<int32_t> gi, go;
+            codec_matrix(c->positions, c->k, c->r, nullptr, G, gi, go);  // r x k
+            for (int p = 0; p < c->r; ++p) {
+                for (int i = 0; i < c->k; ++i) H[size_t(p) * n + i] = G[size_t(p) * c->k + i];
+                H[size_t(p) * n + c->k + p] = 1;
+            }
+        } else {
+            const Field& F = field();
+            for (int j = 0; j < c->r; ++j)
+                for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(c->positions[i]) * j) % kN];
+        }
         std::vector<int32_t> in(n), out(c->r);
         for (int i = 0; i < n; ++i) in[size_t(i)] = i;
         for (int j = 0; j < c->r; ++j) out[size_t(j)] = j;
@@ -113,21 +125,19 @@ uint64_t hash_bytes(const uint8_t* p, size_t len) {
 // the tail kernel) applies every stripe's own plan. Stripes without erased information slots are
 // skipped; the caller has validated every pattern.
 int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
-                              uint64_t n_stripes, uint64_t S, const bool* is_erased, hipStream_t st) {
+                              uint64_t n_stripes, uint64_t S, const bool* is_erased, const int32_t* tr,
+                              hipStream_t st) {
     const size_t n = size_t(c->k) + c->r;
     if ((S & 1) || (uintptr_t(base) % 8) || (stripe_stride % 8) || (symbol_stride % 8)) return RS_ERR_INVALID;
     std::vector<int32_t> ids;
-    std::vector<uint8_t> masks;
-    masks.reserve(size_t(n_stripes) * n);
-    for (uint64_t s = 0; s < n_stripes; ++s) {
-        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
-        if (!count_nonzero(e, c->k)) continue;
-        ids.push_back(int32_t(s));
-        const size_t o = masks.size();
-        masks.resize(o + n);
-        for (size_t i = 0; i < n; ++i) masks[o + i] = e[i] != 0;
-    }
+    for (uint64_t s = 0; s < n_stripes; ++s)
+        if (tr[2 * s + 1]) ids.push_back(int32_t(s));
     if (ids.empty()) return 0;
+    std::vector<uint8_t> masks(ids.size() * n);
+    for (size_t j = 0; j < ids.size(); ++j) {
+        const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + size_t(ids[j]) * n);
+        for (size_t i = 0; i < n; ++i) masks[j * n + i] = e[i] != 0;
+    }
     int rc = scratch_acquire(c, st);
     if (rc) return rc;
     const uint16_t* logt = nullptr;
@@ -157,11 +167,12 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
         return rc;
     if (syn_prepare(c, S, symbol_stride)) {
-        // syndrome route: the t_info x t solves (k_plan_syn_m8), the r syndromes of every selected stripe
-        // into scratch (XOR kernel, dst indexed by the chunk-local stripe), then the per-stripe solves
-        // from the syndromes XORed into the erased information slots (not zeroed first: V1Args::xor_dst).
-        // Option m8_syn_overlap (default): plans and syndromes of chunk i + 1 run on the codec's syndrome
-        // stream beside chunk i's solve on the caller's stream, two buffer sets alternating.
+        // syndrome / re-encode route: the per-stripe solves (k_plan_syn_m8 / k_plan_reenc_m8), the fixed
+        // pass's r outputs of every selected stripe into scratch (XOR kernel, dst indexed by the
+        // chunk-local stripe), then the per-stripe solves from those XORed into the erased information
+        // slots (not zeroed first: V1Args::xor_dst). Option m8_syn_overlap: plans and fixed pass of chunk
+        // i + 1 run on the codec's syndrome stream beside chunk i's solve on the caller's stream, two
+        // buffer sets alternating.
         const uint16_t* expt = nullptr;
         if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
         const int64_t per = int64_t(c->r) * int64_t(S);
@@ -201,7 +212,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             pa.in_stride = in_stride;
             pa.out_stride = out_stride;
             pa.idx_stride = idx_stride;
-            HIP_TRY(launch_plan_syn_m8(pa, cn, sy));
+            HIP_TRY(launch_plan_syn_m8(pa, cn, sy, c->syn_route));
             uint8_t* syn = static_cast<uint8_t*>(c->d_syn) + set * sch * per;
             if ((rc = run_plan(c, *c->syn, base, stripe_stride, symbol_stride, syn, per, int64_t(S), uint64_t(cn), S,
                                sy, c->d_ids + c0, true)))
@@ -230,7 +241,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
-        c->last_kernel = ovl ? "syn_xj+apply_m8_v1_ps(overlap)" : "syn_xj+apply_m8_v1_ps";
+        c->last_kernel = std::string(c->syn_route == 2 ? "reenc_xj" : "syn_xj") + "+apply_m8_v1_ps" + (ovl ? "(overlap)" : "");
         return scratch_release(c, st);
     }
     for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {
@@ -623,6 +634,16 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     std::vector<Group> groups;
     std::unordered_map<uint64_t, std::vector<size_t>> by_hash;
     std::vector<int32_t> tr(size_t(n_stripes) * 2);  // per stripe: t, R
+    // The groups matter only while a host-plan route can still be taken: once their count passes the
+    // point where a device-plan route takes over, the remaining stripes are validated, not grouped
+    // (at 4096 all-distinct patterns the hashing and per-group lists were ~0.5 ms of host time).
+    const bool dev_m8 = c->m <= 8 && n <= 256 && (c->batch_plans == 1 || c->batch_plans == 2);
+    const bool dev_m16 = c->m > 8 && (c->batch_plans == 1 || c->batch_plans == 2) &&
+                         ps16_eligible(c, symbol_size, int64_t(stripe_stride), int64_t(symbol_stride), d_rcv);
+    const size_t group_cap = (dev_m8 || dev_m16) && c->batch_plans == 1 ? 0
+                             : dev_m8                                     ? kHostPlanGroups
+                             : dev_m16                                    ? 1
+                                                                          : SIZE_MAX;
     for (uint64_t s = 0; s < n_stripes; ++s) {
         const uint8_t* e = reinterpret_cast<const uint8_t*>(is_erased + s * n);
         const size_t R = count_nonzero(e, c->k), t = R + count_nonzero(e + c->k, c->r);
@@ -631,6 +652,7 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         tr[2 * s + 1] = int32_t(R);
         if (!R) continue;  // nothing to restore (erased repair slots are never written)
         if (s > uint64_t(INT32_MAX)) return RS_ERR_INVALID;
+        if (groups.size() > group_cap) continue;
         std::vector<size_t>& cand = by_hash[hash_bytes(e, n)];
         size_t g = 0;
         while (g < cand.size() && std::memcmp(groups[cand[g]].key, e, n)) ++g;
@@ -643,13 +665,11 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     if (groups.empty() || !symbol_size) return 0;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (c->m <= 8 && n <= 256 &&
-        (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups)))
+    if (dev_m8 && (c->batch_plans == 1 || groups.size() > kHostPlanGroups))
         return decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
-                                         int64_t(symbol_stride), n_stripes, symbol_size, is_erased, st);
+                                         int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st);
     // GF(2^16): more than one pattern -> per-stripe plans on the syndrome route (one shared syndrome pass)
-    if (c->m > 8 && (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > 1)) &&
-        ps16_eligible(c, symbol_size, int64_t(stripe_stride), int64_t(symbol_stride), d_rcv))
+    if (dev_m16 && (c->batch_plans == 1 || groups.size() > 1))
         return decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride), int64_t(symbol_stride),
                                    n_stripes, symbol_size, is_erased, tr.data(), st);
     std::vector<int32_t> ids;

@@ -295,12 +295,14 @@ struct rsg_codec {
     // rsg_decode_batch with device-built per-stripe plans (k_plan_m8): 0 = host plans per distinct
     // pattern, 1 = device plans, 2 = device plans when more than kHostPlanGroups patterns (default)
     int batch_plans = 2;
-    // device-plan decodes of m <= 8 codes: 1 = syndrome route (fixed r x (k + r) syndrome matrix on the
-    // XOR kernel, then a per-stripe t_info x t solve), 0 = per-stripe survivor matrices (k_plan_m8)
-    int syn_route = 1;
-    // option m8_syn_overlap: that route's plans and syndromes of chunk i + 1 on the codec's syndrome stream
-    // beside chunk i's solve (two buffer sets); 0 = one stream
-    int m8_syn_overlap = 1;
+    // device-plan decodes of m <= 8 codes: 2 = re-encode route (fixed r x (k + r) matrix [G | I] on the
+    // XOR kernel, then a per-stripe t_info x t_info solve; default), 1 = syndrome route (H, then a t_info x t
+    // solve), 0 = per-stripe survivor matrices (k_plan_m8)
+    int syn_route = 2;
+    // option m8_syn_overlap: that route's plans and fixed pass of chunk i + 1 on the codec's syndrome stream
+    // beside chunk i's solve (two buffer sets); 0 = one stream (default: two VALU-bound kernels side by side
+    // ran no faster than in sequence, profiles/r4/ps8_route2.md)
+    int m8_syn_overlap = 0;
     // option m8_ps_kernel: the per-stripe GF(256) solve's kernel: 0 k_apply_m8_v1 (LDS input ring), 1
     // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
     // two dwords per lane)

@@ -1531,6 +1531,98 @@ __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
     }
 }
 
+// Re-encode plans (SynPlanArgs, syn_route 2). The codec's fixed pass computes, for every repair slot P,
+//   S'_P = (G rcv_info)_P + rcv_P          (G the encode matrix: [G | I] on the bit-plane XOR kernel)
+// which is zero for a codeword. With d the differences on the erased slots (erased information slots hold
+// their old contents g, d_Q = g_Q + c_Q; erased repair slots likewise), S'_P = sum_{Q in E_i} G[P][Q] d_Q for
+// every surviving repair slot P. The first t_i = |E_i| of them (R', in slot order; t <= r leaves enough)
+// give a square system, and because G[P][Q] = L_E(Y_Q) / (L_E'(X_P) (X_P + Y_Q)) (gf16.cpp:solve_matrix, E
+// = the repair positions) is a scaled Cauchy matrix, its inverse is again of that form:
+//   W[Q][P] = L_T(X_P) / ((X_P + Y_Q) L_T'(Y_Q)),   T = E_i + (repair slots not in R'), |T| = r,
+// i.e. solve_matrix with targets T, emitted rows E_i, sources R' -- the same evaluation as k_plan_m8.
+// d = W S'_{R'} is then XORed into the erased information slots (V1Args::xor_dst). A t_i x t_i solve from
+// t_i rows of a pattern-independent pass over k + r inputs whose matrix is G plus an identity, against the
+// syndrome route's t_i x t solve after a pass of r x (k + r) Vandermonde rows.
+__global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
+    __shared__ uint16_t tx[256], px[256], qx[256];
+    __shared__ int32_t ps[256], qs[256];
+    __shared__ uint32_t lp[256], ld[256];
+    __shared__ int cnt[4][3];
+    constexpr uint32_t N = 65535u;
+    const int64_t s = blockIdx.x;
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const bool valid = j < a.n;
+    const bool er = valid && a.masks[s * a.n + j] != 0;
+    const bool inf_er = er && j < a.k, rep_ok = valid && j >= a.k && !er;
+    const uint64_t bp = __ballot(inf_er), bq = __ballot(rep_ok);
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    if (lane == 0) {
+        cnt[w][0] = __popcll(bp);
+        cnt[w][1] = __popcll(bq);
+    }
+    __syncthreads();
+    int op = 0, oq = 0, R = 0;
+    for (int v = 0; v < 4; ++v) {
+        if (v < w) op += cnt[v][0], oq += cnt[v][1];
+        R += cnt[v][0];
+    }
+    const uint16_t xj = valid ? a.elem[j] : 0;
+    const int qi = oq + __popcll(bq & below);  // rank among the surviving repair slots
+    if (inf_er) {
+        const int i = op + __popcll(bp & below);
+        px[i] = xj;
+        ps[i] = j;
+    }
+    const bool in_rp = rep_ok && qi < R;  // one of the first R survivors: a source of the solve
+    if (in_rp) {
+        qx[qi] = xj;
+        qs[qi] = j - a.k;
+    }
+    const bool in_t = inf_er || (valid && j >= a.k && !in_rp);
+    const uint64_t bt = __ballot(in_t);
+    if (lane == 0) cnt[w][2] = __popcll(bt);
+    __syncthreads();
+    int ot = 0, T = 0;
+    for (int v = 0; v < 4; ++v) {
+        if (v < w) ot += cnt[v][2];
+        T += cnt[v][2];
+    }
+    if (in_t) tx[ot + __popcll(bt & below)] = xj;
+    __syncthreads();
+    // log L_T(Y_q) for the sources, log L_T'(X_p) for the emitted rows (solve_matrix's lp / ld)
+    if (j < R) {
+        uint32_t sp = 0, sd = 0;
+        for (int e = 0; e < T; ++e) {
+            sp += a.logt[qx[j] ^ tx[e]];
+            if (tx[e] != px[j]) sd += a.logt[px[j] ^ tx[e]];
+        }
+        lp[j] = sp % N;
+        ld[j] = sd % N;
+    }
+    if (j == 0) {
+        a.kr[2 * s] = R;  // K = R: t_i inputs, t_i outputs
+        a.kr[2 * s + 1] = R;
+    }
+    __syncthreads();
+    int32_t* pin = a.pin + s * a.in_stride;
+    for (int q = j; q < a.in_stride; q += 256) pin[q] = q < R ? int32_t(s * a.r + qs[q]) : 0;
+    int32_t* pout = a.pout + s * a.out_stride;
+    for (int p = j; p < a.out_stride; p += 256) pout[p] = p < R ? ps[p] : 0;
+    // row j of the V = 1 records [tile][K][64]: gamma-basis byte of W[j][q] split into nibbles
+    uint32_t* rec = a.pidx + s * a.idx_stride;
+    const int ntiles = (R + 31) / 32;
+    if (j < ntiles * 32) {
+        const int tile = j >> 5, jj = j & 31;
+        uint32_t* r0 = rec + size_t(tile) * R * 64;
+        for (int q = 0; q < R; ++q) {
+            uint32_t b = 0;
+            if (j < R) b = a.g8[((lp[q] + 2 * N - ld[j] - a.logt[px[j] ^ qx[q]]) % N) / 257u];
+            r0[size_t(q) * 64 + jj] = b & 15u;
+            r0[size_t(q) * 64 + 32 + jj] = b >> 4;
+        }
+    }
+}
+
 // Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
 // coefficients from the nibble records, multiplication by masked gamma-multiples.
 __global__ void __launch_bounds__(256) k_apply_m8_ps_tail(V1Args a, int64_t col0, int64_t nbytes) {
@@ -1968,9 +2060,12 @@ hipError_t launch_plan_m8(const PlanArgs& a, int64_t n_sel, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st) {
+hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st, int kind) {
     if (n_sel <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_plan_syn_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    if (kind == 2)
+        hipLaunchKernelGGL(k_plan_reenc_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_plan_syn_m8, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

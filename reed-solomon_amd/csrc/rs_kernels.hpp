@@ -69,7 +69,8 @@ struct SynPlanArgs {
     uint32_t* pidx;        // [n_sel][idx_stride] V = 1 nibble records
     int64_t in_stride, out_stride, idx_stride;
 };
-hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st);
+// kind 1: syndrome-route solves (k_plan_syn_m8); 2: re-encode solves (k_plan_reenc_m8)
+hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st, int kind = 1);
 
 // One GF(2^16) coding matrix built on the device (gf16.cpp:solve_matrix's evaluation) straight into
 // the m = 16 kernels' formats: coefficient tiles (k_apply_m16) and, if rec != null, the packed index

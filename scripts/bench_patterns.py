@@ -47,23 +47,27 @@ mask = torch.from_numpy(pats).to("cuda")
 def run(codec, label, reps):
     if only is not None and label not in only:
         return
-    times = []
+    times, host = [], []
     for _ in range(reps):
         dev.masked_fill_(mask[:, :, None], 0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         codec.decode_batch(dev, pats)
+        host.append(time.perf_counter() - t0)  # the call returns once every launch is queued
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     ok = bool(torch.equal(fp(), ref_fp))
     ms = float(np.median(times)) * 1e3
     print(json.dumps({"case": label, "stripes": n, "patterns": mode, "ms": round(ms, 3),
-                      "GBps": round(alg / ms / 1e6, 1), "restored": ok, "kernel": codec.last_kernel}), flush=True)
+                      "GBps": round(alg / ms / 1e6, 1), "host_ms": round(float(np.median(host)) * 1e3, 3),
+                      "restored": ok, "kernel": codec.last_kernel}), flush=True)
 
 
 syn = rs_amd.Codec(k, r, batch_plans=1)
-if os.environ.get("RS_PS8_NO_OVERLAP"):  # A/B of the overlapped chunks (option m8_syn_overlap)
-    syn.set_option("m8_syn_overlap", 0)
+if os.environ.get("RS_PS8_OVERLAP"):  # A/B of the overlapped chunks (option m8_syn_overlap)
+    syn.set_option("m8_syn_overlap", int(os.environ["RS_PS8_OVERLAP"]))
+if os.environ.get("RS_PS8_ROUTE"):  # A/B of the fixed pass (option syn_route: 1 syndromes, 2 re-encode)
+    syn.set_option("syn_route", int(os.environ["RS_PS8_ROUTE"]))
 if os.environ.get("RS_PS8_KERNEL"):  # A/B of the per-stripe solve kernel (option m8_ps_kernel)
     syn.set_option("m8_ps_kernel", int(os.environ["RS_PS8_KERNEL"]))
 run(syn, "device_plans_syndrome", 5)

@@ -17,4 +17,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   rc=$?; echo "pass $i rc=$rc"
   case $rc in 0) ;; *) tail -3 $D/p$i.log; exit $rc;; esac
 done
-for k in "k_apply_m8_v1<0>" rs_xj_ k_plan_syn_m8; do echo "== $k"; python3 scripts/pmc_summary.py $D "$k"; done
+for k in "k_apply_m8_v1<0>" k_apply_m8_ps_w rs_xj_ k_plan_; do echo "== $k"; python3 scripts/pmc_summary.py $D "$k"; done

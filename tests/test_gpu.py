@@ -535,13 +535,14 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
 
 
 @pytest.mark.parametrize("route,ovl,kern", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1), (0, 0, 1), (1, 0, 2),
-                                            (1, 1, 2), (0, 0, 2)])
+                                            (1, 1, 2), (0, 0, 2), (2, 0, 0), (2, 1, 0), (2, 0, 2), (2, 1, 2)])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
     the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
-    first; ovl 1: chunk i + 1's plans and syndromes on the codec's second stream beside chunk i's solve)
+    first; route 2: the re-encode differences [G | I] of every slot, then a t_info x t_info Cauchy-inverse
+    solve from the first t_info surviving repair rows; ovl 1: chunk i + 1's plans and syndromes on the codec's second stream beside chunk i's solve)
     and the survivor-matrix route (0). Erased slots hold garbage, not zeros: information slots come back
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
@@ -572,8 +573,9 @@ def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     poisoned = dev.clone()
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
+    fixed = {1: "syn_xj", 2: "reenc_xj"}.get(route)
     assert codec.last_kernel == ("apply_m8_v1_ps" if not route else
-                                 "syn_xj+apply_m8_v1_ps(overlap)" if ovl else "syn_xj+apply_m8_v1_ps")
+                                 fixed + "+apply_m8_v1_ps" + ("(overlap)" if ovl else "")), codec.last_kernel
     assert torch.equal(dev[:, :k], full[:, :k])
     rep_er = mask.clone()
     rep_er[:, :k] = False
