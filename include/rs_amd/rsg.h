@@ -43,8 +43,9 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  (default)
  *   "dec_jit_uses" launches of >= 1 MiB before a decode plan is specialised under jit = 2 (default 2)
  *   "xj"           specialised family: 1 bit-plane XOR kernels (default), 0 nibble-table kernels
- *   "m8_mode"      GF(256) kernel without specialisation: 18 one dword per lane, gpr-index lookups
- *                  (default); 2 two dwords per lane; 0 register tables, compiler indexing; 1 masked
+ *   "m8_mode"      GF(256) kernel without specialisation: 20 one dword per lane, one nibble table per
+ *                  input, two accumulator sets, gpr-index lookups (default); 18 the same with two tables
+ *                  and one accumulator set; 2 two dwords per lane; 0 register tables, compiler indexing; 1 masked
  *                  multiples; 3, 4, 14 other register layouts of the gpr-index kernels
  *   "batch_plans"  rsg_decode_batch: 0 host plans per distinct pattern; 1 device-built plans (GF(256):
  *                  per stripe; GF(2^16): see m16_ps); 2 device plans past 16 distinct patterns for GF(256)
@@ -56,7 +57,7 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m8_syn_overlap" that route's plans + fixed pass of the next chunk on a codec stream beside this
  *                  chunk's solve (two buffer sets), 0 one stream (default)
  *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 1 one dword per lane
- *                  without the ring, 2 two dwords per lane
+ *                  without the ring, 2 two dwords per lane, 3 the ring kernel with one nibble table
  *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
  *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
  *                  0 one plan per pattern rebuilt on the stream

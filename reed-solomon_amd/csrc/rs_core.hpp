@@ -247,7 +247,9 @@ struct rsg_codec {
     std::unique_ptr<rsamd::DevPlan> enc;
     std::map<std::vector<uint8_t>, std::unique_ptr<rsamd::DevPlan>> dec;
     std::vector<std::vector<uint8_t>> dec_lru;
-    int m8_mode = 18;
+    // generic GF(256) kernel: 20 = V = 1 with one nibble table per input (k_apply_m8_v1<2>; 10 % under 18 at
+    // K = 128, profiles/r4/v1h_ab.log), 18 = the two-table V = 1 step
+    int m8_mode = 20;
     int m16_mode = 0;  // m = 16 kernels: 0 hand-scheduled (64-row tiles), 1 its timing ablation, 2 compiled
     int m16_plans = 2;  // m = 16 plans: 0 host, 1 device (build_plan_m16_device), 2 device above 64K coefficients
     int m16_route = 1;  // m = 16 matrices with K >= 64: 1 syndrome route (k_cs16 + D x R apply), 0 dense, 2 all
@@ -305,7 +307,7 @@ struct rsg_codec {
     int m8_syn_overlap = 0;
     // option m8_ps_kernel: the per-stripe GF(256) solve's kernel: 0 k_apply_m8_v1 (LDS input ring), 1
     // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
-    // two dwords per lane)
+    // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input)
     int m8_ps_kernel = 0;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;

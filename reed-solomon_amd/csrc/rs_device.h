@@ -111,11 +111,34 @@ __device__ __forceinline__ void wait_vm() {
 
 // ------------------------------------------ m <= 8, one dword per lane per input step (V = 1)
 constexpr int V1_LDS_WORDS = 2048 + RING_SLOTS * 256;
+// NB = 2 (one-table step, gen_asm.py v1h): a third 1024-dword table after the ring, L^-1 of (gamma^4 x) per
+// coordinate byte, so the output stage converts A + gamma^4 B as L^-1(A) ^ G4(B)
+constexpr int V1H_G4 = V1_LDS_WORDS;
+constexpr int V1H_LDS_WORDS = V1_LDS_WORDS + 1024;
 
-// The V = 1 kernels' outputs: row p of the tile (accumulator a0[p] / a1[p - 16], GF(256)^2 coordinates) back
-// to GF(2^16) words and stored to dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst).
+// gamma^4 * v for one GF(256) byte in gamma-basis coordinates (xt8's reduction, four times)
+__device__ __forceinline__ uint32_t gmul_g4(uint32_t v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v = ((v << 1) & 0xFEu) ^ ((v >> 7) * 0x1Du);
+    return v;
+}
+
+// Output p of the tile in GF(2^16) words: accumulator a0[p] / a1[p - 16] (GF(256)^2 coordinates) through
+// L^-1; NB = 2 adds gamma^4 times b0[p] / b1[p - 16] through the G4 table.
+template <int NB>
+__device__ __forceinline__ uint32_t m8_v1_out(const uint32_t* lt, int p, const u32x16& a0, const u32x16& a1,
+                                              const u32x16& b0, const u32x16& b1) {
+    uint32_t w = lds_lookup4(lt + 1024, p < 16 ? a0[p & 15] : a1[p & 15]);
+    if constexpr (NB == 2) w ^= lds_lookup4(lt + V1H_G4, p < 16 ? b0[p & 15] : b1[p & 15]);
+    return w;
+}
+
+// The V = 1 kernels' outputs: row p of the tile back to GF(2^16) words (m8_v1_out) and stored to
+// dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst).
+template <int NB>
 __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt, uint8_t* dst, const int32_t* out,
-                                            int rows, const u32x16& a0, const u32x16& a1) {
+                                            int rows, const u32x16& a0, const u32x16& a1, const u32x16& b0,
+                                            const u32x16& b1) {
     if (a.xor_dst) {  // g ^ (W S): the old contents, loaded 8 at a time ahead of their stores
 #pragma unroll
         for (int p0 = 0; p0 < 32; p0 += 8) {
@@ -127,21 +150,17 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int p = p0 + q;
-                if (p < rows) {
-                    const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
+                if (p < rows)
                     *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) =
-                        lds_lookup4(lt + 1024, v) ^ old[q];
-                }
+                        m8_v1_out<NB>(lt, p, a0, a1, b0, b1) ^ old[q];
             }
         }
         return;
     }
 #pragma unroll
     for (int p = 0; p < 32; ++p) {
-        if (p < rows) {
-            const uint32_t v = p < 16 ? a0[p & 15] : a1[p & 15];
-            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) = lds_lookup4(lt + 1024, v);
-        }
+        if (p < rows)
+            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
     }
 }
 
@@ -151,9 +170,15 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
 // runs `step(y, i, tile, acc0_15, acc16_31, record)` per input (record: the plan's 64-dword nibble
 // record of (tile, input)); one s_barrier per batch. Outputs go back through L^-1 into 4-byte
 // stores. With per-stripe plans (a.ps_kr) K, R, the slot lists and the records are the stripe's own.
-template <class Step>
+// NB = 2: the step also takes the second accumulator set (step(y, i, tile, a0, a1, b0, b1, record)) and
+// lds must hold V1H_LDS_WORDS. CB (1, 2 or 4): inputs converted to coordinates per LDS round trip.
+template <int NB = 1, int CB = 4, class Step>
 __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&& step) {
     for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
+    if constexpr (NB == 2) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 1024; i += 256) lds[V1H_G4 + i] = lds[1024 + (i & ~255) + gmul_g4(i & 255)];
+    }
     __syncthreads();
     const uint32_t* lt = lds;
     uint32_t* ring = lds + 2048;
@@ -206,7 +231,7 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
         else
             wait_vm<3>();
     };
-    u32x16 a0 = 0, a1 = 0;
+    u32x16 a0 = 0, a1 = 0, b0 = 0, b1 = 0;
     for (int b = 0; b < RING_B; ++b)
         if (4 * b + wave < K) issue(4 * b + wave);
     wait_mine(mine(1, RING_B - 1));
@@ -214,13 +239,23 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     for (int b = 0; b < nb; ++b) {
         const int ib = 4 * (b + RING_B) + wave;
         if (ib < K) issue(ib);
-        uint32_t y[4];  // slots past K hold stale bytes and are not used
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = lds_lookup4(lt, ring[((4 * b + j) % RING_SLOTS) * 256 + threadIdx.x]);
+        // the batch's inputs in coordinates (slots past K hold stale bytes and are not used), CB at a time
+        // (one LDS latency per CB inputs; each converted input held across the steps before its own costs a VGPR)
+        uint32_t y[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            if (j % CB == 0) {
+#pragma unroll
+                for (int q = j; q < j + CB; ++q) y[q] = lds_lookup4(lt, ring[((4 * b + q) % RING_SLOTS) * 256 + threadIdx.x]);
+            }
             const int i = 4 * b + j;
-            if (i < K) step(y[j], i, tile, a0, a1, idxb + (size_t(tile) * (a.ps_kr ? K : kfull) + i0 + i) * 64);
+            if (i < K) {
+                const uint32_t* rec = idxb + (size_t(tile) * (a.ps_kr ? K : kfull) + i0 + i) * 64;
+                if constexpr (NB == 2)
+                    step(y[j], i, tile, a0, a1, b0, b1, rec);
+                else
+                    step(y[j], i, tile, a0, a1, rec);
+            }
         }
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
@@ -231,8 +266,9 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
         uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 32) * cw + (chunk0 >> 2) + threadIdx.x;
 #pragma unroll
         for (int p = 0; p < 32; ++p)
-            if (p < rows) part[p * cw] = lds_lookup4(lt + 1024, p < 16 ? a0[p & 15] : a1[p & 15]);
+            if (p < rows) part[p * cw] = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
         return;
     }
-    m8_v1_store(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4, out_idx + tile * 32, rows, a0, a1);
+    m8_v1_store<NB>(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4, out_idx + tile * 32, rows,
+                    a0, a1, b0, b1);
 }

@@ -383,14 +383,36 @@ __device__ __forceinline__ void m8_v1_step(uint32_t y, const uint32_t* cp, u32x1
 #undef RS_M8_V1_OPERANDS
 }
 
+// One-table input step (gen_asm.py v1h): multiples y g^0..3, one nibble table, low-nibble lookups into
+// A = (a0, a1), high-nibble lookups of the same table into B = (b0, b1); the output is A + g^4 B.
+__device__ __forceinline__ void m8_v1h_step(uint32_t y, const uint32_t* cp, u32x16& a0, u32x16& a1, u32x16& b0,
+                                            u32x16& b1) {
+    const uint32_t k1d = 0x1D1D1D1Du;
+    u32x16 T;
+    asm volatile(
+#include "gen/m8_idx_asm_v1h.inc"
+        : "+{v[24:39]}"(a0), "+{v[40:55]}"(a1), "+{v[56:71]}"(b0), "+{v[72:87]}"(b1), "=&{v[8:23]}"(T)
+        : [y0] "v"(y), [cp] "s"(cp), [k1d] "v"(k1d)
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55",
+          "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71");
+}
+
 // V = 1 generic kernel (rs_device.h:m8_v1_run): per input, multiples + tables + 64 gpr-indexed
-// lookups with SMEM-fed indices. The matrix-specialised variant is rs_jit.cpp's rs_v1jit.
+// lookups with SMEM-fed indices. ABL 0: two tables (production v1), 1: v1 without gpr-index mode
+// (timing only), 2: the one-table step (m8_v1h_step, two accumulator sets). The matrix-specialised
+// variant is rs_jit.cpp's rs_v1jit.
 template <int ABL>
 __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
-    m8_v1_run(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
-        m8_v1_step<ABL>(y, rec, a0, a1);
-    });
+    if constexpr (ABL >= 2) {  // inputs converted 1 (ABL 2), 2 (3) or 4 (4) at a time
+        __shared__ __attribute__((aligned(16))) uint32_t lds[V1H_LDS_WORDS];
+        m8_v1_run<2, ABL == 2 ? 1 : ABL == 3 ? 2 : 4>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, u32x16& b0, u32x16& b1,
+                                 const uint32_t* rec) { m8_v1h_step(y, rec, a0, a1, b0, b1); });
+    } else {
+        __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
+        m8_v1_run(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
+            m8_v1_step<ABL>(y, rec, a0, a1);
+        });
+    }
 }
 
 // Per-stripe V = 1 apply without the LDS input ring, for the short solves of rsg_decode_batch (K = t <= r
@@ -427,8 +449,8 @@ __global__ void __launch_bounds__(256) k_apply_m8_ps_w(V1Args a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
     }
-    m8_v1_store(a, lt, a.dst + stripe * a.dst_stripe + col, a.out_idx + local * a.ps_out + tile * 32,
-                min(32, R - tile * 32), a0, a1);
+    m8_v1_store<1>(a, lt, a.dst + stripe * a.dst_stripe + col, a.out_idx + local * a.ps_out + tile * 32,
+                   min(32, R - tile * 32), a0, a1, a0, a1);
 }
 
 // The same with two dwords per lane (the "split" input step of k_apply_m8_idx / _lds, gen_asm.py): each
@@ -1174,11 +1196,12 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
         // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
         // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 split schedule with the multiply-based xtime,
         // 15 no gpr-index mode
-        if (a.mode == 18 || a.mode == 19) {  // V = 1 kernel (19: without gpr-index mode, timing only)
+        if (a.mode == 18 || a.mode == 19 || a.mode == 20) {  // V = 1 kernel (19: without gpr-index mode, timing
+                                                             // only; 20: the one-table step)
             const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
             if (full > 0) {
                 V1Args v = v1_args(a, full, nullptr);
-                v.kslices = a.mode == 18 ? m8_kslices(a, n_stripes, nullptr) : 1;
+                v.kslices = a.mode != 19 ? m8_kslices(a, n_stripes, nullptr) : 1;
                 v.partial = a.scratch;
                 dim3 g(unsigned(n_stripes * full), grid.y, unsigned(v.kslices));
 #ifdef RS_AMD_DIAG
@@ -1186,6 +1209,9 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
                     hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
                 else
 #endif
+                if (a.mode == 20)
+                    hipLaunchKernelGGL((k_apply_m8_v1<2>), g, dim3(256), 0, st, v);
+                else
                     hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
                 if (v.kslices > 1) {
                     const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
@@ -2084,6 +2110,12 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
         f.nchunks = full;
         if (kernel == 1)
             hipLaunchKernelGGL(k_apply_m8_ps_w, dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 3)
+            hipLaunchKernelGGL((k_apply_m8_v1<2>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 4)
+            hipLaunchKernelGGL((k_apply_m8_v1<3>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 5)
+            hipLaunchKernelGGL((k_apply_m8_v1<4>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
         else
             hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
     }

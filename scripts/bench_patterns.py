@@ -79,7 +79,8 @@ if only is None or "host_plans" in only:
 # the same bytes with one shared pattern (t = r information erasures): generic and specialised kernels
 one = np.zeros(k + r, bool)
 one[np.arange(r) * (k // r)] = True
-for label, kw in (("one_pattern_generic", dict(jit=0)), ("one_pattern_xj", dict())):
+gen_kw = dict(jit=0, m8_mode=int(os.environ.get("RS_PS8_M8MODE", "18")))  # A/B of the generic V = 1 step
+for label, kw in (("one_pattern_generic", gen_kw), ("one_pattern_xj", dict())):
     if only is not None and label not in only:
         continue
     c = rs_amd.Codec(k, r, **kw)

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 # matrix-specialised nibble-table V = 1 kernel (rs_v1jit), v1 / idx = generic gpr-index
 # kernels (one / two dwords per lane), table / mask = compiler-indexed reference kernels; "auto" is
 # the library default policy (JIT for encode, generic then JIT for repeated decode patterns)
-VARIANTS = {"jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(m8_mode=18, jit=0), "idx": dict(m8_mode=2, jit=0),
+VARIANTS = {"jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(m8_mode=18, jit=0), "v1h": dict(m8_mode=20, jit=0), "idx": dict(m8_mode=2, jit=0),
             "table": dict(m8_mode=0, jit=0), "mask": dict(m8_mode=1, jit=0), "auto": dict(), "cs_idx": dict()}
 # codec options of a variant (set after construction): "cs_idx" runs the GF(2^16) route's syndromes on
 # the gpr-indexed k_cs16 instead of the default threaded k_cs16t
@@ -535,7 +535,8 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
 
 
 @pytest.mark.parametrize("route,ovl,kern", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1), (0, 0, 1), (1, 0, 2),
-                                            (1, 1, 2), (0, 0, 2), (2, 0, 0), (2, 1, 0), (2, 0, 2), (2, 1, 2)])
+                                            (1, 1, 2), (0, 0, 2), (2, 0, 0), (2, 1, 0), (2, 0, 2), (2, 1, 2),
+                                            (2, 0, 3), (1, 0, 3), (0, 0, 3)])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
@@ -547,7 +548,7 @@ def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
     kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
-    LDS-ring kernel. S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
+    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
     ends in a partial column chunk."""
     if route and S % 2048:
         pytest.skip("the syndrome route covers whole 2 KiB columns (other sizes take the survivor route)")
