@@ -168,7 +168,10 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
-        if (value < 0 || value > 5) return RS_ERR_INVALID;
+        if (value < 0 || value > 6) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 6: timing ablation with wrong results
+        if (value == 6) return RS_ERR_INVALID;
+#endif
         c->m8_ps_kernel = int(value);
         return 0;
     }

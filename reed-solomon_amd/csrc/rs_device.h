@@ -133,35 +133,45 @@ __device__ __forceinline__ uint32_t m8_v1_out(const uint32_t* lt, int p, const u
     return w;
 }
 
+typedef int32_t i32x16s __attribute__((ext_vector_type(16)));
+
+// The 32 output slots of a tile (out[0..31], 16-byte aligned, read-only) into SGPRs: two SMEM loads and
+// one wait, instead of one scalar round trip per output.
+__device__ __forceinline__ void sload32(const int32_t* out, i32x16s& o0, i32x16s& o1) {
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(o0), "=s"(o1)
+                 : "s"(out)
+                 : "memory");
+}
+
 // The V = 1 kernels' outputs: row p of the tile back to GF(2^16) words (m8_v1_out) and stored to
-// dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst).
+// dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst: every old value is loaded first, so the
+// wave waits on one round of loads while it converts its outputs).
 template <int NB>
 __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt, uint8_t* dst, const int32_t* out,
                                             int rows, const u32x16& a0, const u32x16& a1, const u32x16& b0,
                                             const u32x16& b1) {
-    if (a.xor_dst) {  // g ^ (W S): the old contents, loaded 8 at a time ahead of their stores
+    i32x16s o0, o1;
+    sload32(out, o0, o1);
+    auto at = [&](int p) {
+        return reinterpret_cast<uint32_t*>(dst + int64_t(p < 16 ? o0[p & 15] : o1[p & 15]) * a.dst_sym);
+    };
+    if (a.xor_dst) {  // g ^ (W S), in rounds of LB loads (NB = 2 holds twice the accumulators)
+        constexpr int LB = NB == 2 ? 16 : 32;
 #pragma unroll
-        for (int p0 = 0; p0 < 32; p0 += 8) {
-            uint32_t old[8];
+        for (int p0 = 0; p0 < 32; p0 += LB) {
+            uint32_t old[LB];
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                old[q] = p0 + q < rows ? *reinterpret_cast<const uint32_t*>(dst + int64_t(sload(out + p0 + q)) * a.dst_sym)
-                                       : 0u;
+            for (int q = 0; q < LB; ++q) old[q] = p0 + q < rows ? *at(p0 + q) : 0u;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int p = p0 + q;
-                if (p < rows)
-                    *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) =
-                        m8_v1_out<NB>(lt, p, a0, a1, b0, b1) ^ old[q];
-            }
+            for (int q = 0; q < LB; ++q)
+                if (p0 + q < rows) *at(p0 + q) = m8_v1_out<NB>(lt, p0 + q, a0, a1, b0, b1) ^ old[q];
         }
         return;
     }
 #pragma unroll
-    for (int p = 0; p < 32; ++p) {
-        if (p < rows)
-            *reinterpret_cast<uint32_t*>(dst + int64_t(sload(out + p)) * a.dst_sym) = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
-    }
+    for (int p = 0; p < 32; ++p)
+        if (p < rows) *at(p) = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
 }
 
 // Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile

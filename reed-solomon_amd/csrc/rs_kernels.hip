@@ -2116,6 +2116,10 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
             hipLaunchKernelGGL((k_apply_m8_v1<3>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 5)
             hipLaunchKernelGGL((k_apply_m8_v1<4>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+#ifdef RS_AMD_DIAG
+        else if (kernel == 6)  // timing ablation: fixed table registers, no index switches (wrong results)
+            hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+#endif
         else
             hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
     }
