@@ -50,9 +50,10 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
     if (!std::strcmp(name, "m8_mode")) {
-        if (value < 0 || (value > 4 && value < 10) || value > 20) return RS_ERR_INVALID;
-#ifndef RS_AMD_DIAG  // 10-13, 15, 16, 19: timing ablations with wrong results; 17: s_memtime stamps
-        if ((value >= 10 && value <= 13) || (value >= 15 && value <= 17) || value == 19) return RS_ERR_INVALID;
+        if (value < 0 || (value > 4 && value < 10) || value > 21) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 10-13, 15, 16, 19: timing ablations with wrong results; 17, 21: s_memtime stamps
+        if ((value >= 10 && value <= 13) || (value >= 15 && value <= 17) || value == 19 || value == 21)
+            return RS_ERR_INVALID;
 #endif
         c->m8_mode = int(value);
         return 0;
@@ -168,9 +169,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
-        if (value < 0 || value > 6) return RS_ERR_INVALID;
-#ifndef RS_AMD_DIAG  // 6: timing ablation with wrong results
-        if (value == 6) return RS_ERR_INVALID;
+        if (value < 0 || value > 7) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 6: timing ablation with wrong results, 7: phase stamps
+        if (value >= 6) return RS_ERR_INVALID;
 #endif
         c->m8_ps_kernel = int(value);
         return 0;
@@ -359,7 +360,7 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
-    const bool m8_generic = p.m == 8 && p.d_idx && (a.mode == 18 || a.mode == 20) && !(xj_ok && p.xj) && !(jit_ok && p.jit);
+    const bool m8_generic = p.m == 8 && p.d_idx && (a.mode == 18 || a.mode == 20 || a.mode == 21) && !(xj_ok && p.xj) && !(jit_ok && p.jit);
     if ((p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) || m8_generic) {  // split-K scratch for small grids
         int64_t need = 0;
         if ((m8_generic ? m8_kslices(a, int64_t(n_stripes), &need) : m16_kslices(a, int64_t(n_stripes), &need)) > 1) {

@@ -238,6 +238,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_out = out_stride;
             v.ps_idx = idx_stride;
             v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
+            v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
             HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }

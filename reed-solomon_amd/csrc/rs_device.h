@@ -182,14 +182,19 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
 // stores. With per-stripe plans (a.ps_kr) K, R, the slot lists and the records are the stripe's own.
 // NB = 2: the step also takes the second accumulator set (step(y, i, tile, a0, a1, b0, b1, record)) and
 // lds must hold V1H_LDS_WORDS. CB (1, 2 or 4): inputs converted to coordinates per LDS round trip.
-template <int NB = 1, int CB = 4, class Step>
+// STAMP (diagnostic kernels): per wave, s_memtime cycles of [0] table setup, [1] ring prologue, [2] input
+// steps (with their conversions), [3] DMA waits + barriers, [4] output stage, [5] total, [6] / [7] start /
+// end time, into a.stamps[((blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) * 8 + ...].
+__device__ __forceinline__ uint64_t v1_stamp() {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+}
+
+template <int NB = 1, int CB = 4, bool STAMP = false, class Step>
 __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&& step) {
-    for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
-    if constexpr (NB == 2) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < 1024; i += 256) lds[V1H_G4 + i] = lds[1024 + (i & ~255) + gmul_g4(i & 255)];
-    }
-    __syncthreads();
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts = 0;
+    if constexpr (STAMP) ph[6] = ts = v1_stamp();
     const uint32_t* lt = lds;
     uint32_t* ring = lds + 2048;
     const int64_t bid = blockIdx.x;
@@ -242,10 +247,27 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
             wait_vm<3>();
     };
     u32x16 a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    auto lap = [&](int k) {
+        if constexpr (STAMP) {
+            const uint64_t t = v1_stamp();
+            ph[k] += t - ts;
+            ts = t;
+        }
+    };
+    // the ring prologue's DMAs go out first, then the coordinate tables are copied into LDS: the two
+    // latencies overlap (the ring area and the tables are disjoint)
     for (int b = 0; b < RING_B; ++b)
         if (4 * b + wave < K) issue(4 * b + wave);
+    for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
+    if constexpr (NB == 2) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 1024; i += 256) lds[V1H_G4 + i] = lds[1024 + (i & ~255) + gmul_g4(i & 255)];
+    }
+    __syncthreads();
+    lap(0);
     wait_mine(mine(1, RING_B - 1));
     asm volatile("s_barrier" ::: "memory");
+    lap(1);
     for (int b = 0; b < nb; ++b) {
         const int ib = 4 * (b + RING_B) + wave;
         if (ib < K) issue(ib);
@@ -267,8 +289,10 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
                     step(y[j], i, tile, a0, a1, rec);
             }
         }
+        lap(2);
         wait_mine(mine(b + 2, b + RING_B));
         asm volatile("s_barrier" ::: "memory");
+        lap(3);
     }
     const int rows = min(32, R - tile * 32);
     if (a.kslices > 1 && !a.ps_kr) {  // partial products (L^-1 is GF(2)-linear: XOR of converted partials)
@@ -281,4 +305,15 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     }
     m8_v1_store<NB>(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4, out_idx + tile * 32, rows,
                     a0, a1, b0, b1);
+    if constexpr (STAMP) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lap(4);
+        ph[7] = ts;
+        ph[5] = ts - ph[6];
+        if (lane == 0) {
+            uint64_t* o = a.stamps + ((int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave) * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = ph[k];
+        }
+    }
 }

@@ -403,10 +403,15 @@ __device__ __forceinline__ void m8_v1h_step(uint32_t y, const uint32_t* cp, u32x
 // variant is rs_jit.cpp's rs_v1jit.
 template <int ABL>
 __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
-    if constexpr (ABL >= 2) {  // inputs converted 1 (ABL 2), 2 (3) or 4 (4) at a time
+    if constexpr (ABL >= 2 && ABL <= 4) {  // inputs converted 1 (ABL 2), 2 (3) or 4 (4) at a time
         __shared__ __attribute__((aligned(16))) uint32_t lds[V1H_LDS_WORDS];
         m8_v1_run<2, ABL == 2 ? 1 : ABL == 3 ? 2 : 4>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, u32x16& b0, u32x16& b1,
                                  const uint32_t* rec) { m8_v1h_step(y, rec, a0, a1, b0, b1); });
+    } else if constexpr (ABL == 5) {  // diagnostic: the production step with s_memtime phase stamps
+        __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
+        m8_v1_run<1, 4, true>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
+            m8_v1_step<0>(y, rec, a0, a1);
+        });
     } else {
         __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
         m8_v1_run(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
@@ -1196,12 +1201,13 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
         // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
         // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 split schedule with the multiply-based xtime,
         // 15 no gpr-index mode
-        if (a.mode == 18 || a.mode == 19 || a.mode == 20) {  // V = 1 kernel (19: without gpr-index mode, timing
+        if (a.mode == 18 || a.mode == 19 || a.mode == 20 || a.mode == 21) {  // V = 1 kernel (19: without gpr-index mode, timing
                                                              // only; 20: the one-table step)
             const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
             if (full > 0) {
                 V1Args v = v1_args(a, full, nullptr);
-                v.kslices = a.mode != 19 ? m8_kslices(a, n_stripes, nullptr) : 1;
+                v.kslices = a.mode != 19 && a.mode != 21 ? m8_kslices(a, n_stripes, nullptr) : 1;
+                v.stamps = a.stamps;
                 v.partial = a.scratch;
                 dim3 g(unsigned(n_stripes * full), grid.y, unsigned(v.kslices));
 #ifdef RS_AMD_DIAG
@@ -1211,6 +1217,10 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
 #endif
                 if (a.mode == 20)
                     hipLaunchKernelGGL((k_apply_m8_v1<2>), g, dim3(256), 0, st, v);
+#ifdef RS_AMD_DIAG
+                else if (a.mode == 21)
+                    hipLaunchKernelGGL((k_apply_m8_v1<5>), g, dim3(256), 0, st, v);
+#endif
                 else
                     hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
                 if (v.kslices > 1) {
@@ -2119,6 +2129,8 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
 #ifdef RS_AMD_DIAG
         else if (kernel == 6)  // timing ablation: fixed table registers, no index switches (wrong results)
             hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 7)  // the production kernel with phase stamps into f.stamps
+            hipLaunchKernelGGL((k_apply_m8_v1<5>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
 #endif
         else
             hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);

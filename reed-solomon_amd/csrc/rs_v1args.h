@@ -41,6 +41,8 @@ struct V1Args {
     // syndrome route: the erased slots still hold their old contents g, the syndromes saw them, and the
     // solve yields g + c, so g ^ (W S) = c without a pass that zeroes the slots first)
     int32_t xor_dst;
+    // diagnostic builds only (k_apply_m8_v1<5>): per wave, 8 s_memtime phase counters (m8_v1_run STAMP)
+    uint64_t* stamps;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.
