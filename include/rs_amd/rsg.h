@@ -58,6 +58,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  chunk's solve (two buffer sets), 0 one stream (default)
  *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 1 one dword per lane
  *                  without the ring, 2 two dwords per lane, 3 the ring kernel with one nibble table
+ *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0 (default 1; 2-64 walk a stripe's
+ *                  chunks in one workgroup, table setup once, next chunk's ring prologue under the outputs)
  *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
  *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
  *                  0 one plan per pattern rebuilt on the stream

@@ -176,6 +176,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->m8_ps_kernel = int(value);
         return 0;
     }
+    if (!std::strcmp(name, "m8_ps_cpb")) {  // per-stripe GF(256) solve: column chunks per workgroup
+        if (value < 1 || value > 64) return RS_ERR_INVALID;
+        c->m8_ps_cpb = int(value);
+        return 0;
+    }
     if (!std::strcmp(name, "m8_syn_overlap")) {  // GF(256) per-stripe syndrome route: overlapped chunks
         if (value < 0 || value > 1) return RS_ERR_INVALID;
         c->m8_syn_overlap = int(value);

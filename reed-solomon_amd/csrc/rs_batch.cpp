@@ -239,7 +239,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_idx = idx_stride;
             v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
-            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
         c->last_kernel = std::string(c->syn_route == 2 ? "reenc_xj" : "syn_xj") + "+apply_m8_v1_ps" + (ovl ? "(overlap)" : "");
@@ -279,7 +279,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.ps_in = in_stride;
         v.ps_out = out_stride;
         v.ps_idx = idx_stride;
-        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel));
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
     }
     c->last_kernel = "apply_m8_v1_ps";
     return scratch_release(c, st);

@@ -309,6 +309,9 @@ struct rsg_codec {
     // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
     // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input)
     int m8_ps_kernel = 0;
+    // option m8_ps_cpb: 1 KiB column chunks per workgroup of the per-stripe ring kernels (table setup once per
+    // block, the next chunk's ring prologue in flight during this chunk's output stage)
+    int m8_ps_cpb = 1;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;
     void* d_syn = nullptr;  // [chunk][r][S] syndromes

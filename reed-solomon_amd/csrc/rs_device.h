@@ -147,7 +147,7 @@ __device__ __forceinline__ void sload32(const int32_t* out, i32x16s& o0, i32x16s
 // The V = 1 kernels' outputs: row p of the tile back to GF(2^16) words (m8_v1_out) and stored to
 // dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst: every old value is loaded first, so the
 // wave waits on one round of loads while it converts its outputs).
-template <int NB>
+template <int NB, int LBX = 0>
 __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt, uint8_t* dst, const int32_t* out,
                                             int rows, const u32x16& a0, const u32x16& a1, const u32x16& b0,
                                             const u32x16& b1) {
@@ -157,7 +157,7 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
         return reinterpret_cast<uint32_t*>(dst + int64_t(p < 16 ? o0[p & 15] : o1[p & 15]) * a.dst_sym);
     };
     if (a.xor_dst) {  // g ^ (W S), in rounds of LB loads (NB = 2 holds twice the accumulators)
-        constexpr int LB = NB == 2 ? 16 : 32;
+        constexpr int LB = LBX ? LBX : NB == 2 ? 16 : 32;
 #pragma unroll
         for (int p0 = 0; p0 < 32; p0 += LB) {
             uint32_t old[LB];
@@ -191,23 +191,29 @@ __device__ __forceinline__ uint64_t v1_stamp() {
     return v;
 }
 
-template <int NB = 1, int CB = 4, bool STAMP = false, class Step>
+template <int NB = 1, int CB = 4, bool STAMP = false, bool MULTI = false, class Step>
 __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&& step) {
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts = 0;
     if constexpr (STAMP) ph[6] = ts = v1_stamp();
     const uint32_t* lt = lds;
     uint32_t* ring = lds + 2048;
+    // block -> (launch-local stripe, its chunks [cbeg, cend)): MULTI kernels walk a.cpb column chunks of the
+    // stripe, so the table setup is paid once and each next chunk's ring prologue is in flight during the
+    // current chunk's output stage (a separate instantiation: the chunk loop costs registers)
+    const int cpb = MULTI && a.cpb > 1 ? a.cpb : 1;
+    const int64_t ngrp = (a.nchunks + cpb - 1) / cpb;
     const int64_t bid = blockIdx.x;
-    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t local = bid / ngrp;  // launch-local stripe
     const int64_t stripe = RS_STRIPE(a.ids, local);
-    const int64_t chunk0 = (bid - local * a.nchunks) * 1024;
+    const int64_t cbeg = (bid - local * ngrp) * cpb;
+    const int64_t cend = MULTI ? min(cbeg + int64_t(cpb), a.nchunks) : cbeg + 1;
     const int tile = blockIdx.y;
     int K = a.K, R = a.R;
     const int32_t* in_idx = a.in_idx;
     const int32_t* out_idx = a.out_idx;
     const uint32_t* idxb = a.idx;
-    // split-K (small grids, one plan for all stripes): this workgroup takes inputs [i0, i0 + K) of the
-    // list and leaves its partial outputs for k_xor_slices
+    // split-K (small grids, one plan for all stripes, one chunk per block): this workgroup takes inputs
+    // [i0, i0 + K) of the list and leaves its partial outputs for k_xor_slices
     const int slice = blockIdx.z;
     const int kfull = a.K;
     int i0 = 0;
@@ -226,9 +232,14 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     }
     const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
+    const int rows = min(32, R - tile * 32);
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(ring));
-    const uint8_t* gl = a.src + stripe * a.src_stripe + chunk0 + 16 * lane;
-    auto issue = [&](int i) { dma16(gl + int64_t(sload(in_idx + i)) * a.src_sym, ring_lds + uint32_t(i % RING_SLOTS) * 1024u); };
+    // wave-uniform base of the current chunk (SGPRs); the lane's 16-byte offset is added per DMA, so the
+    // chunk loop carries no 64-bit per-lane pointer
+    const uint8_t* gsb = a.src + stripe * a.src_stripe + cbeg * 1024;
+    auto issue = [&](int i) {
+        dma16(gsb + int64_t(sload(in_idx + i)) * a.src_sym + 16 * lane, ring_lds + uint32_t(i % RING_SLOTS) * 1024u);
+    };
     const int nb = (K + 3) / 4;
     auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]
         int c = 0;
@@ -245,6 +256,20 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
             wait_vm<2>();
         else
             wait_vm<3>();
+    };
+    // the prologue's wait after an output stage: that stage's `pend` stores are newer than the prologue's
+    // DMAs and may still be in flight (vmcnt counts both, in issue order)
+    auto wait_pro = [&](int n, int pend) {
+        if (pend == 32) {
+            if (n <= 0)
+                wait_vm<32>();
+            else if (n == 1)
+                wait_vm<33>();
+            else
+                wait_vm<34>();
+        } else {
+            wait_mine(n);
+        }
     };
     u32x16 a0 = 0, a1 = 0, b0 = 0, b1 = 0;
     auto lap = [&](int k) {
@@ -265,46 +290,72 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     }
     __syncthreads();
     lap(0);
-    wait_mine(mine(1, RING_B - 1));
-    asm volatile("s_barrier" ::: "memory");
-    lap(1);
-    for (int b = 0; b < nb; ++b) {
-        const int ib = 4 * (b + RING_B) + wave;
-        if (ib < K) issue(ib);
-        // the batch's inputs in coordinates (slots past K hold stale bytes and are not used), CB at a time
-        // (one LDS latency per CB inputs; each converted input held across the steps before its own costs a VGPR)
-        uint32_t y[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (j % CB == 0) {
-#pragma unroll
-                for (int q = j; q < j + CB; ++q) y[q] = lds_lookup4(lt, ring[((4 * b + q) % RING_SLOTS) * 256 + threadIdx.x]);
-            }
-            const int i = 4 * b + j;
-            if (i < K) {
-                const uint32_t* rec = idxb + (size_t(tile) * (a.ps_kr ? K : kfull) + i0 + i) * 64;
-                if constexpr (NB == 2)
-                    step(y[j], i, tile, a0, a1, b0, b1, rec);
-                else
-                    step(y[j], i, tile, a0, a1, rec);
-            }
-        }
-        lap(2);
-        wait_mine(mine(b + 2, b + RING_B));
+    int pend = 0;
+    for (int64_t c = cbeg; c < cend; ++c) {
+        const int64_t chunk0 = c * 1024;
+        wait_pro(mine(1, RING_B - 1), pend);
         asm volatile("s_barrier" ::: "memory");
-        lap(3);
-    }
-    const int rows = min(32, R - tile * 32);
-    if (a.kslices > 1 && !a.ps_kr) {  // partial products (L^-1 is GF(2)-linear: XOR of converted partials)
-        const int64_t nloc = gridDim.x / a.nchunks, rpad = int64_t(gridDim.y) * 32, cw = a.nchunks * 256;
-        uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 32) * cw + (chunk0 >> 2) + threadIdx.x;
+        lap(1);
+        for (int b = 0; b < nb; ++b) {
+            const int ib = 4 * (b + RING_B) + wave;
+            if (ib < K) issue(ib);
+            // the batch's inputs in coordinates (slots past K hold stale bytes and are not used), CB at a
+            // time (one LDS latency per CB inputs; each converted input held across the steps before its own
+            // costs a VGPR)
+            uint32_t y[4];
 #pragma unroll
-        for (int p = 0; p < 32; ++p)
-            if (p < rows) part[p * cw] = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
-        return;
+            for (int j = 0; j < 4; ++j) {
+                if (j % CB == 0) {
+#pragma unroll
+                    for (int q = j; q < j + CB; ++q)
+                        y[q] = lds_lookup4(lt, ring[((4 * b + q) % RING_SLOTS) * 256 + threadIdx.x]);
+                }
+                const int i = 4 * b + j;
+                if (i < K) {
+                    const uint32_t* rec = idxb + (size_t(tile) * (a.ps_kr ? K : kfull) + i0 + i) * 64;
+                    if constexpr (NB == 2)
+                        step(y[j], i, tile, a0, a1, b0, b1, rec);
+                    else
+                        step(y[j], i, tile, a0, a1, rec);
+                }
+            }
+            lap(2);
+            wait_mine(mine(b + 2, b + RING_B));
+            asm volatile("s_barrier" ::: "memory");
+            lap(3);
+        }
+        if (a.kslices > 1 && !a.ps_kr) {  // partial products (L^-1 is GF(2)-linear: XOR of converted partials)
+            const int64_t nloc = gridDim.x / a.nchunks, rpad = int64_t(gridDim.y) * 32, cw = a.nchunks * 256;
+            uint32_t* part = a.partial + ((slice * nloc + local) * rpad + tile * 32) * cw + (chunk0 >> 2) + threadIdx.x;
+#pragma unroll
+            for (int p = 0; p < 32; ++p)
+                if (p < rows) part[p * cw] = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
+            return;
+        }
+        // every wave has read the whole ring (last barrier): the next chunk's prologue may refill it now
+        if (MULTI && c + 1 < cend) {
+            gsb += 1024;
+            for (int b = 0; b < RING_B; ++b)
+                if (4 * b + wave < K) issue(4 * b + wave);
+        }
+        m8_v1_store<NB, MULTI ? 8 : 0>(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4,
+                                        out_idx + tile * 32, rows, a0, a1, b0, b1);
+        if constexpr (MULTI) {
+            pend = rows;
+            // zero the accumulators where the input step keeps them (NB = 1: v[40:71], gen_asm.py v1)
+            asm volatile(
+                "v_mov_b32 v40, 0\n\tv_mov_b32 v41, 0\n\tv_mov_b32 v42, 0\n\tv_mov_b32 v43, 0\n\t"
+                "v_mov_b32 v44, 0\n\tv_mov_b32 v45, 0\n\tv_mov_b32 v46, 0\n\tv_mov_b32 v47, 0\n\t"
+                "v_mov_b32 v48, 0\n\tv_mov_b32 v49, 0\n\tv_mov_b32 v50, 0\n\tv_mov_b32 v51, 0\n\t"
+                "v_mov_b32 v52, 0\n\tv_mov_b32 v53, 0\n\tv_mov_b32 v54, 0\n\tv_mov_b32 v55, 0\n\t"
+                "v_mov_b32 v56, 0\n\tv_mov_b32 v57, 0\n\tv_mov_b32 v58, 0\n\tv_mov_b32 v59, 0\n\t"
+                "v_mov_b32 v60, 0\n\tv_mov_b32 v61, 0\n\tv_mov_b32 v62, 0\n\tv_mov_b32 v63, 0\n\t"
+                "v_mov_b32 v64, 0\n\tv_mov_b32 v65, 0\n\tv_mov_b32 v66, 0\n\tv_mov_b32 v67, 0\n\t"
+                "v_mov_b32 v68, 0\n\tv_mov_b32 v69, 0\n\tv_mov_b32 v70, 0\n\tv_mov_b32 v71, 0"
+                : "=&{v[40:55]}"(a0), "=&{v[56:71]}"(a1));
+        }
+        lap(4);
     }
-    m8_v1_store<NB>(a, lt, a.dst + stripe * a.dst_stripe + chunk0 + int64_t(threadIdx.x) * 4, out_idx + tile * 32, rows,
-                    a0, a1, b0, b1);
     if constexpr (STAMP) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lap(4);

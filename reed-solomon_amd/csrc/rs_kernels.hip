@@ -407,6 +407,12 @@ __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
         __shared__ __attribute__((aligned(16))) uint32_t lds[V1H_LDS_WORDS];
         m8_v1_run<2, ABL == 2 ? 1 : ABL == 3 ? 2 : 4>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, u32x16& b0, u32x16& b1,
                                  const uint32_t* rec) { m8_v1h_step(y, rec, a0, a1, b0, b1); });
+    } else if constexpr (ABL == 6) {  // the production step over a.cpb column chunks per workgroup (inputs
+                                      // converted two at a time: 91 VGPRs, 5 waves/SIMD)
+        __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
+        m8_v1_run<1, 2, false, true>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
+            m8_v1_step<0>(y, rec, a0, a1);
+        });
     } else if constexpr (ABL == 5) {  // diagnostic: the production step with s_memtime phase stamps
         __shared__ __attribute__((aligned(16))) uint32_t lds[V1_LDS_WORDS];
         m8_v1_run<1, 4, true>(a, lds, [&](uint32_t y, int, int, u32x16& a0, u32x16& a1, const uint32_t* rec) {
@@ -2105,7 +2111,8 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel) {
+hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
+                              int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
     if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch
         V1Args f = v;
@@ -2118,22 +2125,27 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
     if (full > 0) {
         V1Args f = v;
         f.nchunks = full;
+        // the production ring kernel (0) walks cpb chunks per block (k_apply_m8_v1<6>); the others one
+        f.cpb = kernel == 0 ? std::max(1, std::min<int>(cpb, int(full))) : 1;
+        const int64_t blocks = n_sel * ((full + f.cpb - 1) / f.cpb);
         if (kernel == 1)
             hipLaunchKernelGGL(k_apply_m8_ps_w, dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 3)
-            hipLaunchKernelGGL((k_apply_m8_v1<2>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<2>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 4)
-            hipLaunchKernelGGL((k_apply_m8_v1<3>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<3>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 5)
-            hipLaunchKernelGGL((k_apply_m8_v1<4>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<4>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
 #ifdef RS_AMD_DIAG
         else if (kernel == 6)  // timing ablation: fixed table registers, no index switches (wrong results)
-            hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 7)  // the production kernel with phase stamps into f.stamps
-            hipLaunchKernelGGL((k_apply_m8_v1<5>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<5>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
 #endif
+        else if (f.cpb > 1)
+            hipLaunchKernelGGL((k_apply_m8_v1<6>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else
-            hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
+            hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
     }
     if (nbytes % 1024)
         hipLaunchKernelGGL(k_apply_m8_ps_tail, dim3(unsigned(n_sel), unsigned(tiles)), dim3(256), 0, st, v,

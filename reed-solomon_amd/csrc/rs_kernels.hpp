@@ -119,9 +119,10 @@ hipError_t launch_plan16_ps(const Ps16Args& a, int64_t n_sel, hipStream_t st);
 hipError_t launch_plan16_ps_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st);
 // k_apply_m16_v1 in per-stripe mode over the full 1 KiB chunks (v.ps_* set, tiles = the largest stripe's)
 hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
-// V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes)
+// V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes);
+// kernel = option m8_ps_kernel, cpb = column chunks per block of the ring kernels (option m8_ps_cpb)
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st,
-                              int kernel = 0);
+                              int kernel = 0, int cpb = 1);
 
 // dst row j = src row rows[j] for j < nrows, `width` bytes each (16-byte aligned rows, padded pitch)
 hipError_t launch_gather_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, const int32_t* rows,

@@ -43,6 +43,9 @@ struct V1Args {
     int32_t xor_dst;
     // diagnostic builds only (k_apply_m8_v1<5>): per wave, 8 s_memtime phase counters (m8_v1_run STAMP)
     uint64_t* stamps;
+    // m8_v1_run: column chunks per block (<= 1: one; the grid's x then covers n_stripes * ceil(nchunks / cpb)
+    // blocks). Not combined with split-K.
+    int32_t cpb;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

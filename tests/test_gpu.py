@@ -534,12 +534,13 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
         assert np.array_equal(dev.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("route,ovl,kern", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1), (0, 0, 1), (1, 0, 2),
-                                            (1, 1, 2), (0, 0, 2), (2, 0, 0), (2, 1, 0), (2, 0, 2), (2, 1, 2),
-                                            (2, 0, 3), (1, 0, 3), (0, 0, 3)])
+@pytest.mark.parametrize("route,ovl,kern,cpb", [(0, 0, 0, 1), (1, 0, 0, 1), (1, 1, 0, 1), (1, 0, 1, 1), (0, 0, 1, 1),
+                                                (1, 0, 2, 1), (1, 1, 2, 1), (0, 0, 2, 1), (2, 0, 0, 1), (2, 1, 0, 1),
+                                                (2, 0, 2, 1), (2, 1, 2, 1), (2, 0, 3, 1), (1, 0, 3, 1), (0, 0, 3, 1),
+                                                (2, 0, 0, 3), (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2)])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
-def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
+def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
     the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
     first; route 2: the re-encode differences [G | I] of every slot, then a t_info x t_info Cauchy-inverse
@@ -548,7 +549,8 @@ def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
     kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
-    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
+    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>). cpb > 1: the
+    ring kernel walks that many 1 KiB column chunks per workgroup (k_apply_m8_v1<6>; 64 > chunks per symbol). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
     ends in a partial column chunk."""
     if route and S % 2048:
         pytest.skip("the syndrome route covers whole 2 KiB columns (other sizes take the survivor route)")
@@ -559,6 +561,7 @@ def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern):
     codec.set_option("syn_route", route)
     codec.set_option("m8_syn_overlap", ovl)
     codec.set_option("m8_ps_kernel", kern)  # 1: the ring-free per-stripe solve kernel (k_apply_m8_ps_w)
+    codec.set_option("m8_ps_cpb", cpb)
     codec.encode(dev)
     pats = np.zeros((n, k + r), bool)
     for s in range(n):
