@@ -263,13 +263,15 @@ def test_fingerprint_matches_cpu_port():
         assert int(fp[s]) == fingerprint_np(host[s], 0, k + r)
 
 
-@pytest.mark.parametrize("plans", [0, 1])
+@pytest.mark.parametrize("plans,n", [(0, 40), (1, 40), (2, 40), (2, 100)])
 @pytest.mark.parametrize("S", [8192, 8712])
-def test_decode_batch_per_stripe_patterns(S, plans):
+def test_decode_batch_per_stripe_patterns(S, plans, n):
     """rsg_decode_batch: every stripe has its own erasure pattern (information and repair erasures,
     stripes with nothing to restore, repeated patterns) -- each stripe bit-exact vs the oracle, with
-    host plans per pattern (0) and device-built plans (1); S = 8712 adds tail columns."""
-    k, r, n = 128, 32, 40
+    host plans per pattern (0), device-built plans (1) and the default (2: 11 distinct patterns at
+    n = 40 take host plans; 23 at n = 100 pass the 16-pattern threshold, where grouping stops and the
+    device plans take over); S = 8712 adds tail columns."""
+    k, r = 128, 32
     rng = np.random.default_rng(21)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xB7)
@@ -292,6 +294,8 @@ def test_decode_batch_per_stripe_patterns(S, plans):
     dev.copy_(torch.from_numpy(poisoned))
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
+    if plans == 2:
+        assert ("apply_m8_v1_ps" in codec.last_kernel) == (n == 100), codec.last_kernel
     got = dev.cpu().numpy()
     for s in range(n):
         want = poisoned[s].copy()
@@ -537,7 +541,8 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(0, 0, 0, 1), (1, 0, 0, 1), (1, 1, 0, 1), (1, 0, 1, 1), (0, 0, 1, 1),
                                                 (1, 0, 2, 1), (1, 1, 2, 1), (0, 0, 2, 1), (2, 0, 0, 1), (2, 1, 0, 1),
                                                 (2, 0, 2, 1), (2, 1, 2, 1), (2, 0, 3, 1), (1, 0, 3, 1), (0, 0, 3, 1),
-                                                (2, 0, 0, 3), (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2)])
+                                                (2, 0, 0, 3), (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2),
+                                                (2, 0, 4, 1), (2, 0, 5, 1)])
 @pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                                      (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
