@@ -60,9 +60,11 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  without the ring, 2 two dwords per lane, 3 the ring kernel with one nibble table
  *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0 (default 1; 2-64 walk a stripe's
  *                  chunks in one workgroup, table setup once, next chunk's ring prologue under the outputs)
- *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns: 1 one syndrome pass over all slots
- *                  + a device-built t_info x t solve per stripe (default; S a multiple of 1 KiB, r <= 4096);
- *                  0 one plan per pattern rebuilt on the stream
+ *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns (S a multiple of 1 KiB, r <= 4096):
+ *                  1 one syndrome pass over all slots + a device-built t_info x t solve per stripe; 2 the
+ *                  encode route over the information slots + the received repair rows, then a t_info x
+ *                  t_info Cauchy solve per stripe; 3 (default) 2 when the batch's largest pattern needs at
+ *                  least 13/16 r syndromes, else 1; 0 one plan per pattern rebuilt on the stream
  *   "m16_ps_chunk" / "m16_ps_rec_mib"  stripes / record MiB per chunk of that path (0 / 1024 defaults)
  *   "m16_ps_overlap" 1 (default) the next chunk's syndrome pass runs on a codec stream beside this chunk's
  *                  solve (two syndrome buffers); 0 both on the caller's stream

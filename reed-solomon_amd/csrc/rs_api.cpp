@@ -137,7 +137,7 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
     if (!std::strcmp(name, "m16_ps")) {  // rsg_decode_batch of GF(2^16) codes: per-stripe route plans
-        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        if (value < 0 || value > 3) return RS_ERR_INVALID;
         c->m16_ps = int(value);
         return 0;
     }

@@ -426,6 +426,162 @@ int ps16_syn_plan(rsg_codec_t* c, int D, hipStream_t st, DevPlan** out) {
     return 0;
 }
 
+// m16_ps 2 (or 3 for patterns near r): the re-encode variant below, when the codec's encode is the GF(2^16)
+// route (run_cs) and its launches fit (31-bit offsets over the information slots and the r fixed-pass rows)
+bool ps16_reenc_eligible(const rsg_codec_t* c, int tmax, int64_t symbol_stride, uint64_t S) {
+    // 3 (default): when the syndrome route would compute at least 13/16 r syndromes -- at C5 (256 stripes,
+    // t erasures anywhere) the two cross between t = 768 (20.1 vs 21.2 ms) and t = 1024 (29.5 vs 26.2 ms)
+    const int D = std::min<int>(c->r, (tmax + 31) / 32 * 32);
+    const bool want = c->m16_ps == 2 || (c->m16_ps == 3 && 16 * D >= 13 * c->r);
+    const DevPlan* E = c->enc.get();
+    return want && E && E->cs && E->cs->kind == 0 && E->second && E->second->cs &&
+           E->cs->max_slot * symbol_stride + int64_t(S) < (int64_t(1) << 31) &&
+           int64_t(E->cs->D) * int64_t(S) < (int64_t(1) << 31) && int64_t(c->r) * int64_t(S) < (int64_t(1) << 31);
+}
+
+// The re-encode variant (option m16_ps 2): the pattern-independent part is the codec's encode route over
+// the information slots of a contiguous range of stripes (erased ones zeroed first), + the received repair
+// rows (launch_xor_rows), i.e. S' = [G | I] rcv, which run_reenc uses for one pattern; the per-pattern part
+// is each stripe's t_info x t_info Cauchy solve W' from its first t_info surviving repair rows (k_plan16_reenc*,
+// see rs_kernels.hip), applied by k_apply_m16_v1 in per-stripe mode. Against the syndrome route: the fixed
+// pass reads k instead of k + r slots, the solve t_info instead of t inputs, and W' has a closed form (no
+// synthetic division). ids: the selected stripes (ascending), sel_masks their masks.
+int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                              uint64_t S, const std::vector<int32_t>& ids, const uint8_t* sel_masks, int rmax,
+                              hipStream_t st) {
+    const int64_t k = c->k, r = c->r, n = k + r;
+    DevPlan& E = *c->enc;
+    int rc = 0;
+    if ((rc = E.order_after_build(st))) return rc;  // its records are read directly (run_cs)
+    if ((rc = scratch_acquire(c, st))) return rc;
+    const uint16_t *logt = nullptr, *expt = nullptr;
+    const uint8_t* g8 = nullptr;
+    if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
+    if (!c->d_elem) {
+        const Field& F = field();
+        std::vector<uint16_t> el(static_cast<size_t>(n));
+        for (int64_t i = 0; i < n; ++i) el[size_t(i)] = F.exp[c->positions[size_t(i)]];
+        if ((rc = upload(reinterpret_cast<void**>(&c->d_elem), el.data(), size_t(n) * 2))) return rc;
+    }
+    const int64_t nsel = int64_t(ids.size());
+    const int tiles = (rmax + 63) / 64;
+    const int64_t out_stride = int64_t(tiles) * 64, in_stride = out_stride + 16;
+    const int64_t rec_stride = int64_t(tiles) * (rmax + 1) * 64;  // dwords
+    const int64_t per = r * int64_t(S);                            // fixed-pass bytes per stripe
+    // chunks of selected stripes: at most m16_ps_rec_mib of records, and a stripe range (the fixed pass runs
+    // over every stripe of it) of at most 1 GiB of fixed-pass output
+    const int64_t cap_sel = std::max<int64_t>(
+        1, std::min<int64_t>({(int64_t(c->ps_rec_mib) << 20) / (rec_stride * 4), 65535,
+                              c->ps_chunk > 0 ? c->ps_chunk : int64_t(1) << 40}));
+    const int64_t cap_range = std::max<int64_t>(1, (int64_t(1) << 30) / per);
+    std::vector<std::pair<int64_t, int64_t>> chunks;  // [i0, i1) of ids
+    for (int64_t i0 = 0; i0 < nsel;) {
+        int64_t i1 = i0 + 1;
+        while (i1 < nsel && i1 - i0 < cap_sel && ids[size_t(i1)] - ids[size_t(i0)] < cap_range) ++i1;
+        chunks.emplace_back(i0, i1);
+        i0 = i1;
+    }
+    int64_t chunk = 0, range = 0;
+    for (auto& ch : chunks) {
+        chunk = std::max(chunk, ch.second - ch.first);
+        range = std::max<int64_t>(range, ids[size_t(ch.second - 1)] - ids[size_t(ch.first)] + 1);
+    }
+    auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+    const int64_t o_kr = 0, o_ee = al(chunk * 8), o_pe = o_ee + al(chunk * r * 2),
+                  o_po = o_pe + al(chunk * out_stride * 2), o_qe = o_po + al(chunk * out_stride * 4),
+                  o_pi = o_qe + al(chunk * in_stride * 2), o_lq = o_pi + al(chunk * in_stride * 4),
+                  o_lr = o_lq + al(chunk * in_stride * 4), small = o_lr + al(chunk * out_stride * 4);
+    size_t ids_bytes = c->ids_cap * 4;
+    rc = grow(reinterpret_cast<void**>(&c->d_ids), ids_bytes, ids.size() * 4);
+    c->ids_cap = ids_bytes / 4;
+    if (rc) return rc;
+    if ((rc = grow(&c->d_masks, c->masks_cap, size_t(nsel * n)))) return rc;
+    if ((rc = grow(&c->d_reenc, c->reenc_cap, size_t(range * per)))) return rc;
+    const int64_t rec_set = al(chunk * rec_stride * 4);
+    if ((rc = grow(&c->d_ps_rec, c->ps_rec_cap, size_t(2 * rec_set)))) return rc;
+    if ((rc = grow(&c->d_ps_small, c->ps_small_cap, size_t(2 * small)))) return rc;
+    if (!c->ps_side) HIP_TRY(hipStreamCreateWithFlags(&c->ps_side, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1],
+                          &c->ps_ev_used[0], &c->ps_ev_used[1]})
+        if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, sel_masks, size_t(nsel * n)}})))
+        return rc;
+    Ps16Args pa{};
+    pa.elem = c->d_elem;
+    pa.logt = logt;
+    pa.expt = expt;
+    pa.k = c->k;
+    pa.r = c->r;
+    pa.n = int32_t(n);
+    pa.out_stride = out_stride;
+    pa.in_stride = in_stride;
+    pa.rec_stride = rec_stride;
+    pa.tblocks = (tiles + 3) / 4;
+    pa.lblocks = (2 * rmax + 255) / 256;
+    pa.base = base;
+    pa.stripe_stride = stripe_stride;
+    pa.symbol_stride = symbol_stride;
+    pa.S = int64_t(S);
+    uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
+    // the side stream starts after the caller's earlier work on st (the plans zero erased slots)
+    HIP_TRY(hipEventRecord(c->ps_ev_entry, st));
+    HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_entry, 0));
+    std::string fixed;
+    for (size_t ci = 0; ci < chunks.size(); ++ci) {
+        const int64_t i0 = chunks[ci].first, cn = chunks[ci].second - i0;
+        const int64_t s0 = ids[size_t(i0)], ns = ids[size_t(i0 + cn - 1)] - s0 + 1;
+        const int set = int(ci & 1);
+        uint8_t* sm = static_cast<uint8_t*>(c->d_ps_small) + set * small;
+        pa.kr = reinterpret_cast<int32_t*>(sm + o_kr);
+        pa.ee = reinterpret_cast<uint16_t*>(sm + o_ee);
+        pa.pe = reinterpret_cast<uint16_t*>(sm + o_pe);
+        pa.pout = reinterpret_cast<int32_t*>(sm + o_po);
+        pa.qe = reinterpret_cast<uint16_t*>(sm + o_qe);
+        pa.pin = reinterpret_cast<int32_t*>(sm + o_pi);
+        pa.lq = reinterpret_cast<uint32_t*>(sm + o_lq);
+        pa.lr = reinterpret_cast<uint32_t*>(sm + o_lr);
+        pa.rec = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_ps_rec) + set * rec_set);
+        pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(i0) * size_t(n);
+        pa.ids = c->d_ids + i0;
+        // plans on the side stream, once chunk ci - 2 (same buffer set) has been applied
+        if (ci >= 2) HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_used[set], 0));
+        HIP_TRY(launch_plan16_reenc(pa, cn, c->ps_side));
+        HIP_TRY(hipEventRecord(c->ps_ev_zero[set], c->ps_side));
+        HIP_TRY(launch_plan16_reenc_rec(pa, cn, c->ps_side));  // runs beside this chunk's fixed pass
+        HIP_TRY(hipEventRecord(c->ps_ev_plan[set], c->ps_side));
+        // the fixed pass over the stripe range (after the zeroing), + the received repair rows
+        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_zero[set], 0));
+        uint8_t* b = base + s0 * stripe_stride;
+        if ((rc = run_cs(c, E, b, stripe_stride, symbol_stride, y, per, int64_t(S), uint64_t(ns), S, st))) return rc;
+        fixed = c->last_kernel;
+        HIP_TRY(launch_xor_rows(y, per, int64_t(S), b + k * symbol_stride, stripe_stride, symbol_stride, r, int64_t(S),
+                                ns, st));
+        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
+        V1Args v{};
+        v.src = y - s0 * per;  // stripe ids index the range's rows: stripe s at y + (s - s0) * per
+        v.src_stripe = per;
+        v.src_sym = int64_t(S);
+        v.in_idx = pa.pin;
+        v.dst = base;
+        v.dst_stripe = stripe_stride;
+        v.dst_sym = symbol_stride;
+        v.out_idx = pa.pout;
+        v.idx = pa.rec;
+        v.ids = c->d_ids + i0;
+        v.ps_kr = pa.kr;
+        v.ps_in = in_stride;
+        v.ps_out = out_stride;
+        v.ps_idx = rec_stride;
+        v.K = rmax;
+        v.R = rmax;
+        HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
+        HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
+    }
+    if ((rc = E.note_use(st))) return rc;
+    c->last_kernel = "ps16r+" + fixed + "+xor+apply_m16_v1_ps";
+    return scratch_release(c, st);
+}
+
 // tr: per stripe, t (erasures) and R (erased information slots), counted by rsg_decode_batch
 int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
                         uint64_t n_stripes, uint64_t S, const bool* is_erased, const int32_t* tr,
@@ -450,6 +606,8 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
             std::memcpy(masks.data() + i * n, is_erased + size_t(ids[i]) * n, n);
         mask_src = masks.data();
     }
+    if (ps16_reenc_eligible(c, tmax, symbol_stride, S))
+        return decode_batch_m16_ps_reenc(c, base, stripe_stride, symbol_stride, S, ids, mask_src, rmax, st);
     int rc = scratch_acquire(c, st);
     if (rc) return rc;
     const uint16_t *logt = nullptr, *expt = nullptr;

@@ -266,8 +266,10 @@ struct rsg_codec {
     size_t reenc_cap = 0;
     int m16_reenc = 1;  // option m16_reenc: 0 keeps full-pattern decodes on the plain route
     // rsg_decode_batch of GF(2^16) codes with per-stripe patterns (decode_batch_m16_ps): 1 = the syndrome
-    // route with a device-built plan per stripe (default), 0 = a plan per distinct pattern
-    int m16_ps = 1;
+    // route with a device-built plan per stripe, 2 = its re-encode variant (encode route + t_info x t_info
+    // Cauchy solves), 3 = the re-encode variant when the batch's largest pattern needs >= 13/16 r syndromes,
+    // else the syndrome route (default), 0 = a plan per distinct pattern
+    int m16_ps = 3;
     std::map<int, std::unique_ptr<rsamd::DevPlan>> ps_syn;  // k_cs16 plans over all k + r slots, keyed by D
     std::vector<int> ps_syn_lru;
     void *d_ps_rec = nullptr, *d_ps_small = nullptr;  // per-stripe records / lists of decode_batch_m16_ps

@@ -2027,6 +2027,189 @@ __global__ void __launch_bounds__(256) k_plan16_ps_rec(Ps16Args a) {
     }
 }
 
+// ---------------------------------------------- GF(2^16) per-stripe re-encode plans (m16_ps 2)
+// The fixed pass is the codec's encode route over every information slot of the stripe range (erased ones
+// zeroed here first), + the received repair rows: S'_P = (G rcv_info)_P + rcv_P = sum_{Q in E} G[P][Q] c_Q
+// for each surviving repair slot P. The first t_info of them (R', slot order) give a square Cauchy system
+// whose inverse is again scaled Cauchy (k_plan_reenc_m8, gf16.cpp:solve_matrix):
+//   W'[Q][P] = L_T(X_P) / ((X_P + X_Q) L_T'(X_Q)),   T = E + (repair slots not in R'),  |T| = r.
+// k_plan16_reenc: one workgroup per stripe -- E (rows: pe, pout), R' (sources: qe, pin), T (into ee), K = R
+// = t_info, and the erased information slots zeroed.
+__global__ void __launch_bounds__(256) k_plan16_reenc(Ps16Args a) {
+    __shared__ int cnt[4][3];
+    const int64_t s = blockIdx.x;
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    const uint8_t* mask = a.masks + s * a.n;
+    uint16_t* pe = a.pe + s * a.out_stride;
+    int32_t* pout = a.pout + s * a.out_stride;
+    uint16_t* qe = a.qe + s * a.in_stride;
+    int32_t* pin = a.pin + s * a.in_stride;
+    uint16_t* tx = a.ee + s * a.r;
+    int R = 0, Q = 0, T = 0;  // block-uniform running counts: erased info, surviving repair, T
+    for (int c0 = 0; c0 < a.n; c0 += 256) {
+        const int i = c0 + j;
+        const bool valid = i < a.n;
+        const bool er = valid && mask[i] != 0;
+        const bool inf_er = er && i < a.k, rep_ok = valid && i >= a.k && !er;
+        const uint64_t bp = __ballot(inf_er), bq = __ballot(rep_ok);
+        if (lane == 0) {
+            cnt[w][0] = __popcll(bp);
+            cnt[w][1] = __popcll(bq);
+        }
+        __syncthreads();
+        int op = R, oq = Q, tp = 0, tq = 0;
+        for (int v = 0; v < 4; ++v) {
+            if (v < w) op += cnt[v][0], oq += cnt[v][1];
+            tp += cnt[v][0];
+            tq += cnt[v][1];
+        }
+        // every information slot precedes every repair slot: t_info is final for this chunk's repair slots
+        const int rall = R + tp;
+        const uint16_t x = valid ? a.elem[i] : 0;
+        if (inf_er) {
+            const int ip = op + __popcll(bp & below);
+            pe[ip] = x;
+            pout[ip] = i;
+        }
+        const int qi = oq + __popcll(bq & below);
+        const bool src = rep_ok && qi < rall;
+        if (src) {
+            qe[qi] = x;
+            pin[qi] = i - a.k;
+        }
+        const bool in_t = inf_er || (valid && i >= a.k && !src);
+        const uint64_t bt = __ballot(in_t);
+        __syncthreads();  // cnt[.][0..1] read by every wave
+        if (lane == 0) cnt[w][2] = __popcll(bt);
+        __syncthreads();
+        int ot = T, tt = 0;
+        for (int v = 0; v < 4; ++v) {
+            if (v < w) ot += cnt[v][2];
+            tt += cnt[v][2];
+        }
+        if (in_t) {
+            const int it = ot + __popcll(bt & below);
+            if (it < a.r) tx[it] = x;  // |T| = r for a pattern with t <= r (checked by the host)
+        }
+        R += tp;
+        Q += tq;
+        T += tt;
+        __syncthreads();  // cnt is rewritten by the next chunk
+    }
+    for (int p = R + j; p < a.out_stride; p += 256) pe[p] = 0, pout[p] = 0;
+    for (int q = R + j; q < a.in_stride; q += 256) qe[q] = 0, pin[q] = 0;
+    if (j == 0) {
+        a.kr[2 * s] = R;  // K = R: t_info sources, t_info rows
+        a.kr[2 * s + 1] = R;
+    }
+    // zero the erased information slots (the fixed pass reads every information slot)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint8_t* sb = a.base + int64_t(a.ids[s]) * a.stripe_stride;
+    const int64_t units = a.S / 16;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int p = 0; p < R; ++p) {
+        u32x4* d = reinterpret_cast<u32x4*>(sb + int64_t(pout[p]) * a.symbol_stride);
+        for (int64_t x = j; x < units; x += 256) d[x] = z;
+    }
+}
+
+// The log sums: lq[q] = sum_{e in T} log(X_q + X_e) for the sources, lr[p] = sum_{e in T, e != p} log(X_p +
+// X_e) for the rows; lblocks workgroups per stripe, one sum per thread, T staged in LDS, gathers unrolled.
+__global__ void __launch_bounds__(256) k_plan16_reenc_logs(Ps16Args a) {
+    __shared__ uint16_t tx[kPs16MaxR];
+    constexpr uint32_t N = 65535u;
+    const int64_t s = blockIdx.x / a.lblocks;
+    const int blk = int(blockIdx.x - s * a.lblocks);
+    const int R = a.kr[2 * s];
+    const uint16_t* tg = a.ee + s * a.r;
+    for (int e = threadIdx.x; e < a.r; e += 256) tx[e] = tg[e];
+    __syncthreads();
+    const int item = blk * 256 + int(threadIdx.x);  // [0, R): sources, [R, 2R): rows
+    if (item >= 2 * R) return;
+    const bool row = item >= R;
+    const int idx = row ? item - R : item;
+    const uint32_t x = row ? a.pe[s * a.out_stride + idx] : a.qe[s * a.in_stride + idx];
+    uint32_t sum = 0;
+    int e = 0;
+    for (; e + 8 <= a.r; e += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t d = x ^ tx[e + u];
+            v[u] = d ? uint32_t(a.logt[d]) : 0u;  // d = 0 only for a row's own element (excluded)
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; e < a.r; ++e) {
+        const uint32_t d = x ^ tx[e];
+        sum += d ? uint32_t(a.logt[d]) : 0u;
+    }
+    if (row)
+        a.lr[s * a.out_stride + idx] = sum % N;
+    else
+        a.lq[s * a.in_stride + idx] = sum % N;
+}
+
+// The records of W' (k_apply_m16_v1 format, as k_plan16_ps_rec): one wave per (stripe, 64-row tile), one
+// lane per row p, four sources per step (independent gathers): W'[p][q] = alpha^(lq[q] - lr[p] - log(X_p +
+// X_q)); the wave packs the 64 rows' index bytes of source q in LDS and stores the 256-byte record.
+__global__ void __launch_bounds__(256) k_plan16_reenc_rec(Ps16Args a) {
+    __shared__ uint32_t buf[4][4][64];
+    constexpr uint32_t N = 65535u;
+    const int64_t s = blockIdx.x / a.tblocks;
+    const int wave = int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
+    const int tile = int(blockIdx.x - s * a.tblocks) * 4 + wave;
+    const int R = a.kr[2 * s];
+    if (tile * 64 >= R) return;  // no block barrier below
+    const int row = tile * 64 + lane;
+    const bool live = row < R;
+    const uint32_t xp = live ? a.pe[s * a.out_stride + row] : 0u;
+    const uint32_t lrp = live ? a.lr[s * a.out_stride + row] : 0u;
+    const uint16_t* qe = a.qe + s * a.in_stride;
+    const uint32_t* lq = a.lq + s * a.in_stride;
+    uint32_t* rec = a.rec + s * a.rec_stride + size_t(tile) * size_t(R + 1) * 64;
+    uint8_t* lb = reinterpret_cast<uint8_t*>(&buf[wave][0][0]);
+    const int slot0 = 4 * (2 * (lane >> 3) + (lane & 1)) + ((lane & 7) >> 1);  // byte of plane 0
+    for (int q0 = 0; q0 < R; q0 += 4) {
+        uint32_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = min(q0 + u, R - 1);
+            const uint32_t lg = uint32_t(a.logt[xp ^ qe[q]]);  // X_p != X_q: rows are information slots
+            c[u] = live ? uint32_t(a.expt[(lq[q] + 2 * N - lrp - lg) % N]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint8_t* b = lb + u * 256;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) b[64 * n + slot0] = uint8_t(16 * n + ((c[u] >> (4 * n)) & 15u));
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (q0 + u < R) rec[size_t(q0 + u) * 64 + lane] = reinterpret_cast<const uint32_t*>(lb + u * 256)[lane];
+        __builtin_amdgcn_wave_barrier();  // buf is rewritten by the next step
+    }
+}
+
+hipError_t launch_plan16_reenc(const Ps16Args& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0) return hipSuccess;
+    if (a.r > kPs16MaxR || a.lblocks <= 0 || (a.S & 15) || (a.symbol_stride & 15) || (a.stripe_stride & 15) ||
+        (uintptr_t(a.base) & 15))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_plan16_reenc, dim3(unsigned(n_sel)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan16_reenc_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st) {
+    if (n_sel <= 0 || a.tblocks <= 0 || a.lblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_plan16_reenc_logs, dim3(unsigned(n_sel * a.lblocks)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_plan16_reenc_rec, dim3(unsigned(n_sel * a.tblocks)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_plan16_ps(const Ps16Args& a, int64_t n_sel, hipStream_t st) {
     if (n_sel <= 0) return hipSuccess;
     if (a.r > kPs16MaxR || (a.S & 15) || (a.symbol_stride & 15) || (a.stripe_stride & 15) ||

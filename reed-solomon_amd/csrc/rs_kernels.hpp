@@ -113,10 +113,21 @@ struct Ps16Args {
     uint8_t* base;         // stripes: the erased information slots are zeroed (the syndromes read every slot)
     int64_t stripe_stride, symbol_stride, S;
     const int32_t* ids;    // [n_sel] stripe indices
+    // re-encode variant (k_plan16_reenc*): sources = the first t_info surviving repair slots R'
+    int32_t* pin;          // [n_sel][in_stride] their rows in the fixed pass's output (repair slot - k)
+    uint16_t* qe;          // [n_sel][in_stride] their elements X_q
+    uint32_t* lq;          // [n_sel][in_stride] log L_T(X_q)
+    uint32_t* lr;          // [n_sel][out_stride] log L_T'(X_p) of the rows (T = E + repair slots not in R')
+    int64_t in_stride;
+    int32_t lblocks;       // workgroups per stripe of the log sums
 };
 // lists, P and the zeroing (one workgroup per stripe), then the records (tblocks workgroups per stripe)
 hipError_t launch_plan16_ps(const Ps16Args& a, int64_t n_sel, hipStream_t st);
 hipError_t launch_plan16_ps_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st);
+// the re-encode variant: lists + T + zeroing (one workgroup per stripe), the log sums (lblocks per stripe),
+// the records of W' (tblocks per stripe)
+hipError_t launch_plan16_reenc(const Ps16Args& a, int64_t n_sel, hipStream_t st);
+hipError_t launch_plan16_reenc_rec(const Ps16Args& a, int64_t n_sel, hipStream_t st);
 // k_apply_m16_v1 in per-stripe mode over the full 1 KiB chunks (v.ps_* set, tiles = the largest stripe's)
 hipError_t launch_apply_m16_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st);
 // V = 1 kernel over the full 1 KiB chunks + per-stripe tail kernel, plans in v.ps_* (n_sel stripes);

@@ -3,7 +3,8 @@ stripe: GF(2^16) codes take the per-stripe syndrome route (default since round 3
 stripe, a device-built t_info x t solve per stripe) or, with m16_ps=0, build one decode plan per
 pattern on the device and launch per pattern (one plan rebuilt on the stream per pattern), or cache
 per-pattern plans (batch_plans=0). Compared with one shared pattern over the same stripes.
-GB/s counts survivors read + information symbols written."""
+m16_ps=2 is the re-encode variant (the codec's encode route over the information slots, + the received repair
+rows, then a t_info x t_info Cauchy solve per stripe). GB/s counts survivors read + information symbols written."""
 import json
 import os
 import sys
@@ -19,14 +20,16 @@ k, r, S = 4096, 1024, 1024
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 rng = np.random.default_rng(7)
 pats = np.zeros((n, k + r), bool)
+tpat = int(os.environ.get("RS_C5_T", r))  # erasures per stripe (default t = r), anywhere
 for s in range(n):
-    pats[s, rng.choice(k + r, r, replace=False)] = True  # t = r erasures anywhere
+    pats[s, rng.choice(k + r, tpat, replace=False)] = True
 t = pats.sum(1)
 tinfo = pats[:, :k].sum(1)
 alg = float(((k + r - t) + tinfo).sum()) * S
 dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")
 rs_amd.fill_info(dev, k, seed=0x5EED)
 codec = rs_amd.Codec(k, r)
+codec.set_option("m16_ps", 1)  # the syndrome route (the default, 3, picks by the batch's largest pattern)
 codec.encode(dev)
 torch.cuda.synchronize()
 
@@ -43,13 +46,18 @@ mask = torch.from_numpy(pats).to("cuda")
 old = rs_amd.Codec(k, r)
 old.set_option("m16_ps", 0)
 serial = rs_amd.Codec(k, r)
+serial.set_option("m16_ps", 1)
 serial.set_option("m16_ps_overlap", 0)
-runs = [("distinct_patterns_ps16_route", codec), ("distinct_patterns_ps16_route_no_overlap", serial)]
+reenc = rs_amd.Codec(k, r)
+reenc.set_option("m16_ps", 2)  # the re-encode variant: encode route over the information slots + W' per stripe
+runs = [("distinct_patterns_ps16_route", codec), ("distinct_patterns_ps16_reenc", reenc),
+        ("distinct_patterns_ps16_route_no_overlap", serial)]
 for mib in [int(x) for x in os.environ.get("PS_REC_MIB", "").split(",") if x]:  # chunk-size sweep
     cm = rs_amd.Codec(k, r)
     cm.set_option("m16_ps_rec_mib", mib)
     runs.append((f"distinct_patterns_ps16_route_rec{mib}MiB", cm))
-runs += [("distinct_patterns_stream_plans", old), ("distinct_patterns_cached_plans", rs_amd.Codec(k, r, batch_plans=0))]
+if not os.environ.get("RS_C5_ROUTES_ONLY"):
+    runs += [("distinct_patterns_stream_plans", old), ("distinct_patterns_cached_plans", rs_amd.Codec(k, r, batch_plans=0))]
 for label, cdc in runs:
     times = []
     for _ in range(3):

@@ -419,12 +419,21 @@ def test_decode_batch_m16_stream_plans(k, r, S, n):
     assert np.array_equal(dev.cpu().numpy(), got)
 
 
-def test_decode_batch_m16_per_stripe_route_vs_golden():
+def ps16_kernel_ok(name, ps):
+    """rsg_last_kernel of the per-stripe GF(2^16) route: syndromes (m16_ps 1) or the re-encode variant (2)."""
+    if ps == 2:
+        return name.startswith("ps16r+") and name.endswith("+xor+apply_m16_v1_ps")
+    return name == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps"
+
+
+@pytest.mark.parametrize("ps", [1, 2])
+def test_decode_batch_m16_per_stripe_route_vs_golden(ps):
     """rsg_decode_batch at C5 with a different pattern on every stripe (reference reed_solomon.c:443-559):
-    the per-stripe GF(2^16) route (one syndrome pass over all k + r slots, then each stripe's own
-    device-built t_info x t solve). Every stripe's output equals the reference golden of its pattern;
-    erased information slots hold garbage on input; a repair-only stripe and a stripe without erasures
-    are left untouched."""
+    the per-stripe GF(2^16) route (ps 1: one syndrome pass over all k + r slots, then each stripe's own
+    device-built t_info x t solve; ps 2: the encode route over the information slots + the received repair
+    rows, then each stripe's t_info x t_info Cauchy solve). Every stripe's output equals the reference golden
+    of its pattern; erased information slots hold garbage on input; a repair-only stripe and a stripe without
+    erasures are left untouched."""
     cases = [case(nm) for nm in GPU_CASES if nm.startswith("c5ps_")]
     assert len(cases) >= 8
     k, r, S = 4096, 1024, 1024
@@ -433,6 +442,7 @@ def test_decode_batch_m16_per_stripe_route_vs_golden():
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     dev[:, :k] = torch.from_numpy(buf0[:k]).cuda()
     codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_ps", ps)
     codec.encode(dev)
     torch.cuda.synchronize()
     full = dev.cpu().numpy()
@@ -449,7 +459,7 @@ def test_decode_batch_m16_per_stripe_route_vs_golden():
     dev.copy_(torch.from_numpy(host))
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert codec.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", codec.last_kernel
+    assert ps16_kernel_ok(codec.last_kernel, ps), codec.last_kernel
     got = dev.cpu().numpy()
     for s, c in enumerate(cases):
         check_golden(c, got[s].tobytes())
@@ -457,15 +467,18 @@ def test_decode_batch_m16_per_stripe_route_vs_golden():
     assert np.array_equal(got[-1], full[-1])
 
 
+@pytest.mark.parametrize("ps", [1, 2, 3])
 @pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 37), (300, 64, 1024, 70), (600, 100, 3072, 5)])
-def test_decode_batch_m16_per_stripe_route(k, r, S, n):
-    """The per-stripe GF(2^16) route on assorted shapes: random patterns of 1..r erasures anywhere (garbage
-    in erased slots), against the oracle on a sample and byte-identical to the per-pattern plans
-    (m16_ps = 0); erased repair slots keep what they held."""
+def test_decode_batch_m16_per_stripe_route(k, r, S, n, ps):
+    """The per-stripe GF(2^16) route (ps 1 syndromes, 2 re-encode, 3 the default choice: re-encode when the
+    batch's largest pattern needs >= 13/16 r syndromes) on assorted shapes: random patterns of 1..r erasures
+    anywhere (garbage in erased slots), against the oracle on a sample and byte-identical to the
+    per-pattern plans (m16_ps = 0); erased repair slots keep what they held."""
     rng = np.random.default_rng(k + r + n)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xE1)
     codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_ps", ps)
     codec.encode(dev)
     torch.cuda.synchronize()
     full = dev.cpu().numpy()
@@ -479,7 +492,8 @@ def test_decode_batch_m16_per_stripe_route(k, r, S, n):
     dev.copy_(torch.from_numpy(host))
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert codec.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", codec.last_kernel
+    D = min(r, (int(pats.sum(1).max()) + 31) // 32 * 32)
+    assert ps16_kernel_ok(codec.last_kernel, ps if ps < 3 else (2 if 16 * D >= 13 * r else 1)), codec.last_kernel
     got = dev.cpu().numpy()
     assert np.array_equal(got[:, :k], full[:, :k])
     rep = pats.copy()
@@ -499,12 +513,13 @@ def test_decode_batch_m16_per_stripe_route(k, r, S, n):
     assert np.array_equal(dev.cpu().numpy()[:, :k], got[:, :k])
 
 
-@pytest.mark.parametrize("overlap", [0, 1])
+@pytest.mark.parametrize("ps,overlap", [(1, 0), (1, 1), (2, 0)])
 @pytest.mark.parametrize("chunk", [1, 3, 7])
-def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
+def test_decode_batch_m16_per_stripe_route_chunks(chunk, ps, overlap):
     """The per-stripe route in several chunks (m16_ps_chunk): double-buffered plans, and with m16_ps_overlap
-    the next chunk's syndrome pass on its own stream into the other syndrome buffer; byte-identical to the
-    one-chunk decode, stripes without erased information (skipped) mixed in."""
+    the next chunk's syndrome pass on its own stream into the other syndrome buffer (ps 2: the re-encode
+    variant, whose fixed pass covers each chunk's stripe range); byte-identical to the one-chunk decode,
+    stripes without erased information (skipped) mixed in."""
     k, r, S, n = 700, 120, 1024, 17
     rng = np.random.default_rng(chunk * 10 + overlap)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
@@ -526,6 +541,7 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
     want = dev.cpu().numpy()
     assert np.array_equal(want[:, :k], full[:, :k])
     cdc = rs_amd.Codec(k, r)
+    cdc.set_option("m16_ps", ps)
     cdc.set_option("m16_ps_chunk", chunk)
     cdc.set_option("m16_ps_overlap", overlap)
     for it in range(3):  # the second call reuses the streams, events and buffers; the third regrows them
@@ -534,7 +550,7 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, overlap):
         dev.copy_(torch.from_numpy(host))
         assert cdc.decode_batch(dev, pats) == 0
         torch.cuda.synchronize()
-        assert cdc.last_kernel == f"ps16+{CS_DEFAULT}+apply_m16_v1_ps", cdc.last_kernel
+        assert ps16_kernel_ok(cdc.last_kernel, ps), cdc.last_kernel
         assert np.array_equal(dev.cpu().numpy(), want)
 
 
