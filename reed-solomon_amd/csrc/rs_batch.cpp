@@ -543,14 +543,15 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         pa.rec = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->d_ps_rec) + set * rec_set);
         pa.masks = static_cast<const uint8_t*>(c->d_masks) + size_t(i0) * size_t(n);
         pa.ids = c->d_ids + i0;
-        // plans on the side stream, once chunk ci - 2 (same buffer set) has been applied
-        if (ci >= 2) HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_used[set], 0));
-        HIP_TRY(launch_plan16_reenc(pa, cn, c->ps_side));
-        HIP_TRY(hipEventRecord(c->ps_ev_zero[set], c->ps_side));
-        HIP_TRY(launch_plan16_reenc_rec(pa, cn, c->ps_side));  // runs beside this chunk's fixed pass
+        // lists + zeroing on st (after chunk ci - 2's apply, which read the same set, and ahead of the fixed
+        // pass, whose first kernels then do not queue behind the side stream's wide log-sum grid); the log
+        // sums and records on the side stream, beside the fixed pass
+        HIP_TRY(launch_plan16_reenc(pa, cn, st));
+        HIP_TRY(hipEventRecord(c->ps_ev_zero[set], st));
+        HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_zero[set], 0));
+        HIP_TRY(launch_plan16_reenc_rec(pa, cn, c->ps_side));
         HIP_TRY(hipEventRecord(c->ps_ev_plan[set], c->ps_side));
-        // the fixed pass over the stripe range (after the zeroing), + the received repair rows
-        HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_zero[set], 0));
+        // the fixed pass over the stripe range, + the received repair rows
         uint8_t* b = base + s0 * stripe_stride;
         if ((rc = run_cs(c, E, b, stripe_stride, symbol_stride, y, per, int64_t(S), uint64_t(ns), S, st))) return rc;
         fixed = c->last_kernel;
