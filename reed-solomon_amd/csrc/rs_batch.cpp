@@ -559,7 +559,8 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
                                 ns, st));
         HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_plan[set], 0));
         V1Args v{};
-        v.src = y - s0 * per;  // stripe ids index the range's rows: stripe s at y + (s - s0) * per
+        // stripe ids index the range's rows: stripe s at y + (s - s0) * per (the base itself is never read)
+        v.src = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(y) - uintptr_t(s0 * per));
         v.src_stripe = per;
         v.src_sym = int64_t(S);
         v.in_idx = pa.pin;
