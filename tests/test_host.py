@@ -424,3 +424,41 @@ def test_no_compiler_code_touches_in_flight_load_registers(tmp_path):
                 r = _regs(tok)
                 assert not (r and r[1] & pend[r[0]]), (sym, raw)
         assert checked > 0
+
+
+@pytest.mark.parametrize("k,r,t_info,t_rep", [(10, 4, 3, 1), (120, 32, 32, 0), (300, 64, 40, 24), (40, 20, 7, 13)])
+def test_reencode_solve_is_the_inverse_cauchy(k, r, t_info, t_rep):
+    """The closed form behind both per-stripe re-encode plans (k_plan_reenc_m8, k_plan16_reenc_rec):
+    with E the erased information slots, R' the first |E| surviving repair slots and T = E + (repair slots
+    not in R'), W'[p][q] = L_T(X_q) / ((X_q + X_p) L_T'(X_p)) inverts G[R', E] (G = the encode matrix from
+    the oracle, reed_solomon.c:338-441), so W' S'_R' recovers the erased information from the re-encode
+    differences. Checked over GF(2^16) on CPU; GF(256) codes (k + r <= 255) included."""
+    from _util import oracle_encode, oracle_positions
+    exp, log = gf_tables()
+    N = 65535
+    X = exp[oracle_positions(k, r).astype(np.int64)]
+    # G[:, Q] = the repair words of the unit information vector e_Q (one 2-byte word per symbol)
+    G = np.zeros((r, k), np.uint16)
+    for q in range(k):
+        buf = np.zeros((k + r, 2), np.uint8)
+        buf[q, 0] = 1
+        assert oracle_encode(k, r, buf) == 0
+        G[:, q] = buf[k:, 0].astype(np.uint16) | (buf[k:, 1].astype(np.uint16) << 8)
+    rng = np.random.default_rng(k * 7 + t_info)
+    E = np.sort(rng.choice(k, t_info, replace=False))
+    rep_er = np.sort(rng.choice(r, t_rep, replace=False)) + k
+    surv = [s for s in range(k, k + r) if s not in set(rep_er)]
+    Rp = np.array(surv[:t_info])
+    T = np.array(list(E) + [s for s in range(k, k + r) if s not in set(Rp)], dtype=np.int64)
+    assert len(T) == r
+
+    def logsum(x, excl=None):
+        return sum(int(log[int(x ^ X[e])]) for e in T if e != excl) % N
+
+    W = np.zeros((t_info, t_info), np.uint16)
+    for i, p in enumerate(E):
+        lr = logsum(X[p], excl=p)
+        for j, q in enumerate(Rp):
+            W[i, j] = exp[(logsum(X[q]) + 2 * N - lr - int(log[int(X[p] ^ X[q])])) % N]
+    prod = gf_apply(W, G[Rp - k][:, E])
+    assert np.array_equal(prod, np.eye(t_info, dtype=np.uint16))
