@@ -513,6 +513,36 @@ def test_decode_batch_m16_per_stripe_route(k, r, S, n, ps):
     assert np.array_equal(dev.cpu().numpy()[:, :k], got[:, :k])
 
 
+def test_decode_batch_m16_per_stripe_reenc_falls_back():
+    """m16_ps 2 needs the codec's encode on the GF(2^16) route (k >= 64 inputs): a code with k = 40 (k + r >
+    255) encodes densely, so its per-stripe batches take the syndrome route -- bit-exact vs the oracle."""
+    k, r, S, n = 40, 230, 1024, 6
+    rng = np.random.default_rng(40)
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0x40)
+    codec = rs_amd.Codec(k, r)
+    codec.set_option("m16_ps", 2)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.cpu().numpy()
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k + r, int(rng.integers(1, r + 1)), replace=False)] = True
+    host = full.copy()
+    host[pats] = rng.integers(0, 256, (int(pats.sum()), S), dtype=np.uint8)
+    dev.copy_(torch.from_numpy(host))
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert ps16_kernel_ok(codec.last_kernel, 1), codec.last_kernel
+    got = dev.cpu().numpy()
+    assert np.array_equal(got[:, :k], full[:, :k])
+    for s in range(n):
+        want = host[s].copy()
+        want[pats[s]] = 0
+        assert oracle_decode(k, r, want, pats[s], int(pats[s].sum())) == 0
+        assert np.array_equal(got[s, :k], want[:k]), f"stripe {s}"
+
+
 @pytest.mark.parametrize("ps,overlap", [(1, 0), (1, 1), (2, 0)])
 @pytest.mark.parametrize("chunk", [1, 3, 7])
 def test_decode_batch_m16_per_stripe_route_chunks(chunk, ps, overlap):
