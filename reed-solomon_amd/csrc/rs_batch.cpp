@@ -501,8 +501,7 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     if ((rc = grow(&c->d_ps_rec, c->ps_rec_cap, size_t(2 * rec_set)))) return rc;
     if ((rc = grow(&c->d_ps_small, c->ps_small_cap, size_t(2 * small)))) return rc;
     if (!c->ps_side) HIP_TRY(hipStreamCreateWithFlags(&c->ps_side, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&c->ps_ev_entry, &c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1],
-                          &c->ps_ev_used[0], &c->ps_ev_used[1]})
+    for (hipEvent_t* e : {&c->ps_ev_zero[0], &c->ps_ev_zero[1], &c->ps_ev_plan[0], &c->ps_ev_plan[1]})
         if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, sel_masks, size_t(nsel * n)}})))
         return rc;
@@ -523,9 +522,6 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     pa.symbol_stride = symbol_stride;
     pa.S = int64_t(S);
     uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
-    // the side stream starts after the caller's earlier work on st (the plans zero erased slots)
-    HIP_TRY(hipEventRecord(c->ps_ev_entry, st));
-    HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_entry, 0));
     std::string fixed;
     for (size_t ci = 0; ci < chunks.size(); ++ci) {
         const int64_t i0 = chunks[ci].first, cn = chunks[ci].second - i0;
@@ -545,7 +541,8 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         pa.ids = c->d_ids + i0;
         // lists + zeroing on st (after chunk ci - 2's apply, which read the same set, and ahead of the fixed
         // pass, whose first kernels then do not queue behind the side stream's wide log-sum grid); the log
-        // sums and records on the side stream, beside the fixed pass
+        // sums and records on the side stream, beside the fixed pass (its wait on ev_zero orders it after
+        // everything earlier on st, chunk ci - 2's apply included)
         HIP_TRY(launch_plan16_reenc(pa, cn, st));
         HIP_TRY(hipEventRecord(c->ps_ev_zero[set], st));
         HIP_TRY(hipStreamWaitEvent(c->ps_side, c->ps_ev_zero[set], 0));
@@ -577,7 +574,6 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.K = rmax;
         v.R = rmax;
         HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
-        HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
     }
     if ((rc = E.note_use(st))) return rc;
     c->last_kernel = "ps16r+" + fixed + "+xor+apply_m16_v1_ps";
