@@ -82,14 +82,16 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m16_cs_col"   route kernels' block layout: 256 (default) or 1024 bytes per column unit
  *   "m16_cs_thread" route syndromes: 1 k_cs16t, threaded code blocks at full VALU rate (default); 0 k_cs16,
  *                  gpr-indexed subset-table lookups
- * The timing ablations (m8_mode 10-13, 15-17, 19; m16_mode 1; "stamp_buffer") exist only in the
- * diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
+ * The timing ablations (m8_mode 10-13, 15-17, 19, 21; m8_ps_kernel 6, 7; m16_mode 1; "stamp_buffer") exist
+ * only in the diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Device scratch of a codec only grows with the launches it serves, and is reused by later calls: the
- * GF(2^16) per-stripe route of rsg_decode_batch keeps two record sets of up to m16_ps_rec_mib (1 GiB each by
- * default) and two syndrome buffers of up to 1 GiB; the GF(256) syndrome route two syndrome buffers of up
- * to 1 GiB; the route / re-encode decodes up to 1 GiB each; the host pipelines two 256 MiB batch buffers.
+ * GF(2^16) per-stripe routes of rsg_decode_batch keep two record sets of up to m16_ps_rec_mib (1 GiB each by
+ * default) and two syndrome buffers of up to 1 GiB (the re-encode variant: one 1 GiB fixed-pass buffer plus
+ * the encode route's 1 GiB syndrome buffer); the GF(256) fixed pass one buffer of up to 1 GiB (two with
+ * m8_syn_overlap); the route / re-encode decodes up to 1 GiB each; the host pipelines two 256 MiB batch
+ * buffers.
  * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it (plans stay cached;
  * later calls grow it again). */
 int rsg_codec_trim(rsg_codec_t* c);
