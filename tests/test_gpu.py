@@ -1295,7 +1295,8 @@ def test_release_build_ignores_diagnostic_knobs():
     set, a fresh process still encodes and decodes bit-exactly through the same XOR kernel (same content
     hash in its name) as without them."""
     codec = rs_amd.Codec(128, 32)
-    for name, value in [("m8_mode", v) for v in (10, 11, 12, 13, 15, 16, 17, 19)] + [("m16_mode", 1), ("stamp_buffer", 1)]:
+    for name, value in ([("m8_mode", v) for v in (10, 11, 12, 13, 15, 16, 17, 19, 21)] + [("m16_mode", 1), ("stamp_buffer", 1)]
+                        + [("m8_ps_kernel", 6), ("m8_ps_kernel", 7)]):
         with pytest.raises(rs_amd.RSError):
             codec.set_option(name, value)
     import os
