@@ -136,10 +136,14 @@ __device__ __forceinline__ uint32_t m8_v1_out(const uint32_t* lt, int p, const u
 typedef int32_t i32x16s __attribute__((ext_vector_type(16)));
 
 // The 32 output slots of a tile (out[0..31], 16-byte aligned, read-only) into SGPRs: two SMEM loads and
-// one wait, instead of one scalar round trip per output.
+// one wait, instead of one scalar round trip per output. The outputs are early-clobber: the second load
+// reads the base after the first was issued, and SMEM does not interlock its results, so a base placed
+// inside o0 could be overwritten in flight and the second load would fetch from o0's data as an address
+// (round 4's illegal-address fault: s_load_dwordx16 s[8:23], s[10:11] then s_load_dwordx16 s[72:87],
+// s[10:11], 0x40 -- DESIGN.md section 7; scripts/isa_hazards.py checks every kernel for this class).
 __device__ __forceinline__ void sload32(const int32_t* out, i32x16s& o0, i32x16s& o1) {
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(o0), "=s"(o1)
+                 : "=&s"(o0), "=&s"(o1)
                  : "s"(out)
                  : "memory");
 }

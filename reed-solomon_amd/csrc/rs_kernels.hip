@@ -955,7 +955,7 @@ __global__ void __launch_bounds__(256) k_cs16(Cs16Args a) {
     // prologue: group 0's inputs in flight, group 1's offsets and group 0's record requested
     asm volatile(
 #include "gen/m8_idx_asm_cs16_pro.inc"
-        : "={v[136:151]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(ra), [t0] "=&v"(t0)
+        : "=&{v[136:151]}"(ld), "=&{s[76:91]}"(goff), "=&{s[40:55]}"(ra), [t0] "=&v"(t0)
         : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
         : "memory");
     rb = 0;
@@ -1074,7 +1074,7 @@ __global__ void __launch_bounds__(256) k_bs16(Cs16Args a) {
     uint32_t t0;
     asm volatile(
 #include "gen/m8_idx_asm_cs16_pro.inc"
-        : "={v[136:151]}"(ld), "={s[76:91]}"(goff), "={s[40:55]}"(ra), [t0] "=&v"(t0)
+        : "=&{v[136:151]}"(ld), "=&{s[76:91]}"(goff), "=&{s[40:55]}"(ra), [t0] "=&v"(t0)
         : [g0] "s"(goffs), [r0] "s"(rec), [rsrc] "s"(rsrc), [lane] "v"(col)
         : "memory");
     rb = 0;

@@ -1,0 +1,83 @@
+"""CPU check of every gfx950 kernel the libraries carry, and of the hiprtc-specialised kernels, for the
+fault class behind GPUTEST_r04's illegal memory access: a register read while a memory load into it
+is still in flight (CDNA does not interlock memory results; inline asm whose outputs are not
+early-clobber lets the compiler place an asm input inside an asm output).
+
+Round 4's instance: `sload32` (csrc/rs_device.h) compiled in rs_v1jit to
+    s_load_dwordx16 s[8:23], s[10:11], 0x0
+    s_load_dwordx16 s[72:87], s[10:11], 0x40
+The same helper put the same pattern into the production per-stripe solve k_apply_m8_v1<0>.
+No GPU is used: the code objects are disassembled with the ROCm llvm-objdump."""
+import ctypes
+import os
+import shutil
+import sys
+
+import numpy as np
+import pytest
+
+from _util import REPO
+
+sys.path.insert(0, os.path.join(REPO, "scripts"))
+import isa_hazards  # noqa: E402
+
+import rs_amd  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not os.path.exists(f"{isa_hazards.LLVM}/llvm-objdump"), reason="no ROCm llvm-objdump")
+PKG = os.path.join(REPO, "reed-solomon_amd")
+
+
+def _check(path):
+    found = isa_hazards.hazards(isa_hazards.disassemble(path))
+    assert not found, "\n".join(f"{f} @{a}: {i}  in flight {r}" for f, a, i, r in found)
+
+
+def test_checker_flags_the_round4_pattern():
+    """The checker itself: the two SMEM loads of round 4's rs_v1jit, and a clean variant."""
+    bad = """
+0000000000001800 <k>:
+\ts_waitcnt lgkmcnt(0)                                       // 00000000321C: BF8CC07F
+\ts_load_dwordx16 s[8:23], s[10:11], 0x0                     // 000000003224: C0120205 00000000
+\ts_load_dwordx16 s[72:87], s[10:11], 0x40                   // 00000000322C: C0121205 00000040
+\ts_waitcnt lgkmcnt(0)                                       // 000000003234: BF8CC07F
+"""
+    found = isa_hazards.hazards(bad)
+    assert len(found) == 1 and found[0][3] == [("s", 10), ("s", 11)], found
+    good = bad.replace("s[8:23], s[10:11], 0x0", "s[24:39], s[10:11], 0x0")
+    assert not isa_hazards.hazards(good)
+    # a VMEM result read before its vmcnt wait; then the same after the wait
+    vm = """
+0000000000000000 <k2>:
+\tglobal_load_dword v4, v[2:3], off                          // 000000000000: DC508000 047F0002
+\tv_xor_b32_e32 v5, v4, v5                                   // 000000000008: 2A0A0B04
+\ts_waitcnt vmcnt(0)                                         // 00000000000C: BF8C0F70
+\tv_xor_b32_e32 v5, v4, v5                                   // 000000000010: 2A0A0B04
+"""
+    found = isa_hazards.hazards(vm)
+    assert [f[1] for f in found] == ["8"], found
+
+
+@pytest.mark.parametrize("lib", ["librs_amd.so", "librs_amd_diag.so"])
+def test_library_kernels_have_no_inflight_reads(lib):
+    path = os.path.join(PKG, lib)
+    if not os.path.exists(path):
+        pytest.skip(f"{lib} not built")
+    _check(path)
+
+
+# matrix-specialised kernels: (k, r, erasure pattern or None). 128 x 64 is past the XOR kernel's work
+# bound (K * R > 6144), so it compiles the nibble-table rs_v1jit -- the library's default for such shapes
+JIT_SHAPES = [(10, 4, None), (128, 32, None), (128, 64, None), (128, 64, "bench")]
+
+
+@pytest.mark.parametrize("k,r,pattern", JIT_SHAPES)
+def test_jit_kernels_have_no_inflight_reads(k, r, pattern, tmp_path, monkeypatch):
+    monkeypatch.setenv("RS_AMD_JIT_CACHE", str(tmp_path))
+    er = rs_amd.bench_pattern(k, r) if pattern else None
+    rs_amd.jit_precompile(k, r, er)  # raises on failure
+    objs = [os.path.join(tmp_path, f) for f in os.listdir(tmp_path) if f.endswith(".co")]
+    assert objs, "no specialised kernel compiled"
+    if (k, r) == (128, 64):
+        assert all(os.path.basename(o).startswith("v1_") for o in objs), objs  # the nibble-table rs_v1jit
+    for o in objs:
+        _check(o)
