@@ -505,7 +505,9 @@ def main():
     opts = {"auto": {}, "jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(jit=0, m8_mode=18),
             "idx": dict(jit=0, m8_mode=2), "table": dict(jit=0, m8_mode=0), "mask": dict(jit=0, m8_mode=1),
             "m16c": {}}[args.kernel]
-    codec = rs_amd.Codec(k, r, device=local, **opts)
+    # the A/B families idx / table / mask live in the diagnostic library (never a reported value's default)
+    lib = rs_amd.diag_module() if args.kernel in ("idx", "table", "mask") else rs_amd
+    codec = lib.Codec(k, r, device=local, **opts)
     if args.kernel == "m16c":  # GF(2^16) codes: the compiled kernel
         codec.set_option("m16_mode", 2)
     for o in args.opt:

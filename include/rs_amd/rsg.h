@@ -208,6 +208,13 @@ int64_t rsg_symbol_pool_cap(int64_t bytes);
 int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
                   int32_t* fin, int32_t* fin_off);
 const char* rsg_version(void);
+/* 1 when checked launches are on (environment RS_AMD_CHECK set and not "0" at the first call of the
+ * process), else 0. In checked mode every launch group is followed by a device wait and an error read: a
+ * device fault is reported on stderr at the call that queued it (its kernel, the code's k / r, the plan's
+ * K / R and slot ranges, stripes and symbol size) and the call returns RS_ERR_DEVICE; plans' slot lists
+ * are bounds-checked on the host before their first launch (RS_ERR_INVALID). Diagnosis only: each
+ * launch then costs a device round trip. Host only. */
+int rsg_check_enabled(void);
 
 #ifdef __cplusplus
 }

@@ -49,11 +49,12 @@ extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 
 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     if (!c || !name) return RS_ERR_INVALID;
+    // The release build accepts only knobs that select a parity-tested production path:
+    // option-only A/B families, overlap variants and block layouts are diagnostic-build knobs (make diag).
     if (!std::strcmp(name, "m8_mode")) {
         if (value < 0 || (value > 4 && value < 10) || value > 21) return RS_ERR_INVALID;
-#ifndef RS_AMD_DIAG  // 10-13, 15, 16, 19: timing ablations with wrong results; 17, 21: s_memtime stamps
-        if ((value >= 10 && value <= 13) || (value >= 15 && value <= 17) || value == 19 || value == 21)
-            return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 18 / 20: the V = 1 kernels; the rest are A/B families, ablations (wrong results), stamps
+        if (value != 18 && value != 20) return RS_ERR_INVALID;
 #endif
         c->m8_mode = int(value);
         return 0;
@@ -126,6 +127,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     if (!std::strcmp(name, "m16_cs_col")) {  // k_cs16 / k_bs16 block layout (results identical)
         if (value != 256 && value != 1024) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG
+        if (value != 256) return RS_ERR_INVALID;  // 1024: A/B layout, diagnostic build
+#endif
         c->m16_cs_col = int(value);
         return 0;
     }
@@ -148,6 +152,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     if (!std::strcmp(name, "m16_cs_overlap")) {  // one-pattern syndrome route: syndromes beside the second stage
         if (value < 0 || value > 1) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG
+        if (value) return RS_ERR_INVALID;  // measured slower: diagnostic build
+#endif
         c->cs_overlap = int(value);
         return 0;
     }
@@ -170,19 +177,25 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
         if (value < 0 || value > 7) return RS_ERR_INVALID;
-#ifndef RS_AMD_DIAG  // 6: timing ablation with wrong results, 7: phase stamps
-        if (value >= 6) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 0 / 3: the ring kernels; 1, 2, 4, 5: A/B kernels; 6: ablation (wrong results); 7: stamps
+        if (value != 0 && value != 3) return RS_ERR_INVALID;
 #endif
         c->m8_ps_kernel = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_cpb")) {  // per-stripe GF(256) solve: column chunks per workgroup
         if (value < 1 || value > 64) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG
+        if (value != 1) return RS_ERR_INVALID;  // k_apply_m8_v1<6>: measured slower past 2, diagnostic build
+#endif
         c->m8_ps_cpb = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m8_syn_overlap")) {  // GF(256) per-stripe syndrome route: overlapped chunks
         if (value < 0 || value > 1) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG
+        if (value) return RS_ERR_INVALID;  // measured no faster (profiles/r4/ps8_route2.md): diagnostic build
+#endif
         c->m8_syn_overlap = int(value);
         return 0;
     }
@@ -252,13 +265,67 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
                   uint8_t* dst, int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S,
                   hipStream_t st, const int32_t* d_ids, bool dst_local);
 
+bool check_mode() {
+    static const bool on = [] {
+        const char* e = std::getenv("RS_AMD_CHECK");
+        return e && *e && std::strcmp(e, "0") != 0;
+    }();
+    return on;
+}
+
+static void slot_range(const std::vector<int32_t>& v, size_t n, int64_t& lo, int64_t& hi) {
+    lo = INT64_MAX;
+    hi = INT64_MIN;
+    for (size_t i = 0; i < std::min(n, v.size()); ++i) lo = std::min<int64_t>(lo, v[i]), hi = std::max<int64_t>(hi, v[i]);
+}
+
+int check_plan_slots(const rsg_codec_t* c, const DevPlan& p) {
+    const int64_t n = int64_t(c->k) + c->r;
+    int64_t ilo, ihi, olo, ohi;
+    slot_range(p.in_slots, size_t(p.K), ilo, ihi);
+    slot_range(p.out_slots, size_t(p.R), olo, ohi);
+    if ((p.K && (ilo < 0 || ihi >= n)) || (p.R && (olo < 0 || ohi >= n))) {
+        std::fprintf(stderr,
+                     "librs_amd: RS_AMD_CHECK: plan K=%d R=%d has slots outside [0, %lld): in [%lld, %lld], out [%lld, %lld]\n",
+                     p.K, p.R, static_cast<long long>(n), static_cast<long long>(ilo), static_cast<long long>(ihi),
+                     static_cast<long long>(olo), static_cast<long long>(ohi));
+        return RS_ERR_INVALID;
+    }
+    return 0;
+}
+
+int check_launch(const rsg_codec_t* c, const DevPlan* p, const char* where, uint64_t n_stripes, uint64_t S) {
+    const hipError_t sync = hipDeviceSynchronize();
+    const hipError_t last = hipGetLastError();
+    const hipError_t e = sync != hipSuccess ? sync : last;
+    if (e == hipSuccess) return 0;
+    int64_t ilo = 0, ihi = -1, olo = 0, ohi = -1;
+    if (p) {
+        slot_range(p->in_slots, size_t(p->K), ilo, ihi);
+        slot_range(p->out_slots, size_t(p->R), olo, ohi);
+    }
+    std::fprintf(stderr,
+                 "librs_amd: RS_AMD_CHECK: device error '%s' after %s: kernel %s, code k=%d r=%d, plan K=%d R=%d, "
+                 "in slots [%lld, %lld], out slots [%lld, %lld], %llu stripes x %llu bytes\n",
+                 hipGetErrorString(e), where, c ? c->last_kernel.c_str() : "-", c ? c->k : 0, c ? c->r : 0,
+                 p ? p->K : 0, p ? p->R : 0, static_cast<long long>(ilo), static_cast<long long>(ihi),
+                 static_cast<long long>(olo), static_cast<long long>(ohi), static_cast<unsigned long long>(n_stripes),
+                 static_cast<unsigned long long>(S));
+    return RS_ERR_DEVICE;
+}
+
 int run_plan(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, int64_t src_sym, uint8_t* dst,
              int64_t dst_stripe, int64_t dst_sym, uint64_t n_stripes, uint64_t S, hipStream_t st,
              const int32_t* d_ids, bool dst_local) {
     if (p.R == 0 || n_stripes == 0 || S == 0) return 0;
+    if (check_mode() && !p.slots_checked) {
+        if (int rc = check_plan_slots(c, p)) return rc;
+        p.slots_checked = true;
+    }
     const int rc = run_plan_body(c, p, src, src_stripe, src_sym, dst, dst_stripe, dst_sym, n_stripes, S, st, d_ids,
                                  dst_local);
     const int rc2 = p.note_use(st);  // after the launches (also a failed call's partial ones)
+    if (!rc && !rc2) RS_CHECKPOINT(c, &p, "run_plan", n_stripes, S);
     return rc ? rc : rc2;
 }
 
@@ -365,6 +432,7 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
+    a.nslots = int32_t(c->k) + c->r;  // every list of a dispatcher plan names codec (or syndrome) slots
     const bool m8_generic = p.m == 8 && p.d_idx && (a.mode == 18 || a.mode == 20 || a.mode == 21) && !(xj_ok && p.xj) && !(jit_ok && p.jit);
     if ((p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) || m8_generic) {  // split-K scratch for small grids
         int64_t need = 0;
@@ -727,3 +795,5 @@ extern "C" int rsg_gamma_tables(uint16_t* lbyte, uint16_t* ibyte, uint8_t* red) 
 }
 
 extern "C" const char* rsg_version(void) { return RSG_VERSION; }
+
+extern "C" int rsg_check_enabled(void) { return rsamd::check_mode() ? 1 : 0; }

@@ -240,6 +240,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
             HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
+            RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
         c->last_kernel = std::string(c->syn_route == 2 ? "reenc_xj" : "syn_xj") + "+apply_m8_v1_ps" + (ovl ? "(overlap)" : "");
@@ -280,6 +281,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.ps_out = out_stride;
         v.ps_idx = idx_stride;
         HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
+        RS_CHECKPOINT(c, nullptr, "per-stripe GF(256) survivor plans (apply_m8_ps)", uint64_t(cn), S);
     }
     c->last_kernel = "apply_m8_v1_ps";
     return scratch_release(c, st);
@@ -574,6 +576,7 @@ int decode_batch_m16_ps_reenc(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.K = rmax;
         v.R = rmax;
         HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
+        RS_CHECKPOINT(c, &E, "per-stripe GF(2^16) re-encode solve (apply_m16_ps)", uint64_t(cn), S);
     }
     if ((rc = E.note_use(st))) return rc;
     c->last_kernel = "ps16r+" + fixed + "+xor+apply_m16_v1_ps";
@@ -768,6 +771,7 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
         v.K = D;
         v.R = rmax;
         HIP_TRY(launch_apply_m16_ps(v, cn, int64_t(S), tiles, st));
+        RS_CHECKPOINT(c, syn, "per-stripe GF(2^16) syndrome solve (apply_m16_ps)", uint64_t(cn), S);
         HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
     }
     if ((rc = syn->note_use(st))) return rc;

@@ -124,6 +124,7 @@ struct DevPlan {
     std::unique_ptr<DevPlan> route;
     std::vector<uint8_t> erased;  // the pattern (empty: encode), to build `dense`
     int64_t uses = 0;                // launches of this plan (JIT policy)
+    bool slots_checked = false;      // check mode: slot lists bounds-checked on the host
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
     size_t blob_cap = 0;             // its size class (plan_pool)
     // stream-ordered build: the upload (and device fill) ran on `built_on`; `ready` marks its end, so a
@@ -373,6 +374,22 @@ struct rsg_codec {
 };
 
 namespace rsamd {
+
+// ------------------------------------------------------------------ checked launches (rs_api.cpp)
+// RS_AMD_CHECK=1 (read once per process): after every launch group the library waits for the device and
+// reads the sticky error, so a fault is reported at the call that queued it, with its kernel, the plan's
+// K / R and slot ranges, and the call returns RS_ERR_DEVICE; plans' slot lists are bounds-checked on the
+// host before their first launch. Costs a device round trip per launch: diagnosis only.
+bool check_mode();
+// after a launch group: 0, or RS_ERR_DEVICE with the report on stderr (p may be null)
+int check_launch(const rsg_codec_t* c, const DevPlan* p, const char* where, uint64_t n_stripes, uint64_t S);
+// host-side bounds of a plan's slot lists against the codec's k + r slots (check mode, first launch)
+int check_plan_slots(const rsg_codec_t* c, const DevPlan& p);
+#define RS_CHECKPOINT(c, p, where, n, S)                                              \
+    do {                                                                              \
+        if (rsamd::check_mode())                                                      \
+            if (int _rc = rsamd::check_launch((c), (p), (where), (n), (S))) return _rc; \
+    } while (0)
 
 // ------------------------------------------------------------------ rs_api.cpp
 // Launches below this many bytes do not count toward decode specialisation (a compile costs far more

@@ -104,6 +104,19 @@ __device__ __forceinline__ int32_t sload(const int32_t* p) {
     return v;
 }
 
+// Diagnostic builds: a slot index outside [0, nslots) is reported (kernel, block, list position, value) and
+// the access it would address is skipped or redirected to slot 0; release and hiprtc builds compile nothing.
+#if defined(RS_AMD_DIAG) && !defined(RS_JIT_SOURCE)
+#define RS_SLOT_OK(a, slot, what, pos)                                                                          \
+    ((a).nslots <= 0 || ((slot) >= 0 && (slot) < (a).nslots) ||                                                 \
+     ((threadIdx.x & 63) == 0 &&                                                                                 \
+      (printf("librs_amd diag: %s[%d] = %d outside [0, %d) in block (%d, %d)\n", (what), int(pos), int(slot),    \
+              (a).nslots, int(blockIdx.x), int(blockIdx.y)),                                                     \
+       false)))
+#else
+#define RS_SLOT_OK(a, slot, what, pos) true
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -157,8 +170,10 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
                                             const u32x16& b1) {
     i32x16s o0, o1;
     sload32(out, o0, o1);
+    auto slot = [&](int p) { return p < 16 ? o0[p & 15] : o1[p & 15]; };
     auto at = [&](int p) {
-        return reinterpret_cast<uint32_t*>(dst + int64_t(p < 16 ? o0[p & 15] : o1[p & 15]) * a.dst_sym);
+        const int32_t s = slot(p);
+        return reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, s, "out_idx", p) ? s : 0) * a.dst_sym);
     };
     if (a.xor_dst) {  // g ^ (W S), in rounds of LB loads (NB = 2 holds twice the accumulators)
         constexpr int LB = LBX ? LBX : NB == 2 ? 16 : 32;
@@ -242,7 +257,9 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     // chunk loop carries no 64-bit per-lane pointer
     const uint8_t* gsb = a.src + stripe * a.src_stripe + cbeg * 1024;
     auto issue = [&](int i) {
-        dma16(gsb + int64_t(sload(in_idx + i)) * a.src_sym + 16 * lane, ring_lds + uint32_t(i % RING_SLOTS) * 1024u);
+        int32_t s = sload(in_idx + i);
+        if (!RS_SLOT_OK(a, s, "in_idx", i)) s = 0;  // diagnostic builds: report, read slot 0 instead
+        dma16(gsb + int64_t(s) * a.src_sym + 16 * lane, ring_lds + uint32_t(i % RING_SLOTS) * 1024u);
     };
     const int nb = (K + 3) / 4;
     auto mine = [&](int lo, int hi) {  // this wave's outstanding DMA instructions for batches [lo, hi]

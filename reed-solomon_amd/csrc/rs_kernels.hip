@@ -426,6 +426,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_v1(V1Args a) {
     }
 }
 
+#ifdef RS_AMD_DIAG  // option-only per-stripe solve kernels (m8_ps_kernel 1 / 2): diagnostic build only
 // Per-stripe V = 1 apply without the LDS input ring, for the short solves of rsg_decode_batch (K = t <= r
 // inputs per stripe; at C3 32). The ring kernel's four waves of a 1 KiB chunk meet at a barrier every 4
 // inputs and wait for DMA bookkeeping: at K = 32 its waves spent a third of their time parked
@@ -552,6 +553,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_ps_w2(V1Args a) {
     else
         m8_ps_w2_body<false>(a, lt, local, stripe, col, tile, K, R);
 }
+#endif  // RS_AMD_DIAG
 
 template <int ABL, int PD>
 __global__ void __launch_bounds__(256) k_apply_m8_idx(ApplyArgs a, const int32_t* __restrict__ in_idx) {
@@ -1186,6 +1188,7 @@ V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
     v.R = a.R;
     v.nchunks = nchunks_1k;
     v.ids = a.ids;
+    v.nslots = a.nslots;
     return v;
 }
 
@@ -1201,59 +1204,64 @@ void launch_m8_tail(const ApplyArgs& a, int64_t n_stripes, unsigned tiles, hipSt
 template <int RT>
 static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t st) {
     dim3 grid(unsigned(n_stripes * a.nchunks), unsigned((a.R + RT - 1) / RT));
-    if (RT == 32 && a.mode >= 2 && a.idx) {
-        // mode 2: production kernel (LDS-DMA ring over full chunks + register-ring tail);
-        // 3 / 4: register ring 4 / 8 only; 10..16: the LDS-DMA kernel with asm variant ABL = mode - 9
-        // (timing ablations, wrong results except 14 = "full" schedule): 10 no index switching,
-        // 11 multiples + tables only, 12 lookups only, 13 loads only, 14 split schedule with the multiply-based xtime,
-        // 15 no gpr-index mode
-        if (a.mode == 18 || a.mode == 19 || a.mode == 20 || a.mode == 21) {  // V = 1 kernel (19: without gpr-index mode, timing
-                                                             // only; 20: the one-table step)
-            const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
-            if (full > 0) {
-                V1Args v = v1_args(a, full, nullptr);
-                v.kslices = a.mode != 19 && a.mode != 21 ? m8_kslices(a, n_stripes, nullptr) : 1;
-                v.stamps = a.stamps;
-                v.partial = a.scratch;
-                dim3 g(unsigned(n_stripes * full), grid.y, unsigned(v.kslices));
+    // Release build: the generic GF(256) kernels are the V = 1 ones (mode 20: one nibble table per input,
+    // k_apply_m8_v1<2>, the default; mode 18: two tables, k_apply_m8_v1<0>, the per-stripe solve's kernel)
+    // and the register-ring tail kernel. Every other family is an option-only A/B or ablation and lives in
+    // the diagnostic build (make diag): 0 / 1 compiler-indexed table / SGPR-mask kernels, 2 the LDS-DMA
+    // kernel, 3 / 4 register ring 4 / 8 over whole symbols, 10..17 LDS-DMA ablations and stamps, 19 / 21 V = 1
+    // ablation and stamps.
+    if (RT == 32 && a.idx && (a.mode == 18 || a.mode == 19 || a.mode == 20 || a.mode == 21)) {
+        const int64_t full = (a.nbytes / 2048) * 2;  // 1 KiB chunks up to the last full 2 KiB boundary
+        if (full > 0) {
+            V1Args v = v1_args(a, full, nullptr);
+            v.kslices = a.mode != 19 && a.mode != 21 ? m8_kslices(a, n_stripes, nullptr) : 1;
+            v.stamps = a.stamps;
+            v.partial = a.scratch;
+            dim3 g(unsigned(n_stripes * full), grid.y, unsigned(v.kslices));
 #ifdef RS_AMD_DIAG
-                if (a.mode == 19)
-                    hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
-                else
+            if (a.mode == 19)
+                hipLaunchKernelGGL((k_apply_m8_v1<1>), g, dim3(256), 0, st, v);
+            else if (a.mode == 21)
+                hipLaunchKernelGGL((k_apply_m8_v1<5>), g, dim3(256), 0, st, v);
+            else
+#else
+            if (a.mode == 19 || a.mode == 21) return hipErrorInvalidValue;
 #endif
-                if (a.mode == 20)
-                    hipLaunchKernelGGL((k_apply_m8_v1<2>), g, dim3(256), 0, st, v);
-#ifdef RS_AMD_DIAG
-                else if (a.mode == 21)
-                    hipLaunchKernelGGL((k_apply_m8_v1<5>), g, dim3(256), 0, st, v);
-#endif
-                else
-                    hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
-                if (v.kslices > 1) {
-                    const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
-                    hipLaunchKernelGGL(k_xor_slices, dim3(unsigned((rows + 255) / 256), unsigned(n_stripes)), dim3(256),
-                                       0, st, v, int64_t(n_stripes), int64_t(grid.y) * 32, cw);
-                }
+            if (a.mode == 20)
+                hipLaunchKernelGGL((k_apply_m8_v1<2>), g, dim3(256), 0, st, v);
+            else
+                hipLaunchKernelGGL((k_apply_m8_v1<0>), g, dim3(256), 0, st, v);
+            if (v.kslices > 1) {
+                const int64_t cw = full * 256, rows = int64_t(a.R) * cw;
+                hipLaunchKernelGGL(k_xor_slices, dim3(unsigned((rows + 255) / 256), unsigned(n_stripes)), dim3(256),
+                                   0, st, v, int64_t(n_stripes), int64_t(grid.y) * 32, cw);
             }
-            launch_m8_tail(a, n_stripes, grid.y, st);
-        } else if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15) || a.mode == 17) {
+        }
+        launch_m8_tail(a, n_stripes, grid.y, st);
+        return hipGetLastError();
+    }
+#ifdef RS_AMD_DIAG
+    if (RT == 32 && a.mode >= 2 && a.idx) {
+        // mode 2: LDS-DMA ring over full chunks + register-ring tail; 3 / 4: register ring 4 / 8 only;
+        // 10..16: the LDS-DMA kernel with asm variant ABL = mode - 9 (timing ablations, wrong results except
+        // 14 = "full" schedule): 10 no index switching, 11 multiples + tables only, 12 lookups only, 13 loads
+        // only, 14 split schedule with the multiply-based xtime, 15 no gpr-index mode; 17 stamps
+        if (a.mode == 2 || (a.mode >= 10 && a.mode <= 15) || a.mode == 17) {
             ApplyArgs f = a;
             f.nchunks = a.nbytes / 2048;
             if (f.nchunks > 0) {
                 dim3 g(unsigned(n_stripes * f.nchunks), grid.y);
                 switch (a.mode) {
                 case 14: hipLaunchKernelGGL((k_apply_m8_lds<5>), g, dim3(256), 0, st, f, a.in_idx); break;
-#ifdef RS_AMD_DIAG  // timing ablations (wrong results) and stamps: diagnostic build only (make diag)
                 case 10: hipLaunchKernelGGL((k_apply_m8_lds<1>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 11: hipLaunchKernelGGL((k_apply_m8_lds<2>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 12: hipLaunchKernelGGL((k_apply_m8_lds<3>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 13: hipLaunchKernelGGL((k_apply_m8_lds<4>), g, dim3(256), 0, st, f, a.in_idx); break;
                 case 15: hipLaunchKernelGGL((k_apply_m8_lds<6>), g, dim3(256), 0, st, f, a.in_idx); break;
-                case 17:  // production kernel with s_memtime phase counters (needs a.stamps)
+                case 17:  // the LDS-DMA kernel with s_memtime phase counters (needs a.stamps)
                     if (!a.stamps) return hipErrorInvalidValue;
                     hipLaunchKernelGGL((k_apply_m8_lds<0, true>), g, dim3(256), 0, st, f, a.in_idx);
                     break;
-#endif
                 default: hipLaunchKernelGGL((k_apply_m8_lds<0>), g, dim3(256), 0, st, f, a.in_idx); break;
                 }
             }
@@ -1266,19 +1274,19 @@ static hipError_t launch_m8(const ApplyArgs& a, int64_t n_stripes, hipStream_t s
             }
         } else if (a.mode == 4) {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 8>), grid, dim3(256), 0, st, a, a.in_idx);
-#ifdef RS_AMD_DIAG
         } else if (a.mode == 16) {  // loads only, register ring 4 (timing ablation, wrong results)
             hipLaunchKernelGGL((k_apply_m8_idx<4, 4>), grid, dim3(256), 0, st, a, a.in_idx);
-#endif
         } else {
             hipLaunchKernelGGL((k_apply_m8_idx<0, 4>), grid, dim3(256), 0, st, a, a.in_idx);
         }
-    }
-    else if (a.mode == 1)
+    } else if (a.mode == 1)
         hipLaunchKernelGGL((k_apply_m8<RT, 1>), grid, dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL((k_apply_m8<RT, 0>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
+#else
+    return hipErrorInvalidValue;  // no other generic GF(256) family in the release build
+#endif
 }
 
 template <int RT>
@@ -2297,6 +2305,10 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
+#ifndef RS_AMD_DIAG
+    // release build: the LDS-ring solve (0, one column chunk per workgroup) and its one-table variant (3)
+    if ((kernel != 0 && kernel != 3) || cpb > 1) return hipErrorInvalidValue;
+#else
     if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch
         V1Args f = v;
         f.nchunks = nbytes;
@@ -2304,6 +2316,7 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
                            dim3(256), 0, st, f);
         return hipGetLastError();
     }
+#endif
     const int64_t full = nbytes / 1024;
     if (full > 0) {
         V1Args f = v;
@@ -2311,22 +2324,22 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
         // the production ring kernel (0) walks cpb chunks per block (k_apply_m8_v1<6>); the others one
         f.cpb = kernel == 0 ? std::max(1, std::min<int>(cpb, int(full))) : 1;
         const int64_t blocks = n_sel * ((full + f.cpb - 1) / f.cpb);
-        if (kernel == 1)
-            hipLaunchKernelGGL(k_apply_m8_ps_w, dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
-        else if (kernel == 3)
+        if (kernel == 3)
             hipLaunchKernelGGL((k_apply_m8_v1<2>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
+#ifdef RS_AMD_DIAG  // option-only A/B kernels (1, 2, 4, 5, cpb > 1), the ablation (6) and the stamps (7)
+        else if (kernel == 1)
+            hipLaunchKernelGGL(k_apply_m8_ps_w, dim3(unsigned(n_sel * full), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 4)
             hipLaunchKernelGGL((k_apply_m8_v1<3>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 5)
             hipLaunchKernelGGL((k_apply_m8_v1<4>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
-#ifdef RS_AMD_DIAG
         else if (kernel == 6)  // timing ablation: fixed table registers, no index switches (wrong results)
             hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 7)  // the production kernel with phase stamps into f.stamps
             hipLaunchKernelGGL((k_apply_m8_v1<5>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
-#endif
         else if (f.cpb > 1)
             hipLaunchKernelGGL((k_apply_m8_v1<6>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
+#endif
         else
             hipLaunchKernelGGL((k_apply_m8_v1<0>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
     }

@@ -31,6 +31,7 @@ struct ApplyArgs {
     const int32_t* ids;      // optional [n_stripes] stripe indices (per-stripe erasure patterns); null = 0..n-1
     uint32_t* scratch;       // m = 16 split-K partials (codec-owned), scratch_bytes long; may be null
     int64_t scratch_bytes;
+    int32_t nslots;          // diagnostic builds: slot indices lie in [0, nslots) (V1Args::nslots); 0 = unchecked
 };
 // input slices of the split-K m = 16 launch over n_stripes (1 = no split) and the scratch it needs
 int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes);

@@ -531,6 +531,7 @@ int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, i
         a.dst_sym = dst_sym;
         a.units = int64_t(n_stripes) * a.nchunks;
         HIP_TRY(launch_bs16(a, st));
+        RS_CHECKPOINT(c, &p, "GF(2^16) route k_bs16", n_stripes, S);
         const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
         c->work_valu += steps * kValu_bs16;
         c->work_salu += steps * kSalu_bs16;
@@ -572,10 +573,12 @@ int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, i
         a.units = cn * a.nchunks;
         if (thr) {
             HIP_TRY(launch_cs16t(a, sy));
+            RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16t", uint64_t(cn), S);
             c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
             c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSaluStepCs16t;
         } else {
             HIP_TRY(launch_cs16(a, sy));
+            RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16", uint64_t(cn), S);
             const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
             c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
             c->work_salu += steps * kSalu_cs16a;

@@ -46,6 +46,10 @@ struct V1Args {
     // m8_v1_run: column chunks per block (<= 1: one; the grid's x then covers n_stripes * ceil(nchunks / cpb)
     // blocks). Not combined with split-K.
     int32_t cpb;
+    // diagnostic builds (RS_AMD_DIAG): slot indices read from in_idx / out_idx must lie in [0, nslots)
+    // (the codec's k + r); a violation is printed by the first lane of the wave and the access is
+    // skipped instead of faulting. 0 = unchecked.
+    int32_t nslots;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -36,6 +36,35 @@ class RSError(RuntimeError):
         self.rc = rc
 
 
+DIAG_LIB_PATH = os.path.join(HERE, "librs_amd_diag.so")
+
+
+def diag_module():
+    """A second instance of this module bound to the diagnostic library (librs_amd_diag.so: the option-only
+    A/B kernel families, ablations and stamps the release library does not carry), loaded beside the
+    release library in the same process. Raises ImportError when that library is not built."""
+    import importlib.util
+    import sys
+    name = "rs_amd_diag"
+    if name in sys.modules:
+        return sys.modules[name]
+    if not os.path.exists(DIAG_LIB_PATH):
+        raise ImportError(f"{DIAG_LIB_PATH} is missing: build it with `make -C {HERE} diag`")
+    spec = importlib.util.spec_from_file_location(name, os.path.abspath(__file__))
+    mod = importlib.util.module_from_spec(spec)
+    old = os.environ.get("RS_AMD_LIB")
+    os.environ["RS_AMD_LIB"] = DIAG_LIB_PATH
+    try:
+        spec.loader.exec_module(mod)
+    finally:
+        if old is None:
+            os.environ.pop("RS_AMD_LIB", None)
+        else:
+            os.environ["RS_AMD_LIB"] = old
+    sys.modules[name] = mod
+    return mod
+
+
 def build(force=False):
     """Compile librs_amd.so in-tree (hipcc --offload-arch=gfx950)."""
     import subprocess
@@ -109,6 +138,7 @@ class SymbolStatsT(ctypes.Structure):  # include/rs_amd/rsg.h rsg_symbol_stats_t
 _sig("rsg_symbol_stats", ctypes.c_int, ctypes.POINTER(SymbolStatsT))
 _sig("rsg_symbol_pool_cap", i64, i64)
 _sig("rsg_version", ctypes.c_char_p)
+_sig("rsg_check_enabled", ctypes.c_int)
 _sig("gf_create", P)
 _sig("gf_destroy", None, P)
 _sig("gf_mul_ee", u16, P, u16, u16)

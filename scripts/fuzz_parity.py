@@ -239,10 +239,12 @@ def one(family):
     dev = torch.from_numpy(host).cuda()
     kw = {"xj": dict(jit=1), "generic": dict(jit=0), "m16": {}, "route": {}, "reenc": {}, "batch": dict(batch_plans=1),
           "batch16": dict(batch_plans=1)}[family]
-    codec = rs_amd.Codec(k, r, **kw)
+    col = int(rng.choice([256, 1024])) if family in ("route", "reenc") else 256
+    # the 1 KiB route block layout is a diagnostic-build option (rs_amd.diag_module())
+    codec = (rs_amd.diag_module() if col == 1024 else rs_amd).Codec(k, r, **kw)
     if family in ("route", "reenc"):
         codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route at once
-        codec.set_option("m16_cs_col", int(rng.choice([256, 1024])))  # route kernels' block layout
+        codec.set_option("m16_cs_col", col)  # route kernels' block layout
     codec.encode(dev)
     torch.cuda.synchronize()
     enc_kernel = codec.last_kernel

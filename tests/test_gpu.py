@@ -1,5 +1,8 @@
-"""GPU parity tests (MI355X): every golden vector of the compiled reference through the C ABI, with
-each kernel variant, plus multi-stripe round trips checked against the CPU oracle.
+"""GPU parity tests (MI355X) of the production paths: every golden vector of the compiled reference through
+the C ABI under the library's default policy, plus multi-stripe round trips checked against the CPU oracle.
+The non-default kernel variants (options of the release library, and the A/B families of the diagnostic
+library) run the same checks afterwards, in tests/test_gpu_variants.py, so that no option-only family can
+hide the production path behind a failure.
 
 All tests run in one process; they need librs_amd.so built for gfx950 (no CPU fallback exists)."""
 import ctypes
@@ -16,15 +19,32 @@ from _util import (EXTRA_OPS, case, case_inputs, check_golden, extra_inputs, gen
 
 pytestmark = pytest.mark.gpu
 
-# every m <= 8 kernel family: jit = matrix-specialised bit-plane XOR kernel (rs_xj, hiprtc), v1jit =
-# matrix-specialised nibble-table V = 1 kernel (rs_v1jit), v1 / idx = generic gpr-index
-# kernels (one / two dwords per lane), table / mask = compiler-indexed reference kernels; "auto" is
-# the library default policy (JIT for encode, generic then JIT for repeated decode patterns)
+# Kernel variants. "auto" is the library default policy (XOR kernel for encode, generic then XOR kernel for
+# repeated decode patterns): the only one this file runs. Release-library options (test_gpu_variants.py):
+# jit = matrix-specialised bit-plane XOR kernel forced (rs_xj, hiprtc), v1jit = matrix-specialised
+# nibble-table V = 1 kernel (rs_v1jit: the default for shapes the XOR kernel rejects), v1 / v1h = the generic
+# V = 1 kernels (two / one nibble tables per input; v1h is the default generic kernel), cs_idx = the GF(2^16)
+# route's syndromes on the gpr-indexed k_cs16 (the fallback of plans without threaded records).
+# Diagnostic-library A/B families (DIAG_VARIANTS, librs_amd_diag.so): idx = LDS-DMA gpr-index kernel, table /
+# mask = compiler-indexed reference kernels.
 VARIANTS = {"jit": dict(jit=1), "v1jit": dict(jit=1, xj=0), "v1": dict(m8_mode=18, jit=0), "v1h": dict(m8_mode=20, jit=0), "idx": dict(m8_mode=2, jit=0),
             "table": dict(m8_mode=0, jit=0), "mask": dict(m8_mode=1, jit=0), "auto": dict(), "cs_idx": dict()}
+DIAG_VARIANTS = ("idx", "table", "mask")
 # codec options of a variant (set after construction): "cs_idx" runs the GF(2^16) route's syndromes on
 # the gpr-indexed k_cs16 instead of the default threaded k_cs16t
 VARIANT_OPTS = {"cs_idx": {"m16_cs_thread": 0}}
+
+
+def lib_for(variant):
+    """The rs_amd module of a variant's library (the diagnostic one for the A/B families)."""
+    return rs_amd.diag_module() if variant in DIAG_VARIANTS else rs_amd
+
+
+def codec_for(variant, k, r):
+    c = lib_for(variant).Codec(k, r, **VARIANTS[variant])
+    for name, value in VARIANT_OPTS.get(variant, {}).items():
+        c.set_option(name, value)
+    return c
 CS_DEFAULT = "cs16t"  # rsg_last_kernel prefix of the default GF(2^16) syndrome kernel
 
 
@@ -41,8 +61,8 @@ def run_case_gpu(c, variant, options=None):
         buf, er = case_inputs(c, s)
         host[s, :, :S] = buf
     dev = torch.from_numpy(host).cuda()
-    codec = rs_amd.Codec(k, r, **VARIANTS[variant])
-    for name, value in {**VARIANT_OPTS.get(variant, {}), **(options or {})}.items():
+    codec = codec_for(variant, k, r)
+    for name, value in (options or {}).items():
         codec.set_option(name, value)
     st = torch.cuda.current_stream()
     base = dev.data_ptr()
@@ -70,13 +90,16 @@ EXTRA_CASES = [c["name"] for c in manifest()["cases"] if c["op"] in EXTRA_OPS]
 M16_PRODUCTION = ("apply_m16_v1", "apply_m16_rt16", "apply_m16_rt32")  # R <= 32: the compiled tiles
 
 
-@pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("name", BATCH_CASES)
-def test_golden_batch_api(name, variant):
+def test_golden_batch_api(name):
+    golden_batch_case(name, "auto")
+
+
+def golden_batch_case(name, variant):
     c = case(name)
     m16 = c["k"] + c["r"] > 255 and c["op"] != "gmatrix"
-    if variant not in ("mask", "cs_idx") and m16:
-        pytest.skip("m = 16 code: one kernel family, covered by the 'mask' and 'cs_idx' parametrisations")
+    if variant not in ("auto", "cs_idx") and m16:
+        pytest.skip("m = 16 code: the GF(256) kernel variants do not apply ('auto' and 'cs_idx' cover it)")
     if variant == "cs_idx" and not m16:
         pytest.skip("GF(256) code: no syndrome route")
     cs = "cs16" if variant == "cs_idx" else CS_DEFAULT
@@ -153,13 +176,16 @@ def test_golden_drop_in_seq_create(name):
     check_golden(c, b"".join(outs))
 
 
-@pytest.mark.parametrize("variant", list(VARIANTS))
-def test_config2_all_stripes_vs_oracle(variant):
+def test_config2_all_stripes_vs_oracle():
+    config2_case("auto")
+
+
+def config2_case(variant):
     """BASELINE config 2: k=10, r=4, 4 KiB symbols, 1024 stripes -- every stripe bit-exact vs the oracle."""
     k, r, S, n = 10, 4, 4096, 1024
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xC2)
-    codec = rs_amd.Codec(k, r, **VARIANTS[variant])
+    codec = codec_for(variant, k, r)
     codec.encode(dev)
     torch.cuda.synchronize()
     got = dev.cpu().numpy()
@@ -176,14 +202,17 @@ def test_config2_all_stripes_vs_oracle(variant):
     assert np.array_equal(dev.cpu().numpy(), got)
 
 
-@pytest.mark.parametrize("variant", list(VARIANTS))
-def test_config3_shape_roundtrip(variant):
+def test_config3_shape_roundtrip():
+    config3_case("auto")
+
+
+def config3_case(variant):
     """k=128, r=32, 64 KiB symbols on 48 stripes: device generator == host generator, repair of sampled
     stripes == oracle, fingerprint of info unchanged after erase + restore, random patterns too."""
     k, r, S, n = 128, 32, 65536, 48
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0x5EED)
-    codec = rs_amd.Codec(k, r, **VARIANTS[variant])
+    codec = codec_for(variant, k, r)
     codec.encode(dev)
     fp0 = torch.zeros(n, dtype=torch.int64, device="cuda")
     rs_amd.fingerprint(dev, 0, k + r, fp0)
@@ -212,7 +241,64 @@ def test_config3_shape_roundtrip(variant):
         assert torch.equal(fp, fp0), f"pattern t={int(er.sum())}"
 
 
+def test_inflight_scalar_load_fix_on_the_kernels_run(tmp_path, monkeypatch):
+    """GPUTEST_r04's illegal address: sload32 let the compiler put the base of its
+    second s_load_dwordx16 inside the first one's destination. The kernels that inline it, at large grids:
+    rs_v1jit at the faulting C2 launch (1024 stripes x 4 chunks) and at 128 x 64 (its default shape), and
+    the per-stripe solve k_apply_m8_v1<0> over 2048 stripes -- bit-exact -- and the code objects the box
+    compiled for them (fresh JIT cache) and the loaded release library pass scripts/isa_hazards.py."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import isa_hazards
+    monkeypatch.setenv("RS_AMD_JIT_CACHE", str(tmp_path))
+    for k, r, S, n in ((10, 4, 4096, 1024), (128, 64, 4096, 64)):
+        dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+        rs_amd.fill_info(dev, k, seed=0x51)
+        codec = rs_amd.Codec(k, r, jit=1, xj=0)
+        codec.encode(dev)
+        torch.cuda.synchronize()
+        assert codec.last_kernel.startswith("rs_v1jit"), codec.last_kernel
+        got = dev.cpu().numpy()
+        for s in (0, n - 1):
+            want = got[s].copy()
+            want[k:] = 0
+            assert oracle_encode(k, r, want) == 0
+            assert np.array_equal(got[s], want), (k, r, s)
+        er = rs_amd.bench_pattern(k, r)
+        dev[:, torch.from_numpy(er)] = 0
+        codec.decode(dev, er)
+        torch.cuda.synchronize()
+        assert codec.last_kernel.startswith("rs_v1jit"), codec.last_kernel
+        assert np.array_equal(dev.cpu().numpy(), got), (k, r)
+    # the per-stripe solve (k_apply_m8_v1<0>, re-encode route) over 2048 all-distinct stripes
+    k, r, S, n = 128, 32, 2048, 2048
+    dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0x52)
+    codec = rs_amd.Codec(k, r, batch_plans=1)
+    codec.encode(dev)
+    torch.cuda.synchronize()
+    full = dev.clone()
+    rng = np.random.default_rng(52)
+    pats = np.zeros((n, k + r), bool)
+    for s in range(n):
+        pats[s, rng.choice(k, r, replace=False)] = True
+    dev[torch.from_numpy(pats).cuda()] = 0
+    assert codec.decode_batch(dev, pats) == 0
+    torch.cuda.synchronize()
+    assert "apply_m8_v1_ps" in codec.last_kernel, codec.last_kernel
+    assert torch.equal(dev, full)
+    objs = [os.path.join(tmp_path, f) for f in os.listdir(tmp_path) if f.startswith("v1_") and f.endswith(".co")]
+    assert len(objs) >= 2, os.listdir(tmp_path)
+    for path in objs + [rs_amd.LIB_PATH]:
+        found = isa_hazards.hazards(isa_hazards.disassemble(path))
+        assert not found, (path, found[:3])
+
+
 def test_decode_matches_oracle_on_noncodewords():
+    noncodeword_case(["auto"])
+
+
+def noncodeword_case(variants):
     """Arbitrary (non-codeword) survivors: the GPU decoder applies exactly the reference's linear map."""
     k, r, S = 128, 32, 8192
     rng = np.random.default_rng(11)
@@ -221,9 +307,9 @@ def test_decode_matches_oracle_on_noncodewords():
     host = rng.integers(0, 256, (2, k + r, S), dtype=np.uint8)
     host[:, er] = 0
     dev = torch.from_numpy(host).cuda()
-    for variant in VARIANTS:
+    for variant in variants:
         d = dev.clone()
-        rs_amd.Codec(k, r, **VARIANTS[variant]).decode(d, er)
+        codec_for(variant, k, r).decode(d, er)
         torch.cuda.synchronize()
         got = d.cpu().numpy()
         for s in range(2):
@@ -584,14 +670,20 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, ps, overlap):
         assert np.array_equal(dev.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("route,ovl,kern,cpb", [(0, 0, 0, 1), (1, 0, 0, 1), (1, 1, 0, 1), (1, 0, 1, 1), (0, 0, 1, 1),
-                                                (1, 0, 2, 1), (1, 1, 2, 1), (0, 0, 2, 1), (2, 0, 0, 1), (2, 1, 0, 1),
-                                                (2, 0, 2, 1), (2, 1, 2, 1), (2, 0, 3, 1), (1, 0, 3, 1), (0, 0, 3, 1),
-                                                (2, 0, 0, 3), (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2),
-                                                (2, 0, 4, 1), (2, 0, 5, 1)])
-@pytest.mark.parametrize("k,r,S,n", [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
-                                     (128, 32, 32768, 1030), (20, 9, 4096 + 520, 33)])
+SYN_ROUTE_SHAPES = [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40), (128, 32, 32768, 1030),
+                    (20, 9, 4096 + 520, 33)]
+
+
+# release-library settings: the three routes, the LDS-ring solve with two or one nibble tables per input
+# (the A/B kernels, overlapped chunks and multi-chunk workgroups: tests/test_gpu_variants.py, diagnostic library)
+@pytest.mark.parametrize("route,ovl,kern,cpb", [(2, 0, 0, 1), (1, 0, 0, 1), (0, 0, 0, 1), (2, 0, 3, 1), (1, 0, 3, 1),
+                                                (0, 0, 3, 1)])
+@pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
+    syndrome_route_case(rs_amd, k, r, S, n, route, ovl, kern, cpb)
+
+
+def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
     the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
     first; route 2: the re-encode differences [G | I] of every slot, then a t_info x t_info Cauchy-inverse
@@ -608,7 +700,7 @@ def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     rng = np.random.default_rng(k + 3 * n + route)
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0xD5)
-    codec = rs_amd.Codec(k, r, batch_plans=1)
+    codec = lib.Codec(k, r, batch_plans=1)
     codec.set_option("syn_route", route)
     codec.set_option("m8_syn_overlap", ovl)
     codec.set_option("m8_ps_kernel", kern)  # 1: the ring-free per-stripe solve kernel (k_apply_m8_ps_w)
@@ -777,8 +869,7 @@ def test_cs16_threaded_matches_indexed(k, r, S, n):
         assert np.array_equal(outs[1][0][0, k:], want[k:])
 
 
-@pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 37), (300, 64, 3072, 16)])
-def test_cs16_overlapped_chunks_match_serial(k, r, S, n):
+def cs16_overlapped_case(k, r, S, n):
     """m16_cs_overlap = 1 (off by default): the one-pattern syndrome route in four chunks with each chunk's syndromes
     on the codec's syndrome stream beside the previous chunk's second stage (two syndrome buffers) gives
     the same repair symbols and restores as the serial route (0, default), for the bench pattern (k_bs16 second
@@ -787,7 +878,7 @@ def test_cs16_overlapped_chunks_match_serial(k, r, S, n):
     for ovl in (1, 0):
         dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
         rs_amd.fill_info(dev, k, seed=0x0C5)
-        codec = rs_amd.Codec(k, r)
+        codec = (rs_amd.diag_module() if ovl else rs_amd).Codec(k, r)  # overlap: a diagnostic-build option
         codec.set_option("m16_cs_overlap", ovl)
         codec.set_option("m16_route_min_bytes", 0)
         res = []
@@ -903,8 +994,12 @@ def test_xor_kernel_shapes_vs_oracle(k, r):
 
 @pytest.mark.parametrize("k,r,S", [(250, 33, 1024), (300, 64, 2048 + 40), (200, 65, 1024 + 1000), (1000, 100, 2048),
                                    (400, 129, 3072 + 4), (2000, 100, 1024)])
-@pytest.mark.parametrize("route,col", [(0, 1024), (1, 1024), (1, 256)])
+@pytest.mark.parametrize("route,col", [(0, 256), (1, 256)])
 def test_m16_kernel_shapes_vs_oracle(k, r, S, route, col):
+    m16_shapes_case(rs_amd, k, r, S, route, col)
+
+
+def m16_shapes_case(lib, k, r, S, route, col):
     """GF(2^16) codes around the 64-row tiles of k_apply_m16_v1 (one partial tile, exactly one tile, a
     1-row second tile, three tiles) with tail columns, encode and decode bit-exact vs the oracle. Two
     stripes make small grids, so every case also runs split-K (k=2000: 31 input slices). Route 0: the
@@ -916,7 +1011,7 @@ def test_m16_kernel_shapes_vs_oracle(k, r, S, route, col):
     host = np.zeros((n, k + r, S), np.uint8)
     host[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
     dev = torch.from_numpy(host).cuda()
-    codec = rs_amd.Codec(k, r)
+    codec = lib.Codec(k, r)
     codec.set_option("m16_route", route)
     codec.set_option("m16_route_min_bytes", 0)  # decode patterns on the route from their first launch
     codec.set_option("m16_cs_col", col)
@@ -1295,10 +1390,16 @@ def test_release_build_ignores_diagnostic_knobs():
     set, a fresh process still encodes and decodes bit-exactly through the same XOR kernel (same content
     hash in its name) as without them."""
     codec = rs_amd.Codec(128, 32)
-    for name, value in ([("m8_mode", v) for v in (10, 11, 12, 13, 15, 16, 17, 19, 21)] + [("m16_mode", 1), ("stamp_buffer", 1)]
-                        + [("m8_ps_kernel", 6), ("m8_ps_kernel", 7)]):
+    # ablations / stamps, and (round 5) the option-only A/B families, overlap variants and block layouts
+    for name, value in ([("m8_mode", v) for v in (0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 19, 21)]
+                        + [("m16_mode", 1), ("stamp_buffer", 1), ("m16_cs_col", 1024), ("m16_cs_overlap", 1),
+                           ("m8_syn_overlap", 1), ("m8_ps_cpb", 2)]
+                        + [("m8_ps_kernel", v) for v in (1, 2, 4, 5, 6, 7)]):
         with pytest.raises(rs_amd.RSError):
             codec.set_option(name, value)
+    for name, value in [("m8_mode", 18), ("m8_mode", 20), ("m8_ps_kernel", 0), ("m8_ps_kernel", 3), ("m16_cs_col", 256),
+                        ("m16_cs_overlap", 0), ("m8_syn_overlap", 0), ("m8_ps_cpb", 1), ("xj", 0), ("xj", 1)]:
+        codec.set_option(name, value)  # the production settings stay accepted
     import os
     import subprocess
     import sys

@@ -462,3 +462,18 @@ def test_reencode_solve_is_the_inverse_cauchy(k, r, t_info, t_rep):
             W[i, j] = exp[(logsum(X[q]) + 2 * N - lr - int(log[int(X[p] ^ X[q])])) % N]
     prod = gf_apply(W, G[Rp - k][:, E])
     assert np.array_equal(prod, np.eye(t_info, dtype=np.uint16))
+
+
+@pytest.mark.parametrize("value,want", [(None, 0), ("0", 0), ("1", 1)])
+def test_checked_launch_mode_switch(value, want):
+    """RS_AMD_CHECK (rsg_check_enabled): read once per process, so each setting runs in a fresh one."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("RS_AMD_CHECK", None)
+    if value is not None:
+        env["RS_AMD_CHECK"] = value
+    code = ("import sys; sys.path.insert(0, %r); import rs_amd; print(rs_amd._lib.rsg_check_enabled())"
+            % os.path.join(REPO, "reed-solomon_amd"))
+    out = subprocess.check_output([sys.executable, "-c", code], env=env, text=True)
+    assert out.strip().splitlines()[-1] == str(want)

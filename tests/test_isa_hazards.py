@@ -81,3 +81,38 @@ def test_jit_kernels_have_no_inflight_reads(k, r, pattern, tmp_path, monkeypatch
         assert all(os.path.basename(o).startswith("v1_") for o in objs), objs  # the nibble-table rs_v1jit
     for o in objs:
         _check(o)
+
+
+def _kernel_names(path):
+    import re
+    text = isa_hazards.disassemble(path)
+    return {m.group(1) for m in re.finditer(r"^[0-9a-f]+ <([^>]+)>:", text, re.M) if not m.group(1).startswith(("L_", ".L"))}
+
+
+# kernel families reachable only through A/B options, ablations or stamps: diagnostic build only
+DIAG_ONLY = ("k_apply_m8ILi", "k_apply_m8_lds", "k_apply_m8_ps_w", "k_apply_m8_idxILi0ELi8E", "k_apply_m8_idxILi4E",
+             "k_apply_m8_v1ILi1E", "k_apply_m8_v1ILi3E", "k_apply_m8_v1ILi4E", "k_apply_m8_v1ILi5E", "k_apply_m8_v1ILi6E",
+             "k_apply_m16_v1ILi1E")
+# every production kernel (the release library carries exactly these)
+PRODUCTION = ("k_apply_m8_v1ILi0E", "k_apply_m8_v1ILi2E", "k_apply_m8_idxILi0ELi4E", "k_apply_m8_ps_tail", "k_xor_slices",
+              "k_apply_m16ILi16E", "k_apply_m16ILi32E", "k_apply_m16ILi64E", "k_apply_m16_v1ILi0E", "k_cs16E", "k_cs16tE",
+              "k_bs16E", "k_cs16_goff", "k_plan_m8", "k_plan_syn_m8", "k_plan_reenc_m8", "k_plan16_sums", "k_plan16_fill",
+              "k_plan16_ps", "k_plan16_ps_rec", "k_plan16_reenc", "k_plan16_reenc_logs", "k_plan16_reenc_rec",
+              "k_symbol_op", "k_gen_info", "k_fingerprint", "k_gather_rows", "k_put_rows", "k_xor_rows",
+              "k_gather_ptrs", "k_scatter_ptrs")
+
+
+def test_release_build_has_no_ablation_kernels():
+    """The release library's kernel set is the production set: no option-only A/B family, ablation or
+    stamped kernel (those are in librs_amd_diag.so, whose kernel set is a superset)."""
+    rel = _kernel_names(os.path.join(PKG, "librs_amd.so"))
+    bad = sorted(n for n in rel if any(d in n for d in DIAG_ONLY))
+    assert not bad, bad
+    unknown = sorted(n for n in rel if not any(p in n for p in PRODUCTION))
+    assert not unknown, unknown
+    missing = [p for p in PRODUCTION if not any(p in n for n in rel)]
+    assert not missing, missing
+    diag = os.path.join(PKG, "librs_amd_diag.so")
+    if os.path.exists(diag):
+        d = _kernel_names(diag)
+        assert rel <= d and any(any(x in n for x in DIAG_ONLY) for n in d)
