@@ -92,8 +92,11 @@ int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
  * the encode route's 1 GiB syndrome buffer); the GF(256) fixed pass one buffer of up to 1 GiB (two with
  * m8_syn_overlap); the route / re-encode decodes up to 1 GiB each; the host pipelines two 256 MiB batch
  * buffers.
- * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it (plans stay cached;
- * later calls grow it again). */
+ * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it: every buffer above,
+ * the stripe-id lists, the route's slot-offset tables, the GF(2^16) many-pattern batch plan with its records
+ * (up to 256 MiB) and pinned staging, and the host-pipeline buffers. What survives: the cached encode /
+ * decode plans, the per-codec streams and events, and two small tables (slot elements, 2 (k + r) bytes;
+ * the per-stripe route's input list, 4 (r + 16) bytes). Later calls grow the scratch again. */
 int rsg_codec_trim(rsg_codec_t* c);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);

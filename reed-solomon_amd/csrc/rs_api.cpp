@@ -245,6 +245,27 @@ extern "C" int rsg_codec_trim(rsg_codec_t* c) {
     drop(c->d_pin, c->pin_cap);
     drop(c->d_pout, c->pout_cap);
     drop(c->d_pidx, c->pidx_cap);
+    size_t ids_bytes = c->ids_cap * 4;  // ids_cap counts entries
+    drop(reinterpret_cast<void*&>(c->d_ids), ids_bytes);
+    c->ids_cap = 0;
+    for (int i = 0; i < 2; ++i) drop(c->d_goff[i], c->goff_cap[i]);
+    // the GF(2^16) many-pattern batch plan: its staging slots' last uploads first, then the plan (its
+    // destructor guards its own blob), the records it pointed into, and the pinned staging
+    for (int i = 0; i < 2; ++i) {
+        if (c->bp16_rec_pending[i]) HIP_TRY(hipEventSynchronize(c->bp16_ev[i]));
+        c->bp16_rec_pending[i] = false;
+    }
+    if (c->bp16) {
+        c->bp16->d_idx = nullptr;  // a view into d_bp16_rec
+        c->bp16.reset();
+    }
+    size_t none = 0;
+    drop(c->d_bp16, none);
+    drop(c->d_bp16_rec, none);
+    for (int i = 0; i < 2; ++i) {
+        if (c->h_bp16[i]) (void)hipHostFree(c->h_bp16[i]);
+        c->h_bp16[i] = nullptr;
+    }
     for (int i = 0; i < 2; ++i) {
         if (c->hbuf[i]) (void)hipFree(c->hbuf[i]);
         c->hbuf[i] = nullptr;
@@ -280,7 +301,7 @@ static void slot_range(const std::vector<int32_t>& v, size_t n, int64_t& lo, int
 }
 
 int check_plan_slots(const rsg_codec_t* c, const DevPlan& p) {
-    const int64_t n = int64_t(c->k) + c->r;
+    const int64_t n = p.slot_bound ? int64_t(p.slot_bound) : int64_t(c->k) + c->r;
     int64_t ilo, ihi, olo, ohi;
     slot_range(p.in_slots, size_t(p.K), ilo, ihi);
     slot_range(p.out_slots, size_t(p.R), olo, ohi);
@@ -432,7 +453,7 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
-    a.nslots = int32_t(c->k) + c->r;  // every list of a dispatcher plan names codec (or syndrome) slots
+    a.nslots = p.slot_bound ? p.slot_bound : int32_t(c->k) + c->r;  // codec (or syndrome / staging) slots
     const bool m8_generic = p.m == 8 && p.d_idx && (a.mode == 18 || a.mode == 20 || a.mode == 21) && !(xj_ok && p.xj) && !(jit_ok && p.jit);
     if ((p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) || m8_generic) {  // split-K scratch for small grids
         int64_t need = 0;

@@ -781,6 +781,30 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
 
 }  // namespace rsamd
 
+namespace rsamd {
+
+// A per-stripe route that fails after its first launch returns with work still queued on the codec's side
+// and syndrome streams, and without marking the scratch busy: join those streams into the caller's stream
+// and mark the scratch as used by it, so the next call (on any stream) waits for the orphaned kernels
+// before it overwrites lists, records or syndromes they may still read. Best effort: the call's own error
+// is what gets reported.
+static int fenced(rsg_codec_t* c, hipStream_t st, int rc) {
+    if (!rc) return 0;
+    for (hipStream_t s : {c->ps_side, c->ps_synst}) {
+        if (!s) continue;
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(e, s) == hipSuccess) (void)hipStreamWaitEvent(st, e, 0);
+            (void)hipEventDestroy(e);
+        }
+    }
+    (void)scratch_release(c, st);
+    (void)hipGetLastError();
+    return rc;
+}
+
+}  // namespace rsamd
+
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
@@ -827,12 +851,14 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (dev_m8 && (c->batch_plans == 1 || groups.size() > kHostPlanGroups))
-        return decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
-                                         int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st);
+        return fenced(c, st,
+                      decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
+                                                int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st));
     // GF(2^16): more than one pattern -> per-stripe plans on the syndrome route (one shared syndrome pass)
     if (dev_m16 && (c->batch_plans == 1 || groups.size() > 1))
-        return decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride), int64_t(symbol_stride),
-                                   n_stripes, symbol_size, is_erased, tr.data(), st);
+        return fenced(c, st,
+                      decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
+                                          int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st));
     std::vector<int32_t> ids;
     std::vector<size_t> first;
     for (auto& g : groups) {

@@ -125,6 +125,9 @@ struct DevPlan {
     std::vector<uint8_t> erased;  // the pattern (empty: encode), to build `dense`
     int64_t uses = 0;                // launches of this plan (JIT policy)
     bool slots_checked = false;      // check mode: slot lists bounds-checked on the host
+    // slots of the layouts the lists index: 0 = the codec's k + r (every codec plan); the context-free
+    // transforms (rs_refops.cpp) index their own staging rows
+    int32_t slot_bound = 0;
     void* blob = nullptr;            // set: d_in / d_out / d_coef / d_idx are views into this one allocation
     size_t blob_cap = 0;             // its size class (plan_pool)
     // stream-ordered build: the upload (and device fill) ran on `built_on`; `ready` marks its end, so a

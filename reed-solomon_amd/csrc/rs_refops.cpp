@@ -303,6 +303,7 @@ int transform_apply(std::vector<uint16_t> M, const symbol_seq_t* f, symbol_seq_t
     std::unique_ptr<DevPlan> plan;
     if (int rc = build_plan(o.device, 16, std::move(M), int(K), int(R), std::move(in), std::move(out), plan, o.stream))
         return rc;
+    plan->slot_bound = int32_t(std::max(K, R));  // staging rows, not codec slots
     uint8_t* dres = o.d + K * P;
     if (int rc = run_plan(o.codec.get(), *plan, o.d, 0, int64_t(P), dres, 0, int64_t(P), 1, Se, o.stream)) return rc;
     HIP_TRY(hipMemcpyAsync(o.h + K * P, dres, R * P, hipMemcpyDeviceToHost, o.stream));

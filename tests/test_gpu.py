@@ -1531,6 +1531,8 @@ def test_new_pattern_does_not_stall_other_streams():
     """A decode with a new erasure pattern builds its plan on the caller's stream (pinned upload, no
     null-stream copy): while another (blocking) stream is busy with a long encode, the decode call
     returns with that stream still running, and its result is bit-exact."""
+    if rs_amd._lib.rsg_check_enabled():
+        pytest.skip("RS_AMD_CHECK: every launch waits for the device by design")
     hip = ctypes.CDLL("libamdhip64.so")
     k, r, S = 128, 32, 65536
     busy = torch.empty((1024, k + r, S), dtype=torch.uint8, device="cuda")
