@@ -375,6 +375,12 @@ __device__ __forceinline__ void m8_v1_step(uint32_t y, const uint32_t* cp, u32x1
         asm volatile(
 #include "gen/m8_idx_asm_v1.inc"
             RS_M8_V1_OPERANDS);
+#ifdef RS_AMD_DIAG
+    } else if constexpr (ABL == 7) {  // timing ablation: one SMEM round trip per step (wrong results)
+        asm volatile(
+#include "gen/m8_idx_asm_v1_nohi.inc"
+            RS_M8_V1_OPERANDS);
+#endif
     } else {
         asm volatile(
 #include "gen/m8_idx_asm_v1_plain.inc"
@@ -2337,6 +2343,8 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
             hipLaunchKernelGGL((k_apply_m8_v1<1>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 7)  // the production kernel with phase stamps into f.stamps
             hipLaunchKernelGGL((k_apply_m8_v1<5>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 8)  // timing ablation: one record round trip per input step (wrong results)
+            hipLaunchKernelGGL((k_apply_m8_v1<7>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (f.cpb > 1)
             hipLaunchKernelGGL((k_apply_m8_v1<6>), dim3(unsigned(blocks), unsigned(tiles)), dim3(256), 0, st, f);
 #endif

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-5 A/Bs of the GF(256) per-stripe decode (route 2, 4096 C3 stripes, scripts/bench_patterns.py).
+# usage: gpu_r5_ps8.sh MODE
+#   rec    solve kernel 0 vs the diagnostic one-record-round-trip ablation 8 (wrong results): how much of the
+#          step is the high-half record load's exposed latency
+#   base   the production route alone (t32info and rand), two reps
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+MODE=${1:?mode}
+D=gpurun_out/${PS8:-r5_ps8_$MODE}
+mkdir -p $D
+DIAG=$PWD/reed-solomon_amd/librs_amd_diag.so
+run() {  # run LABEL ARGS... with the environment already exported by the caller
+  local label=$1; shift
+  timeout -k 10 300 python3 -u scripts/bench_patterns.py "$@" > $D/$label.log 2>&1 || { tail -5 $D/$label.log; exit 1; }
+  echo "$label $(grep -o '"ms": [0-9.]*' $D/$label.log | head -1) $(grep -o '"restored": [a-z]*' $D/$label.log | head -1)"
+}
+case $MODE in
+rec)
+  for rep in 1 2; do for kern in 0 8; do
+    RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_$rep 4096 t32info device_plans_syndrome
+  done; done ;;
+base)
+  for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done ;;
+*) echo "unknown mode $MODE"; exit 2 ;;
+esac
