@@ -191,6 +191,13 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->m8_ps_cpb = int(value);
         return 0;
     }
+#ifdef RS_AMD_DIAG
+    if (!std::strcmp(name, "m8_ps_ablate")) {  // timing ablations of the per-stripe solve (wrong results)
+        if (value < 0 || value > 7) return RS_ERR_INVALID;
+        c->m8_ps_ablate = int(value);
+        return 0;
+    }
+#endif
     if (!std::strcmp(name, "m8_syn_overlap")) {  // GF(256) per-stripe syndrome route: overlapped chunks
         if (value < 0 || value > 1) return RS_ERR_INVALID;
 #ifndef RS_AMD_DIAG
@@ -319,6 +326,18 @@ int check_launch(const rsg_codec_t* c, const DevPlan* p, const char* where, uint
     const hipError_t sync = hipDeviceSynchronize();
     const hipError_t last = hipGetLastError();
     const hipError_t e = sync != hipSuccess ? sync : last;
+    if (e == hipSuccess && c && c->d_slot_err) {  // diagnostic builds: a device-side slot check fired
+        int32_t rec[4] = {0, 0, 0, 0};
+        if (hipMemcpy(rec, c->d_slot_err, sizeof rec, hipMemcpyDeviceToHost) == hipSuccess && rec[0]) {
+            std::fprintf(stderr,
+                         "librs_amd: RS_AMD_CHECK: %s slot list entry %d = %d outside [0, %d) in block %d after %s: "
+                         "kernel %s, plan K=%d R=%d\n",
+                         rec[0] == 1 ? "input" : "output", rec[1], rec[2], p && p->slot_bound ? p->slot_bound : c->k + c->r,
+                         rec[3], where, c->last_kernel.c_str(), p ? p->K : 0, p ? p->R : 0);
+            (void)hipMemset(c->d_slot_err, 0, sizeof rec);
+            return RS_ERR_DEVICE;
+        }
+    }
     if (e == hipSuccess) return 0;
     int64_t ilo = 0, ihi = -1, olo = 0, ohi = -1;
     if (p) {
@@ -453,7 +472,16 @@ int run_plan_body(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_st
     a.mode = p.m == 8 ? c->m8_mode : c->m16_mode;
     a.stamps = c->stamps;
     a.ids = d_ids;
-    a.nslots = p.slot_bound ? p.slot_bound : int32_t(c->k) + c->r;  // codec (or syndrome / staging) slots
+#ifdef RS_AMD_DIAG
+    if (check_mode()) {  // device-side slot checks (m8_v1_run) with a violation record read by check_launch
+        if (!c->d_slot_err) {
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_slot_err), 16));
+            HIP_TRY(hipMemset(c->d_slot_err, 0, 16));
+        }
+        a.nslots = p.slot_bound ? p.slot_bound : int32_t(c->k) + c->r;  // codec (or syndrome / staging) slots
+        a.slot_err = c->d_slot_err;
+    }
+#endif
     const bool m8_generic = p.m == 8 && p.d_idx && (a.mode == 18 || a.mode == 20 || a.mode == 21) && !(xj_ok && p.xj) && !(jit_ok && p.jit);
     if ((p.m == 16 && p.rt == 64 && p.d_idx && a.mode < 2) || m8_generic) {  // split-K scratch for small grids
         int64_t need = 0;

@@ -238,6 +238,10 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_out = out_stride;
             v.ps_idx = idx_stride;
             v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
+#ifdef RS_AMD_DIAG
+            if (c->m8_ps_ablate & 4) v.xor_dst = 0;  // timing ablation: no old-value loads (wrong results)
+            v.ablate = c->m8_ps_ablate & 3;
+#endif
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
             HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
             RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);

@@ -318,6 +318,9 @@ struct rsg_codec {
     // option m8_ps_cpb: 1 KiB column chunks per workgroup of the per-stripe ring kernels (table setup once per
     // block, the next chunk's ring prologue in flight during this chunk's output stage)
     int m8_ps_cpb = 1;
+    // diagnostic builds: option m8_ps_ablate, timing ablations of the per-stripe solve (wrong results): 1 no
+    // table copy, 2 no output conversion, 4 no old-value loads (xor_dst off)
+    int m8_ps_ablate = 0;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;
     void* d_syn = nullptr;  // [chunk][r][S] syndromes
@@ -370,10 +373,11 @@ struct rsg_codec {
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
                         d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_reenc, d_goff[0], d_goff[1], d_ps_rec,
-                        d_ps_small, static_cast<void*>(d_ps_in)})
+                        d_ps_small, static_cast<void*>(d_ps_in), static_cast<void*>(d_slot_err)})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
+    int32_t* d_slot_err = nullptr;  // checked launches of diagnostic builds: [4] slot-violation record
 };
 
 namespace rsamd {

@@ -104,15 +104,21 @@ __device__ __forceinline__ int32_t sload(const int32_t* p) {
     return v;
 }
 
-// Diagnostic builds: a slot index outside [0, nslots) is reported (kernel, block, list position, value) and
-// the access it would address is skipped or redirected to slot 0; release and hiprtc builds compile nothing.
+// Diagnostic builds with checked launches: a slot index outside [0, nslots) is recorded in a.slot_err (vector
+// stores of the wave's first lane: what, list position, value, block) and the access it would address is
+// redirected to slot 0 (loads) or skipped (stores); release and hiprtc builds compile nothing.
 #if defined(RS_AMD_DIAG) && !defined(RS_JIT_SOURCE)
-#define RS_SLOT_OK(a, slot, what, pos)                                                                          \
-    ((a).nslots <= 0 || ((slot) >= 0 && (slot) < (a).nslots) ||                                                 \
-     ((threadIdx.x & 63) == 0 &&                                                                                 \
-      (printf("librs_amd diag: %s[%d] = %d outside [0, %d) in block (%d, %d)\n", (what), int(pos), int(slot),    \
-              (a).nslots, int(blockIdx.x), int(blockIdx.y)),                                                     \
-       false)))
+__device__ __noinline__ bool rs_slot_fail(int32_t* err, int what, int pos, int32_t slot) {
+    if (err && (threadIdx.x & 63) == 0) {
+        err[0] = what;
+        err[1] = pos;
+        err[2] = slot;
+        err[3] = int32_t(blockIdx.x);
+    }
+    return false;
+}
+#define RS_SLOT_OK(a, slot, what, pos) \
+    ((a).nslots <= 0 || (uint32_t(slot) < uint32_t((a).nslots)) || rs_slot_fail((a).slot_err, (what), (pos), (slot)))
 #else
 #define RS_SLOT_OK(a, slot, what, pos) true
 #endif
@@ -173,8 +179,16 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
     auto slot = [&](int p) { return p < 16 ? o0[p & 15] : o1[p & 15]; };
     auto at = [&](int p) {
         const int32_t s = slot(p);
-        return reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, s, "out_idx", p) ? s : 0) * a.dst_sym);
+        return reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, s, 2, p) ? s : 0) * a.dst_sym);
     };
+#if defined(RS_AMD_DIAG) && !defined(RS_JIT_SOURCE)
+    if (a.ablate & 2) {  // timing ablation: raw accumulators, no L^-1 conversion (wrong results)
+#pragma unroll
+        for (int p = 0; p < 32; ++p)
+            if (p < rows) *at(p) = p < 16 ? a0[p & 15] : a1[p & 15];
+        return;
+    }
+#endif
     if (a.xor_dst) {  // g ^ (W S), in rounds of LB loads (NB = 2 holds twice the accumulators)
         constexpr int LB = LBX ? LBX : NB == 2 ? 16 : 32;
 #pragma unroll
@@ -258,7 +272,7 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     const uint8_t* gsb = a.src + stripe * a.src_stripe + cbeg * 1024;
     auto issue = [&](int i) {
         int32_t s = sload(in_idx + i);
-        if (!RS_SLOT_OK(a, s, "in_idx", i)) s = 0;  // diagnostic builds: report, read slot 0 instead
+        if (!RS_SLOT_OK(a, s, 1, i)) s = 0;  // diagnostic builds: record, read slot 0 instead
         dma16(gsb + int64_t(s) * a.src_sym + 16 * lane, ring_lds + uint32_t(i % RING_SLOTS) * 1024u);
     };
     const int nb = (K + 3) / 4;
@@ -304,7 +318,10 @@ __device__ __forceinline__ void m8_v1_run(const V1Args& a, uint32_t* lds, Step&&
     // latencies overlap (the ring area and the tables are disjoint)
     for (int b = 0; b < RING_B; ++b)
         if (4 * b + wave < K) issue(4 * b + wave);
-    for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
+#if defined(RS_AMD_DIAG) && !defined(RS_JIT_SOURCE)
+    if (!(a.ablate & 1))  // timing ablation: the tables are not copied (wrong results)
+#endif
+        for (int i = threadIdx.x; i < 2048; i += 256) lds[i] = a.ltab[i];
     if constexpr (NB == 2) {
         __syncthreads();
         for (int i = threadIdx.x; i < 1024; i += 256) lds[V1H_G4 + i] = lds[1024 + (i & ~255) + gmul_g4(i & 255)];

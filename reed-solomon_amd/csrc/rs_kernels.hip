@@ -1195,6 +1195,7 @@ V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
     v.nchunks = nchunks_1k;
     v.ids = a.ids;
     v.nslots = a.nslots;
+    v.slot_err = a.slot_err;
     return v;
 }
 

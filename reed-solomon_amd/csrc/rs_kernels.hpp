@@ -32,6 +32,7 @@ struct ApplyArgs {
     uint32_t* scratch;       // m = 16 split-K partials (codec-owned), scratch_bytes long; may be null
     int64_t scratch_bytes;
     int32_t nslots;          // diagnostic builds: slot indices lie in [0, nslots) (V1Args::nslots); 0 = unchecked
+    int32_t* slot_err;       // its violation record (V1Args::slot_err)
 };
 // input slices of the split-K m = 16 launch over n_stripes (1 = no split) and the scratch it needs
 int m16_kslices(const ApplyArgs& a, int64_t n_stripes, int64_t* scratch_bytes);

@@ -46,10 +46,15 @@ struct V1Args {
     // m8_v1_run: column chunks per block (<= 1: one; the grid's x then covers n_stripes * ceil(nchunks / cpb)
     // blocks). Not combined with split-K.
     int32_t cpb;
-    // diagnostic builds (RS_AMD_DIAG): slot indices read from in_idx / out_idx must lie in [0, nslots)
-    // (the codec's k + r); a violation is printed by the first lane of the wave and the access is
-    // skipped instead of faulting. 0 = unchecked.
+    // diagnostic builds (RS_AMD_DIAG) under checked launches (RS_AMD_CHECK): slot indices read from in_idx /
+    // out_idx must lie in [0, nslots) (the codec's k + r); a violation is recorded in slot_err ({1 in / 2 out,
+    // list position, value, block}) and the access goes to slot 0 (loads) or is skipped (stores) instead of
+    // faulting; the host reports it after the launch. nslots 0 = unchecked.
     int32_t nslots;
+    int32_t* slot_err;
+    // diagnostic builds only (option m8_ps_ablate; timing ablations with wrong results): bit 1 skips the
+    // coordinate-table copy into LDS, bit 2 stores the accumulators without the L^-1 conversion
+    int32_t ablate;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

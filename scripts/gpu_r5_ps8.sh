@@ -18,8 +18,13 @@ run() {  # run LABEL ARGS... with the environment already exported by the caller
 }
 case $MODE in
 rec)
-  for rep in 1 2; do for kern in 0 8; do
-    RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_$rep 4096 t32info device_plans_syndrome
+  for rep in 1 2; do
+    run rel_$rep 4096 t32info device_plans_syndrome
+    for kern in 0 8; do RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_$rep 4096 t32info device_plans_syndrome; done
+  done ;;
+abl)   # per-stripe solve fixed costs: ablation bits 1 no table copy, 2 no output conversion, 4 no old-value loads
+  for rep in 1 2; do for ab in 0 1 2 4 7; do
+    RS_AMD_LIB=$DIAG RS_PS8_ABLATE=$ab run a${ab}_$rep 4096 t32info device_plans_syndrome
   done; done ;;
 base)
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done ;;
