@@ -369,7 +369,7 @@ def compute_roofline(work_enc, enc_ms, work_dec, dec_ms):
     XOR kernels per 256-byte column, GF(2^16) steps per step) against the chip's VALU issue peak
     (2 cycles per wave64 op per SIMD at 2.4 GHz). The chip holds ~1.4-1.5 GHz under these loads, and
     gpr-indexed VALU (the GF(2^16) table lookups) issue at half rate on gfx950
-    (profiles/r1_issue_bench.log), so frac ~0.6 (XOR kernels) / ~0.5 (GF(2^16)) are practical ceilings."""
+    (profiles/r1/r1_issue_bench.log), so frac ~0.6 (XOR kernels) / ~0.5 (GF(2^16)) are practical ceilings."""
     v = work_enc[0] + work_dec[0]
     sa = work_enc[1] + work_dec[1]
     t = (enc_ms + dec_ms) / 1e3

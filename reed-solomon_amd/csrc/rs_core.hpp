@@ -284,7 +284,7 @@ struct rsg_codec {
                ps_ev_used[2] = {nullptr, nullptr}, ps_ev_syn[2] = {nullptr, nullptr};
     int ps_overlap = 1;  // 1: chunk i + 1's syndrome pass beside chunk i's solve (two syndrome buffers)
     // option m16_cs_overlap: the same for the one-pattern syndrome route (run_cs); off by default: C5 in four
-    // overlapped chunks measured 77.5-78.3 GB/s against 80.6-80.7 serial (profiles/r3_cs_overlap_ab.log)
+    // overlapped chunks measured 77.5-78.3 GB/s against 80.6-80.7 serial (profiles/r3/r3_cs_overlap_ab.log)
     int cs_overlap = 0;
     int64_t ps_chunk = 0;   // option m16_ps_chunk: max stripes per chunk (0 = by ps_rec_mib)
     int64_t ps_rec_mib = 1024;  // records per chunk (MiB); larger chunks keep k_cs16 busier (measured 48-1024)

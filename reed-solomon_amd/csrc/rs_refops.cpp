@@ -254,7 +254,7 @@ int symbol_op(int op, void* a, element_t coef, const void* b, size_t symbol_size
     }
     const uint32_t lc = op == 0 ? 0u : field().log[coef];
     // large operands: DMA in and out (the copy engines beat the kernel's own PCIe reads there: 1 MiB
-    // gf_madd 172 us with DMA vs 199 us zero-copy, profiles/r3_hostops.jsonl)
+    // gf_madd 172 us with DMA vs 199 us zero-copy, profiles/r3/r3_hostops.jsonl)
     const bool dma = P >= kSymbolOpDmaBytes;
     uint8_t* dv = o.hd;
     if (dma) {
