@@ -37,16 +37,20 @@ void rsg_codec_destroy(rsg_codec_t* c);
 /* Subfield degree m of the code (8 => GF(256) kernels, 16 => general kernels). */
 int rsg_codec_subfield(const rsg_codec_t* c);
 
-/* Options (release build; every value gives identical results, they choose kernels and plans):
+/* Options (every value gives identical results, they choose kernels and plans). The release library
+ * accepts only values that select a parity-tested production path; the values marked [diag] are option-only
+ * A/B families, overlap variants and layouts that exist only in the diagnostic build (make diag,
+ * librs_amd_diag.so) -- the release library returns RS_ERR_INVALID for them:
  *   "jit"          matrix-specialised GF(256) kernels (hiprtc, cached on disk): 0 off, 1 every eligible
  *                  matrix, 2 the encode matrix and decode matrices from their dec_jit_uses-th launch
  *                  (default)
  *   "dec_jit_uses" launches of >= 1 MiB before a decode plan is specialised under jit = 2 (default 2)
- *   "xj"           specialised family: 1 bit-plane XOR kernels (default), 0 nibble-table kernels
+ *   "xj"           specialised family: 1 bit-plane XOR kernels (default), 0 nibble-table kernels (rs_v1jit,
+ *                  also the default for matrices the XOR kernel rejects)
  *   "m8_mode"      GF(256) kernel without specialisation: 20 one dword per lane, one nibble table per
  *                  input, two accumulator sets, gpr-index lookups (default); 18 the same with two tables
- *                  and one accumulator set; 2 two dwords per lane; 0 register tables, compiler indexing; 1 masked
- *                  multiples; 3, 4, 14 other register layouts of the gpr-index kernels
+ *                  and one accumulator set; [diag] 2 two dwords per lane, 0 register tables with compiler
+ *                  indexing, 1 masked multiples, 3, 4, 14 other register layouts of the gpr-index kernels
  *   "batch_plans"  rsg_decode_batch: 0 host plans per distinct pattern; 1 device-built plans (GF(256):
  *                  per stripe; GF(2^16): see m16_ps); 2 device plans past 16 distinct patterns for GF(256)
  *                  codes and past one pattern for GF(2^16) codes (default)
@@ -54,12 +58,14 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  [G | I] of every slot on the bit-plane XOR kernel, then a per-stripe t_info x t_info
  *                  solve from the first t_info surviving repair rows (default); 1 syndromes of every slot
  *                  on that kernel, then a t_info x t solve; 0 survivor matrices
- *   "m8_syn_overlap" that route's plans + fixed pass of the next chunk on a codec stream beside this
- *                  chunk's solve (two buffer sets), 0 one stream (default)
- *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 1 one dword per lane
- *                  without the ring, 2 two dwords per lane, 3 the ring kernel with one nibble table
- *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0 (default 1; 2-64 walk a stripe's
- *                  chunks in one workgroup, table setup once, next chunk's ring prologue under the outputs)
+ *   "m8_syn_overlap" 0 one stream (default); [diag] 1 that route's plans + fixed pass of the next chunk on a
+ *                  codec stream beside this chunk's solve (two buffer sets)
+ *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 3 the ring kernel with
+ *                  one nibble table; [diag] 1 one dword per lane without the ring, 2 two dwords per lane,
+ *                  4 / 5 the one-table kernel converting 2 / 4 inputs per LDS round trip
+ *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0: 1 (default); [diag] 2-64 walk a
+ *                  stripe's chunks in one workgroup (table setup once, next chunk's ring prologue under the
+ *                  outputs)
  *   "m16_ps"       GF(2^16) rsg_decode_batch with per-stripe patterns (S a multiple of 1 KiB, r <= 4096):
  *                  1 one syndrome pass over all slots + a device-built t_info x t solve per stripe; 2 the
  *                  encode route over the information slots + the received repair rows, then a t_info x
@@ -68,8 +74,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m16_ps_chunk" / "m16_ps_rec_mib"  stripes / record MiB per chunk of that path (0 / 1024 defaults)
  *   "m16_ps_overlap" 1 (default) the next chunk's syndrome pass runs on a codec stream beside this chunk's
  *                  solve (two syndrome buffers); 0 both on the caller's stream
- *   "m16_cs_overlap" 1 the one-pattern syndrome route runs >= 16 stripes in 4 chunks, each chunk's
- *                  syndromes on that codec stream beside the previous chunk's second stage; 0 serial (default)
+ *   "m16_cs_overlap" 0 serial (default); [diag] 1 the one-pattern syndrome route runs >= 16 stripes in 4
+ *                  chunks, each chunk's syndromes on that codec stream beside the previous chunk's second stage
  *   "m16_mode"     GF(2^16) dense kernels: 0 hand-scheduled gpr-index kernel for > 32 outputs (default),
  *                  2 the compiled kernel
  *   "m16_plans"    GF(2^16) dense matrices: 0 built on the host, 1 on the device, 2 on the device from 64K
@@ -79,11 +85,12 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m16_route_min_bytes"  bytes a dense decode plan with t > 64 moves before it switches to the route
  *                  (default 1 GiB; 0 = at once)
  *   "m16_reenc"    GF(2^16) decodes without repair erasures and t >= 0.9 r by re-encoding: 1 (default), 0
- *   "m16_cs_col"   route kernels' block layout: 256 (default) or 1024 bytes per column unit
+ *   "m16_cs_col"   route kernels' block layout: 256 bytes per column unit (default); [diag] 1024
  *   "m16_cs_thread" route syndromes: 1 k_cs16t, threaded code blocks at full VALU rate (default); 0 k_cs16,
  *                  gpr-indexed subset-table lookups
- * The timing ablations (m8_mode 10-13, 15-17, 19, 21; m8_ps_kernel 6, 7; m16_mode 1; "stamp_buffer") exist
- * only in the diagnostic build (make diag, librs_amd_diag.so); the release library rejects them.
+ * The timing ablations (wrong results: m8_mode 10-13, 15, 16, 19; m8_ps_kernel 6, 8; "m8_ps_ablate"; m16_mode
+ * 1) and the s_memtime stamps (m8_mode 17, 21; m8_ps_kernel 7; "stamp_buffer") exist only in the diagnostic
+ * build too.
  * Returns RS_ERR_INVALID for unknown names or values. */
 int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
 /* Device scratch of a codec only grows with the launches it serves, and is reused by later calls: the
