@@ -102,8 +102,8 @@ int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
  * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it: every buffer above,
  * the stripe-id lists, the route's slot-offset tables, the GF(2^16) many-pattern batch plan with its records
  * (up to 256 MiB) and pinned staging, and the host-pipeline buffers. What survives: the cached encode /
- * decode plans, the per-codec streams and events, and two small tables (slot elements, 2 (k + r) bytes;
- * the per-stripe route's input list, 4 (r + 16) bytes). Later calls grow the scratch again. */
+ * decode plans, the per-codec streams and events, and three small tables (slot elements, 2 (k + r) bytes;
+ * the per-stripe route's input list, 4 (r + 16) bytes; a 256-byte zero buffer). Later calls grow the scratch again. */
 int rsg_codec_trim(rsg_codec_t* c);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);
@@ -217,6 +217,11 @@ int64_t rsg_symbol_pool_cap(int64_t bytes);
  * NULL and are written only when it applies. Host only. */
 int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
                   int32_t* fin, int32_t* fin_off);
+/* Source of the masked (masked = 1) or plain XOR kernel of the GF(256) per-stripe route's fixed pass over all
+ * k + r slots: route 1 the r syndromes, 2 the re-encode differences [G | I]. The masked form reads every
+ * slot whose bit is set in its stripe's mask words as zero. RS_ERR_INVALID when the route does not apply
+ * (m = 16 codes, K * R past the XOR kernel's bound). Host only (emulator tests). */
+int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len);
 const char* rsg_version(void);
 /* 1 when checked launches are on (environment RS_AMD_CHECK set and not "0" at the first call of the
  * process), else 0. In checked mode every launch group is followed by a device wait and an error read: a

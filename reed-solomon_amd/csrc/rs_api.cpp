@@ -193,7 +193,7 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
 #ifdef RS_AMD_DIAG
     if (!std::strcmp(name, "m8_ps_ablate")) {  // timing ablations of the per-stripe solve (wrong results)
-        if (value < 0 || value > 7) return RS_ERR_INVALID;
+        if (value < 0 || value > 3) return RS_ERR_INVALID;
         c->m8_ps_ablate = int(value);
         return 0;
     }
@@ -252,6 +252,7 @@ extern "C" int rsg_codec_trim(rsg_codec_t* c) {
     drop(c->d_pin, c->pin_cap);
     drop(c->d_pout, c->pout_cap);
     drop(c->d_pidx, c->pidx_cap);
+    drop(c->d_mbits, c->mbits_cap);
     size_t ids_bytes = c->ids_cap * 4;  // ids_cap counts entries
     drop(reinterpret_cast<void*&>(c->d_ids), ids_bytes);
     c->ids_cap = 0;

@@ -47,6 +47,28 @@ int stage_lists(rsg_codec_t* c, hipStream_t st, std::initializer_list<ListPart> 
 // host plan cache holds 16; past it every pattern would cost a host build, an upload and a launch).
 constexpr size_t kHostPlanGroups = 16;
 
+// The fixed r x (k + r) matrix of the GF(256) per-stripe route over every slot: route 1 the r syndromes,
+// H[j][i] = X_i^j (reed_solomon.c:443-559); route 2 the re-encode differences [G | I] (k_plan_reenc_m8), G the
+// encode matrix, I on the repair slots.
+std::vector<uint16_t> syn_fixed_matrix(const std::vector<uint16_t>& positions, int k, int r, int route) {
+    const int n = k + r;
+    std::vector<uint16_t> H(size_t(r) * n);
+    if (route == 2) {
+        std::vector<uint16_t> G;
+        std::vector<int32_t> gi, go;
+        codec_matrix(positions, uint16_t(k), uint16_t(r), nullptr, G, gi, go);  // r x k
+        for (int p = 0; p < r; ++p) {
+            for (int i = 0; i < k; ++i) H[size_t(p) * n + i] = G[size_t(p) * k + i];
+            H[size_t(p) * n + k + p] = 1;
+        }
+    } else {
+        const Field& F = field();
+        for (int j = 0; j < r; ++j)
+            for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(positions[i]) * j) % kN];
+    }
+    return H;
+}
+
 // Syndrome route eligibility: the r x (k + r) syndrome matrix H[j][i] = X_i^j runs on its bit-plane XOR
 // kernel (built once per codec), which covers whole 2 KiB column blocks only.
 bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
@@ -55,22 +77,7 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
         int64_t(n) * symbol_stride >= (int64_t(1) << 31) || int64_t(c->r) * int64_t(S) >= (int64_t(1) << 31))
         return false;
     if (!c->syn) {
-        // syn_route 1: the r syndromes, H[j][i] = X_i^j over all k + r slots (reed_solomon.c:443-559);
-        // 2: the re-encode differences [G | I] (k_plan_reenc_m8), G = the encode matrix, I on the repair slots
-        std::vector<uint16_t> H(size_t(c->r) * n);
-        if (c->syn_route == 2) {
-            std::vector<uint16_t> G;
-            std::vector<int32_t> gi, go;
-            codec_matrix(c->positions, c->k, c->r, nullptr, G, gi, go);  // r x k
-            for (int p = 0; p < c->r; ++p) {
-                for (int i = 0; i < c->k; ++i) H[size_t(p) * n + i] = G[size_t(p) * c->k + i];
-                H[size_t(p) * n + c->k + p] = 1;
-            }
-        } else {
-            const Field& F = field();
-            for (int j = 0; j < c->r; ++j)
-                for (int i = 0; i < n; ++i) H[size_t(j) * n + i] = F.exp[(uint64_t(c->positions[i]) * j) % kN];
-        }
+        std::vector<uint16_t> H = syn_fixed_matrix(c->positions, c->k, c->r, c->syn_route);
         std::vector<int32_t> in(n), out(c->r);
         for (int i = 0; i < n; ++i) in[size_t(i)] = i;
         for (int j = 0; j < c->r; ++j) out[size_t(j)] = j;
@@ -80,7 +87,8 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
             c->syn_failed = true;
             return false;
         }
-        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj) || !p->xj) {
+        // the masked form: each stripe's erased slots read as zero (XJArgs::masks)
+        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, true) || !p->xj) {
             std::fprintf(stderr, "librs_amd: syndrome XOR kernel unavailable; per-stripe survivor plans\n");
             c->syn_failed = true;
             return false;
@@ -88,6 +96,33 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
         c->syn = std::move(p);
     }
     return true;
+}
+
+// The masked fixed pass of one chunk of the syndrome / re-encode route: the r rows of every selected stripe
+// into the chunk-local scratch, each stripe's erased slots (bits of its mask words) read as zero, so the
+// per-stripe solve yields the erased information symbols themselves and stores them.
+static int syn_fixed_pass(rsg_codec_t* c, const uint8_t* base, int64_t stripe_stride, int64_t symbol_stride,
+                          uint8_t* syn, int64_t per, uint64_t S, int64_t cn, const int32_t* d_ids,
+                          const uint32_t* d_mbits, uint32_t mw, hipStream_t st) {
+    DevPlan& p = *c->syn;
+    if (int rc = p.order_after_build(st)) return rc;
+    XJArgs x{};
+    x.src = base;
+    x.src_stripe = stripe_stride;
+    x.dst = syn;
+    x.dst_stripe = per;
+    x.src_sym = int32_t(symbol_stride);
+    x.dst_sym = int32_t(S);
+    x.ids = d_ids;
+    x.dst_local = 1u;
+    x.mask_words = mw;
+    x.masks = d_mbits;
+    x.zero = static_cast<const uint8_t*>(c->d_zero);
+    c->last_kernel = p.xj->name;
+    const int rc = xj_launch(*p.xj, x, cn, int64_t(S / 2048) * (2048 / kXjChunk), st);
+    const int rc2 = p.note_use(st);
+    if (!rc && !rc2) RS_CHECKPOINT(c, &p, "per-stripe fixed pass (masked rs_xj)", uint64_t(cn), S);
+    return rc ? rc : rc2;
 }
 
 // Nonzero bytes of [p, p + len): an erasure pattern's set entries (a bool is erased when nonzero, as in
@@ -164,13 +199,31 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     if ((rc = grow(&c->d_pin, c->pin_cap, size_t(chunk * in_stride) * 4))) return rc;
     if ((rc = grow(&c->d_pout, c->pout_cap, size_t(chunk * out_stride) * 4))) return rc;
     if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(chunk * idx_stride) * 4))) return rc;
-    if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
+    const bool syn = syn_prepare(c, S, symbol_stride);
+    // the masked fixed pass takes each stripe's pattern as bit words too ([nsel][mw])
+    const uint32_t mw = uint32_t((n + 31) / 32);
+    std::vector<uint32_t> mbits(syn ? ids.size() * mw : 0, 0);
+    for (size_t j = 0; syn && j < ids.size(); ++j)
+        for (size_t i = 0; i < n; ++i)
+            if (masks[j * n + i]) mbits[j * mw + i / 32] |= 1u << (i % 32);
+    if (syn) {
+        if ((rc = grow(&c->d_mbits, c->mbits_cap, std::max<size_t>(mbits.size() * 4, 4)))) return rc;
+        if (!c->d_zero) {
+            HIP_TRY(hipMalloc(&c->d_zero, 256));
+            HIP_TRY(hipMemset(c->d_zero, 0, 256));
+        }
+    }
+    if ((rc = syn ? stage_lists(c, st,
+                                {{c->d_ids, ids.data(), ids.size() * 4},
+                                 {c->d_masks, masks.data(), masks.size()},
+                                 {c->d_mbits, mbits.data(), mbits.size() * 4}})
+                  : stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
         return rc;
-    if (syn_prepare(c, S, symbol_stride)) {
-        // syndrome / re-encode route: the per-stripe solves (k_plan_syn_m8 / k_plan_reenc_m8), the fixed
-        // pass's r outputs of every selected stripe into scratch (XOR kernel, dst indexed by the
-        // chunk-local stripe), then the per-stripe solves from those XORed into the erased information
-        // slots (not zeroed first: V1Args::xor_dst). Option m8_syn_overlap: plans and fixed pass of chunk
+    if (syn) {
+        // syndrome / re-encode route: the per-stripe solves (k_plan_syn_m8 / k_plan_reenc_m8), the masked
+        // fixed pass's r outputs of every selected stripe into scratch (XOR kernel, dst indexed by the
+        // chunk-local stripe; erased slots read as zero, so nothing needs zeroing first), then the per-stripe
+        // solves from those stored into the erased information slots. Option m8_syn_overlap: plans and fixed pass of chunk
         // i + 1 run on the codec's syndrome stream beside chunk i's solve on the caller's stream, two
         // buffer sets alternating.
         const uint16_t* expt = nullptr;
@@ -214,8 +267,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             pa.idx_stride = idx_stride;
             HIP_TRY(launch_plan_syn_m8(pa, cn, sy, c->syn_route));
             uint8_t* syn = static_cast<uint8_t*>(c->d_syn) + set * sch * per;
-            if ((rc = run_plan(c, *c->syn, base, stripe_stride, symbol_stride, syn, per, int64_t(S), uint64_t(cn), S,
-                               sy, c->d_ids + c0, true)))
+            if ((rc = syn_fixed_pass(c, base, stripe_stride, symbol_stride, syn, per, S, cn, c->d_ids + c0,
+                                     static_cast<const uint32_t*>(c->d_mbits) + size_t(c0) * mw, mw, sy)))
                 return rc;
             if (ovl) {
                 HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
@@ -237,9 +290,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_in = in_stride;
             v.ps_out = out_stride;
             v.ps_idx = idx_stride;
-            v.xor_dst = 1;  // the erased slots were not zeroed: their contents g + (g + c)
+            v.xor_dst = 0;  // the masked fixed pass read the erased slots as zero: the solve yields them
 #ifdef RS_AMD_DIAG
-            if (c->m8_ps_ablate & 4) v.xor_dst = 0;  // timing ablation: no old-value loads (wrong results)
             v.ablate = c->m8_ps_ablate & 3;
 #endif
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
@@ -899,4 +951,23 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         ++gi;
     }
     return scratch_release(c, st);
+}
+
+extern "C" int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len) {
+    if (uint32_t(k) + r > kN || (route != 1 && route != 2)) return RS_ERR_INVALID;
+    const std::vector<uint16_t> pos = code_positions(k, r);
+    if (subfield_degree(pos) > 8) return RS_ERR_INVALID;
+    const int n = int(k) + r;
+    if (!xj_supported(8, n, r)) return RS_ERR_INVALID;
+    std::vector<int32_t> in(static_cast<size_t>(n)), out(static_cast<size_t>(r));
+    for (int i = 0; i < n; ++i) in[size_t(i)] = i;
+    for (int j = 0; j < r; ++j) out[size_t(j)] = j;
+    const std::string src = xj_source(syn_fixed_matrix(pos, k, r, route), n, r, in, out, true, masked != 0);
+    if (len) *len = src.size();
+    if (buf && cap) {
+        const size_t m = std::min(cap - 1, src.size());
+        std::memcpy(buf, src.data(), m);
+        buf[m] = 0;
+    }
+    return 0;
 }

@@ -319,7 +319,7 @@ struct rsg_codec {
     // block, the next chunk's ring prologue in flight during this chunk's output stage)
     int m8_ps_cpb = 1;
     // diagnostic builds: option m8_ps_ablate, timing ablations of the per-stripe solve (wrong results): 1 no
-    // table copy, 2 no output conversion, 4 no old-value loads (xor_dst off)
+    // table copy, 2 no output conversion
     int m8_ps_ablate = 0;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;
@@ -373,11 +373,16 @@ struct rsg_codec {
         }
         for (void* p : {static_cast<void*>(d_ids), static_cast<void*>(d_elem), d_masks, d_kr, d_pin, d_pout, d_pidx,
                         d_partial, d_syn, d_bp16, d_bp16_rec, d_cs, d_reenc, d_goff[0], d_goff[1], d_ps_rec,
-                        d_ps_small, static_cast<void*>(d_ps_in), static_cast<void*>(d_slot_err)})
+                        d_ps_small, static_cast<void*>(d_ps_in), static_cast<void*>(d_slot_err), d_mbits, d_zero})
             if (p) (void)hipFree(p);
     }
     std::string last_kernel = "none";
     int32_t* d_slot_err = nullptr;  // checked launches of diagnostic builds: [4] slot-violation record
+    // GF(256) per-stripe route: the selected stripes' patterns as bit words ([nsel][ceil((k + r) / 32)]) for the
+    // masked fixed pass, and the 256-byte zero buffer its erased slots read
+    void* d_mbits = nullptr;
+    size_t mbits_cap = 0;
+    void* d_zero = nullptr;
 };
 
 namespace rsamd {
@@ -417,6 +422,10 @@ int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out
 // codec scratch shared by launches on different streams: wait for / mark the last user
 int scratch_acquire(rsg_codec_t* c, hipStream_t st);
 int scratch_release(rsg_codec_t* c, hipStream_t st);
+
+// ------------------------------------------------------------------ rs_batch.cpp
+// the fixed r x (k + r) matrix of the GF(256) per-stripe route (1 syndromes, 2 re-encode differences [G | I])
+std::vector<uint16_t> syn_fixed_matrix(const std::vector<uint16_t>& positions, int k, int r, int route);
 
 // ------------------------------------------------------------------ rs_route16.cpp
 int make_plan(rsg_codec_t* c, const bool* erased, std::unique_ptr<DevPlan>& out, hipStream_t st);

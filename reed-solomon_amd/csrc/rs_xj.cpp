@@ -169,6 +169,9 @@ struct XjConfig {
                        // 3: 1 over each early load burst
     int early = 1;     // 1 (ring 2): pair g+2's loads go out inside pair g, right after its last row that reads
                        // one of the pair's raw inputs (those rows first), so a load has ~1.5 pairs to land
+    int masked = 0;    // 1 (set_masked; the per-stripe fixed pass of rsg_decode_batch): every input slot whose
+                       // bit is set in the launch-local stripe's mask words reads a zero buffer instead
+                       // (s_bitcmp1 + s_cselect_b64 on the load's base pair): erased slots count as zero
     // env: read the RS_XJ_* generation knobs (experiments, the emulator tests through rsg_xj_source, the
     // diagnostic build). The kernels the release library launches are generated with the defaults
     // whatever the environment says, so no deployment's environment changes the shipped kernel.
@@ -217,6 +220,14 @@ struct XjConfig {
         splitwait = (splitwait && !lds && !share && cpb == 1) ? 1 : 0;
         inlinefin = (inlinefin && !lfin && cpb == 1) ? 1 : 0;
     }
+    // masked loads exist for the default layout only (global loads with an SGPR base pair per input, one
+    // column per block, plain block order)
+    void set_masked() {
+        masked = 1;
+        buffer = lds = lfin = share = xcd = spread = 0;
+        cpb = 1;
+        ring = 2;
+    }
     // the column loop needs the last pair in ring slot 1, so the next column's pair 0 has slot 0 to itself
     void set_k(int K) {
         if (((K + 7) / 8) % 2) cpb = 1;
@@ -242,6 +253,7 @@ struct XjConfig {
         if (splitwait) s += " splitwait";
         if (inlinefin) s += " inlinefin";
         if (prio) s += " prio";
+        if (masked) s += " masked";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -497,6 +509,11 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
                 ops.push_back(E.fmt("s_mul_i32 s62, s34, %d", slot));
                 ops.push_back(E.fmt("s_add_u32 s%d, s%d, s62", 40 + 2 * j, next_col ? 60 : 32));
                 ops.push_back(E.fmt("s_addc_u32 s%d, s%d, 0", 41 + 2 * j, next_col ? 61 : 33));
+                if (C.masked) {  // an erased slot of this stripe reads the zero buffer
+                    ops.push_back(E.fmt("s_bitcmp1_b32 %%[mw%d], %d", slot / 32, slot % 32));
+                    ops.push_back(E.fmt("s_cselect_b64 s[%d:%d], %%[zb], s[%d:%d]", 40 + 2 * j, 41 + 2 * j, 40 + 2 * j,
+                                        41 + 2 * j));
+                }
                 ops.push_back(E.fmt("global_load_dword v%d, %s, s[%d:%d]%s", dst, COL, 40 + 2 * j, 41 + 2 * j,
                                     (C.nt & 1) ? " nt" : ""));
             }
@@ -803,8 +820,9 @@ static void count_insts(const std::vector<std::string>& L, uint64_t mult, uint64
 }
 
 static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-               const std::vector<int32_t>& out_slots, uint64_t* valu, uint64_t* salu) {
+               const std::vector<int32_t>& out_slots, bool masked, uint64_t* valu, uint64_t* salu) {
     XjConfig C(R);
+    if (masked) C.set_masked();
     C.set_k(K);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
@@ -820,9 +838,12 @@ static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::v
 }
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots, bool env_knobs) {
+                      const std::vector<int32_t>& out_slots, bool env_knobs, bool masked) {
     XjConfig C(R, env_knobs);
+    if (masked) C.set_masked();
     C.set_k(K);
+    int nmw = 0;  // mask words the loads test (slot / 32 < nmw)
+    for (int32_t v : in_slots) nmw = std::max(nmw, v / 32 + 1);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
     for (size_t e = 0; e < M.size(); ++e) cb[e] = C.lfin ? gamma8().coord(M[e]) : B.bits(M[e]);
@@ -834,7 +855,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
          "typedef unsigned int xj_u4 __attribute__((ext_vector_type(4)));\n"
          "struct XJArgs { const uint8_t* src; int64_t src_stripe; uint8_t* dst; int64_t dst_stripe;"
          " int32_t src_sym, dst_sym; const int32_t* ids; const uint16_t* tab; uint32_t nchunks, ncols,"
-         " dst_local; };\n"
+      << (C.masked ? " dst_local, mask_words; const uint32_t* masks; const uint8_t* zero; };\n" : " dst_local; };\n")
       << "// K=" << K << " R=" << R << " roles=" << roles << " pairs=" << pairs << " " << C.tag() << "\n"
       << "extern \"C\" __global__ void __launch_bounds__(" << 64 * roles * pairs << ") rs_xj(XJArgs a) {\n";
     if (C.lfin) {
@@ -878,6 +899,11 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
              "  const uint32_t la = lb + (threadIdx.x & 63u) * 4u;\n"
              "  {\n";
     }
+    if (C.masked) {  // the launch-local stripe's mask words; the zero buffer's base for this column
+        o << "  const uint32_t* xj_mk = a.masks + (uint64_t)blockIdx.y * a.mask_words;\n";
+        for (int w = 0; w < nmw; ++w) o << "  const uint32_t mw" << w << " = xj_mk[" << w << "];\n";
+        o << "  const uint64_t zb = (uint64_t)a.zero - (uint64_t)blockIdx.x * 256u;\n";
+    }
     o << "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
          "  const uint64_t db = (uint64_t)a.dst + dstripe * (uint64_t)a.dst_stripe;\n"
          "  const uint32_t sl = (uint32_t)sb, sh = (uint32_t)(sb >> 32), dl = (uint32_t)db, dh = (uint32_t)(db >> 32);\n"
@@ -892,7 +918,12 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
           << (C.cpb > 1 ? "  : [col] \"+v\"(col) : [nc] \"s\"(nc), [cs] \"s\"(cs), "  // no LDS address: one VGPR fewer (3 waves/SIMD)
                         : "  : : [col] \"v\"(col), [la] \"v\"(la), ")
           << "[sl] \"s\"(sl), [sh] \"s\"(sh), [dl] \"s\"(dl), [dh] \"s\"(dh),"
-             " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)\n  : "
+             " [ss] \"s\"(a.src_sym), [ds] \"s\"(a.dst_sym), [lb] \"s\"(lb)";
+        if (C.masked) {
+            for (int m = 0; m < nmw; ++m) o << ", [mw" << m << "] \"s\"(mw" << m << ")";
+            o << ", [zb] \"s\"(zb)";
+        }
+        o << "\n  : "
           << clob << ");\n    break;\n";
     }
     o << "  }\n  }\n}\n";
@@ -924,8 +955,8 @@ int xj_pairs(int R) {
 // (rocprofv3 Kernel_Name) tell the encode and decode kernels of one run apart; the same hash names
 // the kernel in rsg_last_kernel ("rs_xj[RxK:<hash>]").
 static std::string xj_named_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                                   const std::vector<int32_t>& out_slots, std::string* fname) {
-    std::string src = xj_source(M, K, R, in_slots, out_slots);
+                                   const std::vector<int32_t>& out_slots, std::string* fname, bool masked = false) {
+    std::string src = xj_source(M, K, R, in_slots, out_slots, false, masked);
     char nm[32];
     std::snprintf(nm, sizeof nm, "rs_xj_%08llx", static_cast<unsigned long long>(jit_hash(src) & 0xffffffff));
     const std::string key = ") rs_xj(XJArgs a)";
@@ -936,20 +967,20 @@ static std::string xj_named_source(const std::vector<uint16_t>& M, int K, int R,
 }
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                  const std::vector<int32_t>& out_slots) {
+                  const std::vector<int32_t>& out_slots, bool masked) {
     if (!xj_supported(8, K, R)) return 0;
     std::string fname;
-    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname);
+    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname, masked);
     std::vector<char> code;
     return jit_code(src, "xj", jit_hash(src), code) ? 3 : 0;
 }
 
 int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out) {
+             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, bool masked) {
     out.reset();
     if (!xj_supported(8, K, R)) return 0;
     std::string fname;
-    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname);
+    const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname, masked);
     uint64_t h = 0;
     std::shared_ptr<JitModule> mod;
     if (jit_module(src, "xj", mod, &h)) return 3;
@@ -957,17 +988,19 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     k->mod = mod;
     (void)hipGetDevice(&k->device);
     k->roles = xj_roles(R);
-    k->pairs = XjConfig(R).lfin ? xj_pairs(R) : 0;
+    k->masked = masked;
     {
         XjConfig C(R);
+        if (masked) C.set_masked();
         C.set_k(K);
         k->cpb = C.cpb;
+        k->pairs = C.lfin ? xj_pairs(R) : 0;
     }
     if (hipModuleGetFunction(&k->fn, jit_module_handle(*mod), fname.c_str()) != hipSuccess) return 3;
     char nm[64];
     std::snprintf(nm, sizeof nm, "rs_xj[%dx%d:%s]", R, K, fname.c_str() + 6);
     k->name = nm;
-    xj_counts(M, K, R, in_slots, out_slots, &k->valu_per_col, &k->salu_per_col);
+    xj_counts(M, K, R, in_slots, out_slots, masked, &k->valu_per_col, &k->salu_per_col);
     out = std::move(k);
     return 0;
 }
@@ -1058,6 +1091,7 @@ int xj_launch(const XjKernel& k, const XJArgs& a0, int64_t n_stripes, int64_t nc
             a.src += s0 * a.src_stripe;
             a.dst += s0 * a.dst_stripe;
         }
+        if (a.masks) a.masks += s0 * int64_t(a.mask_words);  // indexed by the launch-local stripe
         a.nchunks = uint32_t(nchunks);
         const unsigned ny = unsigned(std::min<int64_t>(65535, n_stripes - s0));
         void* args[] = {&a};

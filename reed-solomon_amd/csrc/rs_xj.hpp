@@ -36,6 +36,12 @@ struct XJArgs {
     const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch)
     uint32_t nchunks, ncols;   // chunks per stripe (set by xj_launch); persistent form: chunks in the launch
     uint32_t dst_local;        // 1: dst indexed by the launch-local stripe (ids only select the source)
+    // masked kernels (xj_build(..., masked)): input slot i of launch-local stripe s reads the zero buffer when
+    // bit i % 32 of masks[s * mask_words + i / 32] is set. The fields trail the struct, so unmasked kernels
+    // (whose generated source declares only the fields above) read the same prefix.
+    uint32_t mask_words;
+    const uint32_t* masks;
+    const uint8_t* zero;       // >= 256 zero bytes
 };
 
 struct XjKernel {
@@ -45,6 +51,7 @@ struct XjKernel {
     int roles = 0;  // waves per column (opr outputs each)
     int pairs = 0;  // > 0: persistent kernel (LDS finish), columns per workgroup in flight, grid <= CUs
     int cpb = 1;    // consecutive 256-byte columns per workgroup (column loop), grid.x = chunks / cpb
+    bool masked = false;  // per-stripe input masks (XJArgs::masks)
     std::string name;
     // wave instructions per 256-byte column, all role waves together, counted in the generated asm
     // (the XOR network, the finish once per role, loads / stores / addressing); the compiler's few
@@ -84,12 +91,13 @@ int xj_fin();                // generation setting (RS_XJ_FIN, default 0)
 int xj_pairs(int R);         // columns per workgroup (1 unless the LDS-table finish is on)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
 // env_knobs: honour the RS_XJ_* generation knobs (inspection / emulator tests; the launched kernels never do)
+// masked: the per-stripe input-mask form (XjConfig::masked, XJArgs::masks), default layout only
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots, bool env_knobs = false);
+                      const std::vector<int32_t>& out_slots, bool env_knobs = false, bool masked = false);
 int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out);
+             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, bool masked = false);
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                  const std::vector<int32_t>& out_slots);
+                  const std::vector<int32_t>& out_slots, bool masked = false);
 // Launches over the first `nchunks` 256-byte column chunks of every stripe.
 int xj_launch(const XjKernel& k, const XJArgs& a, int64_t n_stripes, int64_t nchunks, hipStream_t st);
 

@@ -189,3 +189,55 @@ def test_xj_column_loop_matches_oracle(k, r, kind, cpb, ncols, monkeypatch):
         assert "cpb%d" % cpb in src
         _run_grid(src, mem, S4, 0, ncols, cpb)
         assert np.array_equal(mem.b.reshape(k + r, S4)[:k], full[:k])
+
+
+def xj_fixed_source(k, r, route, masked):
+    n = ctypes.c_size_t()
+    assert _lib.rsg_xj_fixed_source(k, r, route, masked, None, 0, ctypes.byref(n)) == 0
+    buf = ctypes.create_string_buffer(n.value + 1)
+    assert _lib.rsg_xj_fixed_source(k, r, route, masked, buf, n.value + 1, ctypes.byref(n)) == 0
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("route", [1, 2])
+@pytest.mark.parametrize("k,r,kind", [(128, 32, "t32info"), (128, 32, "mixed"), (10, 4, "mixed"), (30, 17, "t32info"),
+                                      (20, 9, "none")])
+def test_xj_masked_fixed_pass(k, r, kind, route):
+    """The per-stripe route's masked fixed pass (rsg_decode_batch, GF(256)): with garbage in the erased slots,
+    the masked kernel equals the plain kernel run on the same stripe with those slots zeroed, for the
+    syndrome (1) and re-encode (2) matrices; for route 2 that is [G | I] applied to the zeroed stripe, i.e.
+    the oracle's repair of the zeroed information XOR the zeroed received repair."""
+    n = k + r
+    rng = np.random.default_rng(k * 7 + r + route)
+    full = _random_stripe(k, r, k + 3 * r)
+    assert oracle_encode(k, r, full) == 0
+    er = np.zeros(n, bool)
+    if kind == "t32info":
+        er[rng.choice(k, min(k, r), replace=False)] = True
+    elif kind == "mixed":
+        er[rng.choice(n, r, replace=False)] = True
+    rcv = full.copy()
+    rcv[er] = rng.integers(0, 256, (int(er.sum()), S), dtype=np.uint8)  # garbage, not zeros
+    zeroed = rcv.copy()
+    zeroed[er] = 0
+    words = [0] * ((n + 31) // 32)
+    for i in np.nonzero(er)[0]:
+        words[i // 32] |= 1 << (i % 32)
+    src = xj_fixed_source(k, r, route, 1)
+    assert "s_bitcmp1_b32" in src and "masked" in src
+    zero = (n + r) * S
+    mem = Memory(zero + 256)
+    mem.b[:n * S] = rcv.reshape(-1)
+    run_block(src, mem, 0, S, n * S, S, masks=words, zero=zero)
+    got = mem.b[n * S:(n + r) * S].reshape(r, S).copy()
+    ref = Memory((n + r) * S)
+    ref.b[:n * S] = zeroed.reshape(-1)
+    plain = xj_fixed_source(k, r, route, 0)
+    assert "s_bitcmp1_b32" not in plain
+    run_block(plain, ref, 0, S, n * S, S)
+    assert np.array_equal(got, ref.b[n * S:].reshape(r, S))
+    if route == 2:
+        info = zeroed.copy()
+        info[k:] = 0
+        assert oracle_encode(k, r, info) == 0
+        assert np.array_equal(got, info[k:] ^ zeroed[k:])

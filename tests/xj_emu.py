@@ -136,6 +136,15 @@ class Wave:
                 continue
             if op in ("s_nop", "s_getpc_b64", "s_barrier", "s_setprio"):
                 continue
+            if op == "s_bitcmp1_b32":  # masked loads: SCC = bit a[1] of a[0]
+                self.scc = (self.val(a[0]) >> (self.val(a[1]) & 31)) & 1
+                continue
+            if op == "s_cselect_b64":  # dst pair = SCC ? src0 : src1 (a "%[name]" source is a 64-bit operand)
+                lo = int(re.match(r"s\[(\d+):", a[0]).group(1))
+                pick = a[1] if self.scc else a[2]
+                v = self.ops[pick[2:-1]] if pick.startswith("%[") else self.pair(pick)
+                self.s[lo], self.s[lo + 1] = np.uint64(v & 0xFFFFFFFF), np.uint64((v >> 32) & 0xFFFFFFFF)
+                continue
             # gpr-index mode (s_set_gpr_idx_on ..., gpr_idx(SRC0)): src0 of VALU ops is offset by the index
             if op == "s_set_gpr_idx_on":
                 assert a[1] == "gpr_idx(SRC0)", ln
@@ -342,10 +351,11 @@ class Memory:
         self.b[idx.reshape(-1)] = np.ascontiguousarray(val, dtype="<u4").view(np.uint8)
 
 
-def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, gx=1):
+def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, gx=1, masks=None, zero=None):
     """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`
     (LDS base address 0; each role's ring region at role * region bytes). Column-loop kernels (cpb > 1)
-    process `ncols` columns from `chunk`, `gx` (the grid's x size) columns apart."""
+    process `ncols` columns from `chunk`, `gx` (the grid's x size) columns apart. Masked kernels take the
+    stripe's mask words (`masks`, list of ints) and the byte address of a zero buffer in `mem` (`zero`)."""
     finish, roles = split_source(src)
     m = re.search(r"\(uint32_t\)role \* (\d+)u", src)
     region = int(m.group(1)) if m else 0
@@ -362,6 +372,10 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, 
                    dh=dst_base >> 32, ss=src_sym, ds=dst_sym, lb=lb, nc=ncols, cs=gx * 256,
                    la=(lb + np.arange(64) * 4).astype(np.uint32))
         ops["col"] = col.copy()
+        if masks is not None:  # the kernel's C prologue: mask words and the zero base of this column
+            for i, w in enumerate(masks):
+                ops[f"mw{i}"] = int(w)
+            ops["zb"] = (int(zero) - chunk * 256) & 0xFFFFFFFFFFFFFFFF
         wave = Wave(mem, ops)
         wave.lds = lds
         waves.append(wave)
