@@ -222,6 +222,9 @@ int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int
  * slot whose bit is set in its stripe's mask words as zero. RS_ERR_INVALID when the route does not apply
  * (m = 16 codes, K * R past the XOR kernel's bound). Host only (emulator tests). */
 int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len);
+/* Compiles the masked fixed-pass kernel of that route into the JIT cache, like rsg_jit_precompile (0 when the
+ * route does not apply). Host only. */
+int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route);
 const char* rsg_version(void);
 /* 1 when checked launches are on (environment RS_AMD_CHECK set and not "0" at the first call of the
  * process), else 0. In checked mode every launch group is followed by a device wait and an error read: a

@@ -953,6 +953,17 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     return scratch_release(c, st);
 }
 
+extern "C" int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route) {
+    if (uint32_t(k) + r > kN || (route != 1 && route != 2)) return RS_ERR_INVALID;
+    const std::vector<uint16_t> pos = code_positions(k, r);
+    const int n = int(k) + r;
+    if (subfield_degree(pos) > 8 || !xj_supported(8, n, r)) return 0;
+    std::vector<int32_t> in(static_cast<size_t>(n)), out(static_cast<size_t>(r));
+    for (int i = 0; i < n; ++i) in[size_t(i)] = i;
+    for (int j = 0; j < r; ++j) out[size_t(j)] = j;
+    return xj_precompile(syn_fixed_matrix(pos, k, r, route), n, r, in, out, true);
+}
+
 extern "C" int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len) {
     if (uint32_t(k) + r > kN || (route != 1 && route != 2)) return RS_ERR_INVALID;
     const std::vector<uint16_t> pos = code_positions(k, r);

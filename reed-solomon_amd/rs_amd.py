@@ -139,6 +139,7 @@ _sig("rsg_symbol_stats", ctypes.c_int, ctypes.POINTER(SymbolStatsT))
 _sig("rsg_symbol_pool_cap", i64, i64)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("rsg_check_enabled", ctypes.c_int)
+_sig("rsg_xj_fixed_precompile", ctypes.c_int, u16, u16, ctypes.c_int)
 _sig("rsg_xj_fixed_source", ctypes.c_int, u16, u16, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
      ctypes.POINTER(ctypes.c_size_t))
 _sig("gf_create", P)

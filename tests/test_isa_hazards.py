@@ -116,3 +116,13 @@ def test_release_build_has_no_ablation_kernels():
     if os.path.exists(diag):
         d = _kernel_names(diag)
         assert rel <= d and any(any(x in n for x in DIAG_ONLY) for n in d)
+
+
+@pytest.mark.parametrize("k,r,route", [(128, 32, 2), (128, 32, 1), (10, 4, 2)])
+def test_masked_fixed_pass_compiles_without_inflight_reads(k, r, route, tmp_path, monkeypatch):
+    """The GF(256) per-stripe route's masked fixed-pass kernel compiles with hiprtc and has no in-flight read."""
+    monkeypatch.setenv("RS_AMD_JIT_CACHE", str(tmp_path))
+    assert rs_amd._lib.rsg_xj_fixed_precompile(k, r, route) == 0
+    objs = [os.path.join(tmp_path, f) for f in os.listdir(tmp_path) if f.endswith(".co")]
+    assert len(objs) == 1, objs
+    _check(objs[0])
