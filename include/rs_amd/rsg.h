@@ -102,8 +102,8 @@ int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value);
  * rsg_codec_trim waits for the codec's outstanding work on that scratch and frees it: every buffer above,
  * the stripe-id lists, the route's slot-offset tables, the GF(2^16) many-pattern batch plan with its records
  * (up to 256 MiB) and pinned staging, and the host-pipeline buffers. What survives: the cached encode /
- * decode plans, the per-codec streams and events, and three small tables (slot elements, 2 (k + r) bytes;
- * the per-stripe route's input list, 4 (r + 16) bytes; a 256-byte zero buffer). Later calls grow the scratch again. */
+ * decode plans, the per-codec streams and events, and two small tables (slot elements, 2 (k + r) bytes;
+ * the per-stripe route's input list, 4 (r + 16) bytes). Later calls grow the scratch again. */
 int rsg_codec_trim(rsg_codec_t* c);
 /* Name of the kernel the last encode/decode launched (diagnostics). */
 const char* rsg_last_kernel(const rsg_codec_t* c);

@@ -253,6 +253,11 @@ extern "C" int rsg_codec_trim(rsg_codec_t* c) {
     drop(c->d_pout, c->pout_cap);
     drop(c->d_pidx, c->pidx_cap);
     drop(c->d_mbits, c->mbits_cap);
+    {
+        size_t zc = size_t(c->zero_cap);
+        drop(c->d_zero, zc);
+        c->zero_cap = 0;
+    }
     size_t ids_bytes = c->ids_cap * 4;  // ids_cap counts entries
     drop(reinterpret_cast<void*&>(c->d_ids), ids_bytes);
     c->ids_cap = 0;

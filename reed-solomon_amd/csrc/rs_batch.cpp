@@ -200,24 +200,19 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
     if ((rc = grow(&c->d_pout, c->pout_cap, size_t(chunk * out_stride) * 4))) return rc;
     if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(chunk * idx_stride) * 4))) return rc;
     const bool syn = syn_prepare(c, S, symbol_stride);
-    // the masked fixed pass takes each stripe's pattern as bit words too ([nsel][mw])
+    // the masked fixed pass takes each stripe's pattern as bit words ([chunk][mw]), written by the plan kernels
     const uint32_t mw = uint32_t((n + 31) / 32);
-    std::vector<uint32_t> mbits(syn ? ids.size() * mw : 0, 0);
-    for (size_t j = 0; syn && j < ids.size(); ++j)
-        for (size_t i = 0; i < n; ++i)
-            if (masks[j * n + i]) mbits[j * mw + i / 32] |= 1u << (i % 32);
     if (syn) {
-        if ((rc = grow(&c->d_mbits, c->mbits_cap, std::max<size_t>(mbits.size() * 4, 4)))) return rc;
-        if (!c->d_zero) {
-            HIP_TRY(hipMalloc(&c->d_zero, 256));
-            HIP_TRY(hipMemset(c->d_zero, 0, 256));
+        if (S > c->zero_cap) {  // one symbol of zeros: erased slots' columns read it column for column
+            if (c->d_zero) (void)hipFree(c->d_zero);
+            c->d_zero = nullptr;
+            c->zero_cap = 0;
+            HIP_TRY(hipMalloc(&c->d_zero, S));
+            HIP_TRY(hipMemset(c->d_zero, 0, S));
+            c->zero_cap = S;
         }
     }
-    if ((rc = syn ? stage_lists(c, st,
-                                {{c->d_ids, ids.data(), ids.size() * 4},
-                                 {c->d_masks, masks.data(), masks.size()},
-                                 {c->d_mbits, mbits.data(), mbits.size() * 4}})
-                  : stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
+    if ((rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}, {c->d_masks, masks.data(), masks.size()}})))
         return rc;
     if (syn) {
         // syndrome / re-encode route: the per-stripe solves (k_plan_syn_m8 / k_plan_reenc_m8), the masked
@@ -238,6 +233,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         if ((rc = grow(&c->d_pin, c->pin_cap, size_t(nset * sch * in_stride) * 4))) return rc;
         if ((rc = grow(&c->d_pout, c->pout_cap, size_t(nset * sch * out_stride) * 4))) return rc;
         if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
+        if ((rc = grow(&c->d_mbits, c->mbits_cap, size_t(nset * sch) * mw * 4))) return rc;
         hipStream_t sy = st;
         if (ovl) {
             if ((rc = overlap_objects(c))) return rc;
@@ -265,10 +261,12 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             pa.in_stride = in_stride;
             pa.out_stride = out_stride;
             pa.idx_stride = idx_stride;
+            pa.mbits = static_cast<uint32_t*>(c->d_mbits) + size_t(set * sch) * mw;
+            pa.mw = int32_t(mw);
             HIP_TRY(launch_plan_syn_m8(pa, cn, sy, c->syn_route));
             uint8_t* syn = static_cast<uint8_t*>(c->d_syn) + set * sch * per;
-            if ((rc = syn_fixed_pass(c, base, stripe_stride, symbol_stride, syn, per, S, cn, c->d_ids + c0,
-                                     static_cast<const uint32_t*>(c->d_mbits) + size_t(c0) * mw, mw, sy)))
+            if ((rc = syn_fixed_pass(c, base, stripe_stride, symbol_stride, syn, per, S, cn, c->d_ids + c0, pa.mbits,
+                                     mw, sy)))
                 return rc;
             if (ovl) {
                 HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));

@@ -379,10 +379,11 @@ struct rsg_codec {
     std::string last_kernel = "none";
     int32_t* d_slot_err = nullptr;  // checked launches of diagnostic builds: [4] slot-violation record
     // GF(256) per-stripe route: the selected stripes' patterns as bit words ([nsel][ceil((k + r) / 32)]) for the
-    // masked fixed pass, and the 256-byte zero buffer its erased slots read
+    // masked fixed pass, and the zero buffer (one symbol long) its erased slots read
     void* d_mbits = nullptr;
     size_t mbits_cap = 0;
     void* d_zero = nullptr;
+    uint64_t zero_cap = 0;
 };
 
 namespace rsamd {

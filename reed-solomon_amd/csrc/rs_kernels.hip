@@ -1509,6 +1509,14 @@ __global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
 // Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Erased slots are
 // not zeroed: their old contents g enter the syndromes, the solve yields g + c for the erased information
 // slots, and the apply XORs that into g (V1Args::xor_dst). Erased repair slots only shift their own unknowns.
+// The stripe's pattern as bit words for the masked fixed pass: wave w's ballot covers slots 64w .. 64w + 63.
+__device__ __forceinline__ void plan_mask_words(const SynPlanArgs& a, int64_t s, int w, int lane, uint64_t bits) {
+    if (!a.mbits || lane != 0) return;
+    uint32_t* o = a.mbits + s * a.mw;
+    if (2 * w < a.mw) o[2 * w] = uint32_t(bits);
+    if (2 * w + 1 < a.mw) o[2 * w + 1] = uint32_t(bits >> 32);
+}
+
 __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
     __shared__ uint16_t ee[256], pe[256];
     __shared__ int32_t ps[256];
@@ -1521,6 +1529,7 @@ __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
     const bool er = valid && a.masks[s * a.n + j] != 0;
     const uint64_t be = __ballot(er), bp = __ballot(er && j < a.k);
     const uint64_t below = (uint64_t(1) << lane) - 1;
+    plan_mask_words(a, s, w, lane, be);
     if (lane == 0) {
         cnt[w][0] = __popcll(be);
         cnt[w][1] = __popcll(bp);
@@ -1613,6 +1622,7 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
     const bool inf_er = er && j < a.k, rep_ok = valid && j >= a.k && !er;
     const uint64_t bp = __ballot(inf_er), bq = __ballot(rep_ok);
     const uint64_t below = (uint64_t(1) << lane) - 1;
+    plan_mask_words(a, s, w, lane, __ballot(er));
     if (lane == 0) {
         cnt[w][0] = __popcll(bp);
         cnt[w][1] = __popcll(bq);

@@ -70,6 +70,8 @@ struct SynPlanArgs {
     int32_t* pout;         // [n_sel][out_stride] erased information slots
     uint32_t* pidx;        // [n_sel][idx_stride] V = 1 nibble records
     int64_t in_stride, out_stride, idx_stride;
+    uint32_t* mbits;       // [n_sel][mw] the pattern as bit words (slot i: bit i % 32 of word i / 32), for the
+    int32_t mw;            // masked fixed pass (XJArgs::masks)
 };
 // kind 1: syndrome-route solves (k_plan_syn_m8); 2: re-encode solves (k_plan_reenc_m8)
 hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st, int kind = 1);

@@ -903,7 +903,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
         o << "  const uint32_t* xj_mk = a.masks + (uint64_t)blockIdx.y * a.mask_words;\n";
         for (int w = 0; w < nmw; ++w)  // wave-uniform values for the asm's SGPR operands
             o << "  const uint32_t mw" << w << " = __builtin_amdgcn_readfirstlane(xj_mk[" << w << "]);\n";
-        o << "  const uint64_t zb = (uint64_t)a.zero - (uint64_t)blockIdx.x * 256u;\n";
+        o << "  const uint64_t zb = (uint64_t)a.zero;\n";  // a zero buffer as long as the symbols
     }
     o << "  const uint64_t sb = (uint64_t)a.src + stripe * (uint64_t)a.src_stripe;\n"
          "  const uint64_t db = (uint64_t)a.dst + dstripe * (uint64_t)a.dst_stripe;\n"

@@ -41,7 +41,8 @@ struct XJArgs {
     // (whose generated source declares only the fields above) read the same prefix.
     uint32_t mask_words;
     const uint32_t* masks;
-    const uint8_t* zero;       // >= 256 zero bytes
+    const uint8_t* zero;       // zero bytes, at least as many as a symbol has (an erased slot's column c reads
+                               // zero + c, so the reads of different columns spread over the memory channels)
 };
 
 struct XjKernel {

@@ -29,6 +29,10 @@ abl)   # per-stripe solve fixed costs: ablation bits 1 no table copy, 2 no outpu
 prof)  # rocprofv3 kernel split of the production route (t32info, 4096 stripes)
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 scripts/bench_patterns.py 4096 t32info device_plans_syndrome > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
   grep '^{' $D/prof.log; head -8 $D/prof/run_kernel_stats.csv | cut -c1-160 ;;
+baseprof)  # the production route twice, then its rocprofv3 kernel split
+  for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done
+  timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 scripts/bench_patterns.py 4096 t32info device_plans_syndrome > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
+  grep '^{' $D/prof.log; head -6 $D/prof/run_kernel_stats.csv | cut -c1-160 ;;
 base)
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done ;;
 *) echo "unknown mode $MODE"; exit 2 ;;

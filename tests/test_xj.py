@@ -226,7 +226,7 @@ def test_xj_masked_fixed_pass(k, r, kind, route):
     src = xj_fixed_source(k, r, route, 1)
     assert "s_bitcmp1_b32" in src and "masked" in src
     zero = (n + r) * S
-    mem = Memory(zero + 256)
+    mem = Memory(zero + S)  # the zero buffer is one symbol long
     mem.b[:n * S] = rcv.reshape(-1)
     run_block(src, mem, 0, S, n * S, S, masks=words, zero=zero)
     got = mem.b[n * S:(n + r) * S].reshape(r, S).copy()

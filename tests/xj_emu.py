@@ -375,7 +375,7 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, 
         if masks is not None:  # the kernel's C prologue: mask words and the zero base of this column
             for i, w in enumerate(masks):
                 ops[f"mw{i}"] = int(w)
-            ops["zb"] = (int(zero) - chunk * 256) & 0xFFFFFFFFFFFFFFFF
+            ops["zb"] = int(zero)
         wave = Wave(mem, ops)
         wave.lds = lds
         waves.append(wave)
