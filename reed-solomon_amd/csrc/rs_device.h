@@ -202,9 +202,21 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
         }
         return;
     }
+    // Branch-free: outputs are stored from p = 31 down, and every p >= rows goes to output rows - 1's address
+    // first, so that output's own store (same lane, same address, later in program order) is the one that
+    // stays; straight-line groups of 8 conversions keep 32 LDS reads in flight.
+    const int32_t slast = sload(out + (rows - 1));
 #pragma unroll
-    for (int p = 0; p < 32; ++p)
-        if (p < rows) *at(p) = m8_v1_out<NB>(lt, p, a0, a1, b0, b1);
+    for (int p0 = 24; p0 >= 0; p0 -= 8) {
+        uint32_t w[8];
+#pragma unroll
+        for (int q = 7; q >= 0; --q) w[q] = m8_v1_out<NB>(lt, p0 + q, a0, a1, b0, b1);
+#pragma unroll
+        for (int q = 7; q >= 0; --q) {
+            const int32_t sl = p0 + q < rows ? slot(p0 + q) : slast;
+            *reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, sl, 2, p0 + q) ? sl : 0) * a.dst_sym) = w[q];
+        }
+    }
 }
 
 // Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile
