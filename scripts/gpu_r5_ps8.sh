@@ -3,6 +3,7 @@
 # usage: gpu_r5_ps8.sh MODE
 #   rec    solve kernel 0 vs the diagnostic one-record-round-trip ablation 8 (wrong results): how much of the
 #          step is the high-half record load's exposed latency
+#   kern   the production solve vs diagnostic solve kernels KERNS (default 1), t32info and rand
 #   base   the production route alone (t32info and rand), two reps
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -33,6 +34,15 @@ baseprof)  # the production route twice, then its rocprofv3 kernel split
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 scripts/bench_patterns.py 4096 t32info device_plans_syndrome > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
   grep '^{' $D/prof.log; head -6 $D/prof/run_kernel_stats.csv | cut -c1-160 ;;
+kern)  # the production solve against diagnostic solve kernels $KERNS (m8_ps_kernel values), t32info and rand
+  for rep in 1 2; do
+    run rel_t32_$rep 4096 t32info device_plans_syndrome
+    run rel_rand_$rep 4096 rand device_plans_syndrome
+    for kern in ${KERNS:-1}; do
+      RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_t32_$rep 4096 t32info device_plans_syndrome
+      RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_rand_$rep 4096 rand device_plans_syndrome
+    done
+  done ;;
 base)
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done ;;
 *) echo "unknown mode $MODE"; exit 2 ;;
