@@ -208,7 +208,9 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             c->d_zero = nullptr;
             c->zero_cap = 0;
             HIP_TRY(hipMalloc(&c->d_zero, S));
-            HIP_TRY(hipMemset(c->d_zero, 0, S));
+            // zeroed on the launch stream and waited for: later calls may come on other streams (once per growth)
+            HIP_TRY(hipMemsetAsync(c->d_zero, 0, S, st));
+            HIP_TRY(hipStreamSynchronize(st));
             c->zero_cap = S;
         }
     }
@@ -218,9 +220,9 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         // syndrome / re-encode route: the per-stripe solves (k_plan_syn_m8 / k_plan_reenc_m8), the masked
         // fixed pass's r outputs of every selected stripe into scratch (XOR kernel, dst indexed by the
         // chunk-local stripe; erased slots read as zero, so nothing needs zeroing first), then the per-stripe
-        // solves from those stored into the erased information slots. Option m8_syn_overlap: plans and fixed pass of chunk
-        // i + 1 run on the codec's syndrome stream beside chunk i's solve on the caller's stream, two
-        // buffer sets alternating.
+        // solves from those stored into the erased information slots. Option m8_syn_overlap (diagnostic build): plans
+        // and fixed pass of chunk i + 1 run on the codec's syndrome stream beside chunk i's solve on the caller's
+        // stream, two buffer sets alternating.
         const uint16_t* expt = nullptr;
         if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
         const int64_t per = int64_t(c->r) * int64_t(S);
