@@ -55,9 +55,10 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  per stripe; GF(2^16): see m16_ps); 2 device plans past 16 distinct patterns for GF(256)
  *                  codes and past one pattern for GF(2^16) codes (default)
  *   "syn_route"    GF(256) device-plan decodes (S a multiple of 2 KiB): 2 the re-encode differences
- *                  [G | I] of every slot on the bit-plane XOR kernel, then a per-stripe t_info x t_info
- *                  solve from the first t_info surviving repair rows (default); 1 syndromes of every slot
- *                  on that kernel, then a t_info x t solve; 0 survivor matrices
+ *                  [G | I] of every slot on the bit-plane XOR kernel (each stripe's erased slots read as
+ *                  zero), then a per-stripe t_info x t_info solve from the first t_info surviving repair rows
+ *                  that stores the erased information symbols (default); 1 syndromes of every slot on that
+ *                  kernel, then a t_info x t solve; 0 survivor matrices. Erased slots may hold anything.
  *   "m8_syn_overlap" 0 one stream (default); [diag] 1 that route's plans + fixed pass of the next chunk on a
  *                  codec stream beside this chunk's solve (two buffer sets)
  *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 3 the ring kernel with
