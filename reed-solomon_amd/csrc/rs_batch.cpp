@@ -236,6 +236,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         if ((rc = grow(&c->d_pout, c->pout_cap, size_t(nset * sch * out_stride) * 4))) return rc;
         if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
         if ((rc = grow(&c->d_mbits, c->mbits_cap, size_t(nset * sch) * mw * 4))) return rc;
+        // the prefetching solve (m8_ps_kernel 9) needs whole 1 KiB chunks and 32-bit input offsets
+        const bool pf = c->m8_ps_kernel == 9 && S % 1024 == 0 && uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull;
         hipStream_t sy = st;
         if (ovl) {
             if ((rc = overlap_objects(c))) return rc;
@@ -265,6 +267,10 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             pa.idx_stride = idx_stride;
             pa.mbits = static_cast<uint32_t*>(c->d_mbits) + size_t(set * sch) * mw;
             pa.mw = int32_t(mw);
+            if (pf) {  // packed records for k_apply_m8_pf, in the same buffer (a quarter of its stride)
+                pa.pidx8 = reinterpret_cast<uint8_t*>(pa.pidx);
+                pa.idx8_stride = idx_stride * 4;
+            }
             HIP_TRY(launch_plan_syn_m8(pa, cn, sy, c->syn_route));
             uint8_t* syn = static_cast<uint8_t*>(c->d_syn) + set * sch * per;
             if ((rc = syn_fixed_pass(c, base, stripe_stride, symbol_stride, syn, per, S, cn, c->d_ids + c0, pa.mbits,
@@ -295,7 +301,9 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ablate = c->m8_ps_ablate & 3;
 #endif
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
-            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
+            v.src_bytes = cn * per;
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, pf ? 9 : c->m8_ps_kernel == 9 ? 0 : c->m8_ps_kernel,
+                                       c->m8_ps_cpb));
             RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
@@ -336,7 +344,9 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.ps_in = in_stride;
         v.ps_out = out_stride;
         v.ps_idx = idx_stride;
-        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel, c->m8_ps_cpb));
+        // survivor plans carry the 64-dword records: the prefetching solve (9) does not take them
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel == 9 ? 0 : c->m8_ps_kernel,
+                                   c->m8_ps_cpb));
         RS_CHECKPOINT(c, nullptr, "per-stripe GF(256) survivor plans (apply_m8_ps)", uint64_t(cn), S);
     }
     c->last_kernel = "apply_m8_v1_ps";

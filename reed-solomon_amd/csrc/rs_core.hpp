@@ -313,7 +313,8 @@ struct rsg_codec {
     int m8_syn_overlap = 0;
     // option m8_ps_kernel: the per-stripe GF(256) solve's kernel: 0 k_apply_m8_v1 (LDS input ring), 1
     // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
-    // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input)
+    // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input), 9
+    // k_apply_m8_pf (no ring, every load issued a step or more ahead; packed records from the plan kernels)
     int m8_ps_kernel = 0;
     // option m8_ps_cpb: 1 KiB column chunks per workgroup of the per-stripe ring kernels (table setup once per
     // block, the next chunk's ring prologue in flight during this chunk's output stage)

@@ -1509,6 +1509,10 @@ __global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
 // Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Erased slots are
 // not zeroed: their old contents g enter the syndromes, the solve yields g + c for the erased information
 // slots, and the apply XORs that into g (V1Args::xor_dst). Erased repair slots only shift their own unknowns.
+// Byte of lookup L in a packed k_apply_m8_pf record (gen_asm.py ps8pf_kernel): L = 8 m + 2 k + d sits in byte
+// k of dword 2 m + d, so one s_lshr_b64 of a dword pair brings the next byte of both dwords down.
+__device__ __forceinline__ int pf_byte(int L) { return 4 * (2 * (L >> 3) + (L & 1)) + ((L & 7) >> 1); }
+
 // The stripe's pattern as bit words for the masked fixed pass: wave w's ballot covers slots 64w .. 64w + 63.
 __device__ __forceinline__ void plan_mask_words(const SynPlanArgs& a, int64_t s, int w, int lane, uint64_t bits) {
     if (!a.mbits || lane != 0) return;
@@ -1587,9 +1591,20 @@ __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
             for (int i = t - 1; i >= 0; --i) {
                 uint32_t b = 0;
                 if (q) b = a.g8[((uint32_t(a.logt[q]) + N - ld) % N) / 257u];
-                r0[size_t(i) * 64 + jj] = b & 15u;
-                r0[size_t(i) * 64 + 32 + jj] = b >> 4;
+                if (a.pidx8) {
+                    uint8_t* r8 = a.pidx8 + s * a.idx8_stride + (size_t(tile) * t + i) * 64;
+                    r8[pf_byte(jj)] = uint8_t(b & 15u);
+                    r8[pf_byte(32 + jj)] = uint8_t(b >> 4);
+                } else {
+                    r0[size_t(i) * 64 + jj] = b & 15u;
+                    r0[size_t(i) * 64 + 32 + jj] = b >> 4;
+                }
                 if (i > 0) q = cf[cur][i] ^ gmul(xp, q);
+            }
+        } else if (a.pidx8) {
+            for (int i = 0; i < t; ++i) {
+                uint8_t* r8 = a.pidx8 + s * a.idx8_stride + (size_t(tile) * t + i) * 64;
+                r8[pf_byte(jj)] = r8[pf_byte(32 + jj)] = 0;
             }
         } else {
             for (int i = 0; i < t; ++i) r0[size_t(i) * 64 + jj] = r0[size_t(i) * 64 + 32 + jj] = 0u;
@@ -1684,10 +1699,59 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
         for (int q = 0; q < R; ++q) {
             uint32_t b = 0;
             if (j < R) b = a.g8[((lp[q] + 2 * N - ld[j] - a.logt[px[j] ^ qx[q]]) % N) / 257u];
+            if (a.pidx8) {
+                uint8_t* r8 = a.pidx8 + s * a.idx8_stride + (size_t(tile) * R + q) * 64;
+                r8[pf_byte(jj)] = uint8_t(b & 15u);
+                r8[pf_byte(32 + jj)] = uint8_t(b >> 4);
+                continue;
+            }
             r0[size_t(q) * 64 + jj] = b & 15u;
             r0[size_t(q) * 64 + 32 + jj] = b >> 4;
         }
     }
+}
+
+// Per-stripe solve with every load issued ahead of its use (m8_ps_kernel 9). The ring kernel's waves spend
+// about half their cycles waiting (SMEM record halves fetched inside each step, a slot read per batch, one
+// barrier per 4 inputs; profiles/r4/ps8_route2.md); here each wave runs its own 256-byte column with no
+// barrier after the table copy, and the whole input loop is one asm statement (gen_asm.py ps8pf_kernel) in
+// which the next input's packed record (one SMEM load of 16 dwords) and coordinate-table reads are issued a
+// step ahead and the raw inputs four inputs ahead, so each step waits once for loads issued a step earlier.
+// Records are the plan kernels' packed form (SynPlanArgs::pidx8); same math as k_apply_m8_v1<0>, same
+// output stage. The coordinate tables must sit at LDS address 0: lt is the kernel's only LDS array.
+__global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
+    __shared__ uint32_t lt[2048];
+    if (uint32_t(reinterpret_cast<uintptr_t>(lt)) != 0u) __builtin_trap();  // folded away: lt is at 0
+    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    __syncthreads();
+    const int64_t bid = blockIdx.x;
+    const int64_t local = bid / a.nchunks;  // launch-local stripe
+    const int64_t stripe = RS_STRIPE(a.ids, local);
+    const int64_t chunk = bid - local * a.nchunks;
+    const int tile = blockIdx.y;
+    const int K = sload(a.ps_kr + 2 * local), R = sload(a.ps_kr + 2 * local + 1);
+    if (tile * 32 >= R || K <= 0) return;  // uniform over the block
+    const uint32_t col = uint32_t(chunk * 1024) + threadIdx.x * 4u;
+    const uint64_t sbase = uint64_t(reinterpret_cast<uintptr_t>(a.src + (a.src_local ? local : stripe) * a.src_stripe));
+    const uint32_t nrec = a.src_bytes > 0 && a.src_bytes < 0xFFFFFFFFll ? uint32_t(a.src_bytes) : 0xFFFFFFFFu;
+    const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, nrec, 0x20000u};
+    const uint32_t* rec = a.idx + local * a.ps_idx + size_t(tile) * size_t(K) * 16;
+    const int32_t* pin = a.in_idx + local * a.ps_in;
+    u32x16 a0, a1;
+    asm volatile(
+#include "gen/m8_idx_asm_ps8pf_kernel.inc"
+        : "=&{v[32:47]}"(a0), "=&{v[48:63]}"(a1)
+        : [rec] "s"(rec), [pin] "s"(pin), [nk] "s"(K), [sym] "s"(uint32_t(a.src_sym)), [rsrc] "s"(rsrc),
+          [col] "v"(col)
+        : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+          "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
+          "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75",
+          "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54",
+          "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
+          "s70", "s71", "s72", "s73", "s74", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85",
+          "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc", "memory");
+    m8_v1_store<1>(a, lt, a.dst + stripe * a.dst_stripe + chunk * 1024 + int64_t(threadIdx.x) * 4,
+                   a.out_idx + local * a.ps_out + tile * 32, min(32, R - tile * 32), a0, a1, a0, a1);
 }
 
 // Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
@@ -2322,8 +2386,16 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
+    if (kernel == 9) {  // prefetching solve: packed records, whole 1 KiB chunks only
+        if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
+        V1Args f = v;
+        f.nchunks = nbytes / 1024;
+        hipLaunchKernelGGL(k_apply_m8_pf, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        return hipGetLastError();
+    }
 #ifndef RS_AMD_DIAG
-    // release build: the LDS-ring solve (0, one column chunk per workgroup) and its one-table variant (3)
+    // release build: the LDS-ring solve (0, one column chunk per workgroup), its one-table variant (3) and the
+    // prefetching solve (9, above)
     if ((kernel != 0 && kernel != 3) || cpb > 1) return hipErrorInvalidValue;
 #else
     if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch

@@ -72,6 +72,11 @@ struct SynPlanArgs {
     int64_t in_stride, out_stride, idx_stride;
     uint32_t* mbits;       // [n_sel][mw] the pattern as bit words (slot i: bit i % 32 of word i / 32), for the
     int32_t mw;            // masked fixed pass (XJArgs::masks)
+    // non-null: records in k_apply_m8_pf's packed form instead ([n_sel][idx8_stride bytes], per (tile, input)
+    // 64 bytes: lookup L = 8 m + 2 k + d in byte k of dword 2 m + d; L < 32 the low nibble of output L, else
+    // the high nibble of output L - 32)
+    uint8_t* pidx8;
+    int64_t idx8_stride;
 };
 // kind 1: syndrome-route solves (k_plan_syn_m8); 2: re-encode solves (k_plan_reenc_m8)
 hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t st, int kind = 1);

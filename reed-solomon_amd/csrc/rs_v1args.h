@@ -55,6 +55,8 @@ struct V1Args {
     // diagnostic builds only (option m8_ps_ablate; timing ablations with wrong results): bit 1 skips the
     // coordinate-table copy into LDS, bit 2 stores the accumulators without the L^-1 conversion
     int32_t ablate;
+    // k_apply_m8_pf: bytes of the input buffer from src (the buffer resource's range; 0 = unchecked)
+    int64_t src_bytes;
 };
 
 // Stripe processed by launch-local stripe `s`: ids[s] when a stripe-id list is given.

@@ -34,15 +34,19 @@ baseprof)  # the production route twice, then its rocprofv3 kernel split
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 scripts/bench_patterns.py 4096 t32info device_plans_syndrome > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
   grep '^{' $D/prof.log; head -6 $D/prof/run_kernel_stats.csv | cut -c1-160 ;;
-kern)  # the production solve against diagnostic solve kernels $KERNS (m8_ps_kernel values), t32info and rand
+kern)  # the production solve against solve kernels $KERNS (m8_ps_kernel values; library $KLIB, default the
+       # diagnostic one), t32info and rand
   for rep in 1 2; do
     run rel_t32_$rep 4096 t32info device_plans_syndrome
     run rel_rand_$rep 4096 rand device_plans_syndrome
     for kern in ${KERNS:-1}; do
-      RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_t32_$rep 4096 t32info device_plans_syndrome
-      RS_AMD_LIB=$DIAG RS_PS8_KERNEL=$kern run k${kern}_rand_$rep 4096 rand device_plans_syndrome
+      RS_AMD_LIB=${KLIB:-$DIAG} RS_PS8_KERNEL=$kern run k${kern}_t32_$rep 4096 t32info device_plans_syndrome
+      RS_AMD_LIB=${KLIB:-$DIAG} RS_PS8_KERNEL=$kern run k${kern}_rand_$rep 4096 rand device_plans_syndrome
     done
   done ;;
+kprof)  # rocprofv3 kernel split with solve kernel $KERN (release library)
+  RS_PS8_KERNEL=${KERN:-9} timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 scripts/bench_patterns.py 4096 t32info device_plans_syndrome > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
+  grep '^{' $D/prof.log; head -6 $D/prof/run_kernel_stats.csv | cut -c1-160 ;;
 base)
   for rep in 1 2; do for pat in t32info rand; do run ${pat}_$rep 4096 $pat device_plans_syndrome; done; done ;;
 *) echo "unknown mode $MODE"; exit 2 ;;

@@ -671,13 +671,13 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, ps, overlap):
 
 
 SYN_ROUTE_SHAPES = [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40), (128, 32, 32768, 1030),
-                    (20, 9, 4096 + 520, 33)]
+                    (20, 9, 4096 + 520, 33), (100, 70, 4096, 50)]
 
 
 # release-library settings: the three routes, the LDS-ring solve with two or one nibble tables per input
 # (the A/B kernels, overlapped chunks and multi-chunk workgroups: tests/test_gpu_variants.py, diagnostic library)
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(2, 0, 0, 1), (1, 0, 0, 1), (0, 0, 0, 1), (2, 0, 3, 1), (1, 0, 3, 1),
-                                                (0, 0, 3, 1)])
+                                                (0, 0, 3, 1), (2, 0, 9, 1), (1, 0, 9, 1), (0, 0, 9, 1)])
 @pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd, k, r, S, n, route, ovl, kern, cpb)
@@ -692,7 +692,9 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb):
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
     kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
-    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>). cpb > 1: the
+    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>); 9: the prefetching
+    solve k_apply_m8_pf on packed records (route 0 keeps the ring kernel: survivor plans are not packed;
+    r = 70 gives three output tiles and up to 70 inputs per stripe). cpb > 1: the
     ring kernel walks that many 1 KiB column chunks per workgroup (k_apply_m8_v1<6>; 64 > chunks per symbol). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
     ends in a partial column chunk."""
     if route and S % 2048:

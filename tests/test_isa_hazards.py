@@ -94,7 +94,7 @@ DIAG_ONLY = ("k_apply_m8ILi", "k_apply_m8_lds", "k_apply_m8_ps_w", "k_apply_m8_i
              "k_apply_m8_v1ILi1E", "k_apply_m8_v1ILi3E", "k_apply_m8_v1ILi4E", "k_apply_m8_v1ILi5E", "k_apply_m8_v1ILi6E",
              "k_apply_m16_v1ILi1E")
 # every production kernel (the release library carries exactly these)
-PRODUCTION = ("k_apply_m8_v1ILi0E", "k_apply_m8_v1ILi2E", "k_apply_m8_idxILi0ELi4E", "k_apply_m8_ps_tail", "k_xor_slices",
+PRODUCTION = ("k_apply_m8_v1ILi0E", "k_apply_m8_v1ILi2E", "k_apply_m8_idxILi0ELi4E", "k_apply_m8_ps_tail", "k_apply_m8_pf", "k_xor_slices",
               "k_apply_m16ILi16E", "k_apply_m16ILi32E", "k_apply_m16ILi64E", "k_apply_m16_v1ILi0E", "k_cs16E", "k_cs16tE",
               "k_bs16E", "k_cs16_goff", "k_plan_m8", "k_plan_syn_m8", "k_plan_reenc_m8", "k_plan16_sums", "k_plan16_fill",
               "k_plan16_ps", "k_plan16_ps_rec", "k_plan16_reenc", "k_plan16_reenc_logs", "k_plan16_reenc_rec",

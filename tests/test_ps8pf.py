@@ -1,0 +1,105 @@
+"""CPU checks of the prefetching per-stripe GF(256) solve loop (gen_asm.py ps8pf_kernel, k_apply_m8_pf).
+
+The generated asm statement runs in the instruction emulator (tests/xj_emu.py) with scalar-memory and LDS
+reads landing only at the waits that retire them, so a register named while its load is in flight fails
+the test, as does a wrong wait count on the raw-input ring. The accumulators it leaves are compared with a
+numpy model of the V = 1 step (coordinate lookup, gamma multiples, nibble tables, lookups), for input counts
+that end the loop at every step position and past the slot-block and record-bank turnovers.
+"""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(__file__))
+from xj_emu import Memory, Wave  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GEN = os.path.join(HERE, "..", "reed-solomon_amd", "csrc", "gen_asm.py")
+
+
+@pytest.fixture(scope="module")
+def pf_lines(tmp_path_factory):
+    out = tmp_path_factory.mktemp("pf") / "pf.inc"
+    subprocess.check_call([sys.executable, GEN, str(out), "ps8pf_kernel"])
+    lines = []
+    for ln in open(out):
+        m = re.match(r'^"(.*)\\n\\t"$', ln.strip())
+        if m:
+            lines.append(m.group(1))
+    return lines
+
+
+def pf_byte(L):
+    return 4 * (2 * (L >> 3) + (L & 1)) + ((L & 7) >> 1)
+
+
+def xt8(m):
+    return (((m << 1) & 0xFEFEFEFE) ^ (((m >> 7) & 0x01010101) * 0x1D)) & 0xFFFFFFFF
+
+
+def model(raw, lt, lo, hi):
+    """raw [K][64] input dwords, lt [1024] coordinate tables, lo / hi [K][32] nibble indices -> acc [32][64]."""
+    acc = np.zeros((32, 64), np.uint64)
+    for i in range(raw.shape[0]):
+        x = raw[i].astype(np.uint64)
+        y = lt[x & 255] ^ lt[256 + ((x >> 8) & 255)] ^ lt[512 + ((x >> 16) & 255)] ^ lt[768 + (x >> 24)]
+        m = [y]
+        for _ in range(7):
+            m.append(xt8(m[-1]))
+        tl = [np.zeros(64, np.uint64) for _ in range(16)]
+        th = [np.zeros(64, np.uint64) for _ in range(16)]
+        for e in range(16):
+            for b in range(4):
+                if (e >> b) & 1:
+                    tl[e] = tl[e] ^ m[b]
+                    th[e] = th[e] ^ m[4 + b]
+        for p in range(32):
+            acc[p] ^= tl[lo[i, p]] ^ th[hi[i, p]]
+    return acc.astype(np.uint32)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 7, 8, 9, 12, 13, 16, 17, 31, 32, 40])
+def test_ps8pf_loop_matches_model(pf_lines, K):
+    rng = np.random.default_rng(1000 + K)
+    S = 4096                 # input symbol stride (bytes)
+    nslots = 48
+    col = 1024 + 256         # chunk 1, wave 1
+    src_base, rec_base, pin_base = 0, nslots * S, nslots * S + 64 * 1024
+    mem = Memory(pin_base + 4 * (K + 64) + 64)
+    mem.b[:nslots * S] = rng.integers(0, 256, nslots * S, dtype=np.uint8)
+    slots = rng.permutation(nslots)[:K].astype(np.uint32)
+    pin = np.zeros(K + 64, np.uint32)  # zero padding past K (the plan kernels write in_stride entries)
+    pin[:K] = slots
+    mem.b[pin_base:pin_base + 4 * pin.size] = pin.view(np.uint8)
+    lo = rng.integers(0, 16, (K, 32))
+    hi = rng.integers(0, 16, (K, 32))
+    rec = np.zeros((K + 1) * 64, np.uint8)  # one record of padding: the loop prefetches record K
+    for i in range(K):
+        for p in range(32):
+            rec[i * 64 + pf_byte(p)] = lo[i, p]
+            rec[i * 64 + pf_byte(32 + p)] = hi[i, p]
+    rec[K * 64:] = rng.integers(0, 256, 64, dtype=np.uint8)
+    mem.b[rec_base:rec_base + rec.size] = rec
+    lt = rng.integers(0, 1 << 32, 1024, dtype=np.uint64)
+    lds = np.zeros(8192, np.uint8)
+    lds[:4096] = lt.astype("<u4").view(np.uint8)
+    ops = dict(col=(col + 4 * np.arange(64)).astype(np.uint32), rec=rec_base, pin=pin_base, nk=K, sym=S,
+               rsrc=(src_base, nslots * S))
+    w = Wave(mem, ops, lgkm=True)
+    w.lds = lds
+    w.run(pf_lines, [])
+    assert not w.vm and not w.lg, "loads left in flight at the end of the statement"
+    raw = np.stack([mem.load32(np.uint64(src_base + int(s) * S + col) + 4 * np.arange(64, dtype=np.uint64))
+                    for s in slots])
+    want = model(raw, lt, lo, hi)
+    got = w.v[32:64]
+    assert np.array_equal(got, want)
+
+
+def test_ps8pf_record_bytes_cover_each_lookup_once():
+    pos = sorted(pf_byte(L) for L in range(64))
+    assert pos == list(range(64))

@@ -33,8 +33,13 @@ def _vreg(tok):
 
 
 class Wave:
-    def __init__(self, mem, operands):
+    def __init__(self, mem, operands, lgkm=False):
         self.v = np.zeros((256, 64), np.uint32)
+        # lgkm=True: scalar-memory and LDS reads land only when an s_waitcnt lgkmcnt retires them (SMEM returns
+        # out of order, so only lgkmcnt(0) retires it; LDS reads retire in order when no SMEM is pending); an
+        # instruction that names a register with a read still in flight raises
+        self.lgkm = lgkm
+        self.lg = []  # [("s", first sgpr, words) | ("v", vgpr, data)]
         self.s = np.zeros(128, np.uint64)
         self.scc = 0
         self.m0 = 0
@@ -71,11 +76,15 @@ class Wave:
         self.v[_vreg(tok)] = np.asarray(x, dtype=np.uint64).astype(np.uint32) if np.ndim(x) else np.uint32(x)
 
     def pair(self, tok):
+        if tok.startswith("%["):  # a 64-bit SGPR-pair operand
+            return int(self.ops[tok[2:-1]])
         m = re.match(r"s\[(\d+):(\d+)\]", tok)
         lo, hi = int(m.group(1)), int(m.group(2))
         return int(self.s[lo]) | (int(self.s[hi]) << 32)
 
     def vsharp(self, tok):
+        if tok.startswith("%["):  # a V# operand: (base, num_records)
+            return int(self.ops[tok[2:-1]][0])
         m = re.match(r"s\[(\d+):(\d+)\]", tok)
         lo = int(m.group(1))
         return int(self.s[lo]) | ((int(self.s[lo + 1]) & 0xFFFF) << 32)
@@ -88,6 +97,33 @@ class Wave:
                 self.lds[r[1]] = data
             elif r is not None:
                 self.v[r] = data
+
+    def retire_lgkm(self, n):
+        """s_waitcnt lgkmcnt(n) under the lgkm model."""
+        if n == 0 or not any(k == "s" for k, _, _ in self.lg):
+            while len(self.lg) > n:
+                kind, r, data = self.lg.pop(0)
+                if kind == "s":
+                    for w, x in enumerate(data):
+                        self.s[r + w] = np.uint64(int(x))
+                else:
+                    self.v[r] = data
+
+    def check_lgkm(self, ln):
+        if not self.lg:
+            return
+        busy_v = {r for k, r, _ in self.lg if k == "v"}
+        busy_s = set()
+        for k, r, data in self.lg:
+            if k == "s":
+                busy_s.update(range(r, r + len(data)))
+        for tok in re.findall(r"\bv(\d+)\b", ln):
+            assert int(tok) not in busy_v, f"v{tok} named while its LDS read is in flight: {ln}"
+        names = {int(t) for t in re.findall(r"\bs(\d+)\b", ln)}
+        for lo, hi in re.findall(r"s\[(\d+):(\d+)\]", ln):
+            names.update(range(int(lo), int(hi) + 1))
+        hit = names & busy_s
+        assert not hit, f"s{sorted(hit)[0]} named while its scalar load is in flight: {ln}"
 
     def check_vgprs(self, ln):
         busy = {r for r, _ in self.vm if isinstance(r, int)}
@@ -112,8 +148,13 @@ class Wave:
                 m = re.search(r"vmcnt\((\d+)\)", rest)
                 if m:
                     self.retire(int(m.group(1)))
+                m = re.search(r"lgkmcnt\((\d+)\)", rest)
+                if m and self.lgkm:
+                    self.retire_lgkm(int(m.group(1)))
                 continue
             self.check_vgprs(ln)
+            if self.lgkm:
+                self.check_lgkm(ln)
             if op == "s_setpc_b64":
                 self.setpc = a[0]
                 return
@@ -166,6 +207,9 @@ class Wave:
                 assert int(m.group(2)) - lo + 1 == cnt, ln
                 addr = self.pair(a[1]) + int(a[2], 0)
                 words = self.mem.load32(np.uint64(addr) + 4 * np.arange(cnt, dtype=np.uint64))
+                if self.lgkm:
+                    self.lg.append(("s", lo, words))
+                    continue
                 for w in range(cnt):
                     self.s[lo + w] = np.uint64(int(words[w]))
                 continue
@@ -291,11 +335,15 @@ class Wave:
                 idx = addr[:, None] + np.arange(4)[None, :]
                 self.lds[idx.reshape(-1)] = np.ascontiguousarray(self.val(a1), dtype="<u4").view(np.uint8)
             elif op == "ds_read_b32":
-                base, off = a[1].split()
-                assert off.startswith("offset:"), ln
-                addr = self.val(base).astype(np.int64) + int(off.split(":")[1])
+                base, _, off = a[1].partition(" ")
+                assert not off or off.startswith("offset:"), ln
+                addr = self.val(base).astype(np.int64) + (int(off.split(":")[1]) if off else 0)
                 idx = addr[:, None] + np.arange(4)[None, :]
-                self.vset(a[0], self.lds[idx].copy().view("<u4").reshape(-1))
+                data = self.lds[idx].copy().view("<u4").reshape(-1)
+                if self.lgkm:
+                    self.lg.append(("v", _vreg(a[0]), data))
+                else:
+                    self.vset(a[0], data)
             elif op in ("ds_read_u16", "ds_read_u16_d16_hi"):
                 # gfx950 (SRAM-ECC): d16 loads do not preserve the other half -- it is zeroed
                 addr = self.val(a[1]).astype(np.int64)
@@ -306,7 +354,8 @@ class Wave:
                 voff = self.val(a[1]).astype(np.uint64)
                 addr = self.vsharp(a[2]) + self.val(a[3].split()[0]) + voff
                 # raw buffer (stride 0) range check on the VGPR offset: out of range loads return 0
-                nrec = int(self.s[int(re.match(r"s\[(\d+):", a[2]).group(1)) + 2])
+                nrec = (int(self.ops[a[2][2:-1]][1]) if a[2].startswith("%[")
+                        else int(self.s[int(re.match(r"s\[(\d+):", a[2]).group(1)) + 2]))
                 inb = voff < np.uint64(nrec)
                 data = self.mem.load32(np.where(inb, addr, np.uint64(0)))
                 self.vm.append((_vreg(a[0]), np.where(inb, data, np.uint32(0)).astype(np.uint32)))
