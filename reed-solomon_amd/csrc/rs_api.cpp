@@ -163,6 +163,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->ps_chunk = value;
         return 0;
     }
+    if (!std::strcmp(name, "m8_syn_scratch_mib")) {  // GF(256) per-stripe route: fixed-pass scratch per chunk
+        if (value < 1 || value > 4095) return RS_ERR_INVALID;
+        c->syn_scratch_mib = value;
+        return 0;
+    }
     if (!std::strcmp(name, "m16_ps_rec_mib")) {  // its record bytes per chunk
         if (value < 1 || value > 4096) return RS_ERR_INVALID;
         c->ps_rec_mib = value;
@@ -176,12 +181,22 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
-        if (value < 0 || value > 9) return RS_ERR_INVALID;
-#ifndef RS_AMD_DIAG  // 0 / 3: the ring kernels; 9: the prefetching kernel; 1, 2, 4, 5: A/B kernels; 6, 8: ablations
-                     // (wrong results); 7: stamps
-        if (value != 0 && value != 3 && value != 9) return RS_ERR_INVALID;
+        if (value < 0 || value > 10) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG  // 0 / 3: the ring kernels; 9 / 10: the prefetching kernels; 1, 2, 4, 5: A/B kernels; 6, 8:
+                     // ablations (wrong results); 7: stamps
+        if (value != 0 && value != 3 && value != 9 && value != 10) return RS_ERR_INVALID;
 #endif
         c->m8_ps_kernel = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m8_syn_masked")) {  // per-stripe fixed pass masked (1) or plain + XOR solve (0)
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        if (int(value) != c->m8_syn_masked) {
+            if (c->syn && c->syn->xj) (void)hipDeviceSynchronize();  // the old pass may still be queued
+            c->syn.reset();  // rebuilt in the other form at the next call
+            c->syn_failed = false;
+        }
+        c->m8_syn_masked = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_cpb")) {  // per-stripe GF(256) solve: column chunks per workgroup

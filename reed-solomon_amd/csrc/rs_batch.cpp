@@ -87,8 +87,8 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
             c->syn_failed = true;
             return false;
         }
-        // the masked form: each stripe's erased slots read as zero (XJArgs::masks)
-        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, true) || !p->xj) {
+        // the masked form (default): each stripe's erased slots read as zero (XJArgs::masks)
+        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, c->m8_syn_masked != 0) || !p->xj) {
             std::fprintf(stderr, "librs_amd: syndrome XOR kernel unavailable; per-stripe survivor plans\n");
             c->syn_failed = true;
             return false;
@@ -115,13 +115,15 @@ static int syn_fixed_pass(rsg_codec_t* c, const uint8_t* base, int64_t stripe_st
     x.dst_sym = int32_t(S);
     x.ids = d_ids;
     x.dst_local = 1u;
-    x.mask_words = mw;
-    x.masks = d_mbits;
-    x.zero = static_cast<const uint8_t*>(c->d_zero);
+    if (p.xj->masked) {
+        x.mask_words = mw;
+        x.masks = d_mbits;
+        x.zero = static_cast<const uint8_t*>(c->d_zero);
+    }
     c->last_kernel = p.xj->name;
     const int rc = xj_launch(*p.xj, x, cn, int64_t(S / 2048) * (2048 / kXjChunk), st);
     const int rc2 = p.note_use(st);
-    if (!rc && !rc2) RS_CHECKPOINT(c, &p, "per-stripe fixed pass (masked rs_xj)", uint64_t(cn), S);
+    if (!rc && !rc2) RS_CHECKPOINT(c, &p, "per-stripe fixed pass (rs_xj)", uint64_t(cn), S);
     return rc ? rc : rc2;
 }
 
@@ -226,7 +228,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         const uint16_t* expt = nullptr;
         if ((rc = plan_tables(c->device, &logt, &g8, &expt))) return rc;
         const int64_t per = int64_t(c->r) * int64_t(S);
-        int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (int64_t(1) << 30) / per));
+        int64_t sch = std::max<int64_t>(1, std::min<int64_t>(chunk, (c->syn_scratch_mib << 20) / per));
         const bool ovl = c->m8_syn_overlap && nsel > sch / 2;
         if (ovl) sch = std::max<int64_t>(1, std::min<int64_t>(sch, (nsel + 3) / 4));  // at least 4 chunks
         const int nset = ovl ? 2 : 1;
@@ -237,7 +239,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
         if ((rc = grow(&c->d_mbits, c->mbits_cap, size_t(nset * sch) * mw * 4))) return rc;
         // the prefetching solve (m8_ps_kernel 9) needs whole 1 KiB chunks and 32-bit input offsets
-        const bool pf = c->m8_ps_kernel == 9 && S % 1024 == 0 && uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull;
+        const bool pf = (c->m8_ps_kernel == 9 || c->m8_ps_kernel == 10) && S % 1024 == 0 &&
+                        uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull;
         hipStream_t sy = st;
         if (ovl) {
             if ((rc = overlap_objects(c))) return rc;
@@ -296,14 +299,16 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             v.ps_in = in_stride;
             v.ps_out = out_stride;
             v.ps_idx = idx_stride;
-            v.xor_dst = 0;  // the masked fixed pass read the erased slots as zero: the solve yields them
+            // masked fixed pass: the erased slots read as zero, the solve yields them; plain pass: the solve yields
+            // g + c for old contents g, XORed into the slots
+            v.xor_dst = c->syn->xj->masked ? 0 : 1;
 #ifdef RS_AMD_DIAG
             v.ablate = c->m8_ps_ablate & 3;
 #endif
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
             v.src_bytes = cn * per;
-            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, pf ? 9 : c->m8_ps_kernel == 9 ? 0 : c->m8_ps_kernel,
-                                       c->m8_ps_cpb));
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st,
+                                       pf ? c->m8_ps_kernel : c->m8_ps_kernel >= 9 ? 0 : c->m8_ps_kernel, c->m8_ps_cpb));
             RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
@@ -345,7 +350,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         v.ps_out = out_stride;
         v.ps_idx = idx_stride;
         // survivor plans carry the 64-dword records: the prefetching solve (9) does not take them
-        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel == 9 ? 0 : c->m8_ps_kernel,
+        HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, c->m8_ps_kernel >= 9 ? 0 : c->m8_ps_kernel,
                                    c->m8_ps_cpb));
         RS_CHECKPOINT(c, nullptr, "per-stripe GF(256) survivor plans (apply_m8_ps)", uint64_t(cn), S);
     }

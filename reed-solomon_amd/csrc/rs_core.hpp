@@ -316,6 +316,13 @@ struct rsg_codec {
     // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input), 9
     // k_apply_m8_pf (no ring, every load issued a step or more ahead; packed records from the plan kernels)
     int m8_ps_kernel = 0;
+    // option m8_syn_masked: 1 (default) the per-stripe fixed pass reads each stripe's erased slots as zero (masked
+    // rs_xj) and the solve stores the erased symbols; 0 the plain pass over the slots as they are and a solve
+    // that XORs its result into them (one old-value load per output)
+    int m8_syn_masked = 1;
+    // option m8_syn_scratch_mib: fixed-pass output scratch of the GF(256) per-stripe route per chunk of stripes
+    // (r x S bytes per stripe; the chunk count sets the launch count)
+    int64_t syn_scratch_mib = 1024;
     // option m8_ps_cpb: 1 KiB column chunks per workgroup of the per-stripe ring kernels (table setup once per
     // block, the next chunk's ring prologue in flight during this chunk's output stage)
     int m8_ps_cpb = 1;

@@ -144,11 +144,11 @@ __device__ __forceinline__ uint32_t gmul_g4(uint32_t v) {
 
 // Output p of the tile in GF(2^16) words: accumulator a0[p] / a1[p - 16] (GF(256)^2 coordinates) through
 // L^-1; NB = 2 adds gamma^4 times b0[p] / b1[p - 16] through the G4 table.
-template <int NB>
+template <int NB, int G4 = V1H_G4>
 __device__ __forceinline__ uint32_t m8_v1_out(const uint32_t* lt, int p, const u32x16& a0, const u32x16& a1,
                                               const u32x16& b0, const u32x16& b1) {
     uint32_t w = lds_lookup4(lt + 1024, p < 16 ? a0[p & 15] : a1[p & 15]);
-    if constexpr (NB == 2) w ^= lds_lookup4(lt + V1H_G4, p < 16 ? b0[p & 15] : b1[p & 15]);
+    if constexpr (NB == 2) w ^= lds_lookup4(lt + G4, p < 16 ? b0[p & 15] : b1[p & 15]);
     return w;
 }
 
@@ -170,7 +170,7 @@ __device__ __forceinline__ void sload32(const int32_t* out, i32x16s& o0, i32x16s
 // The V = 1 kernels' outputs: row p of the tile back to GF(2^16) words (m8_v1_out) and stored to
 // dst + out[p] * dst_sym, or XORed into it (V1Args::xor_dst: every old value is loaded first, so the
 // wave waits on one round of loads while it converts its outputs).
-template <int NB, int LBX = 0>
+template <int NB, int LBX = 0, int G4 = V1H_G4>
 __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt, uint8_t* dst, const int32_t* out,
                                             int rows, const u32x16& a0, const u32x16& a1, const u32x16& b0,
                                             const u32x16& b1) {
@@ -198,7 +198,7 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
             for (int q = 0; q < LB; ++q) old[q] = p0 + q < rows ? *at(p0 + q) : 0u;
 #pragma unroll
             for (int q = 0; q < LB; ++q)
-                if (p0 + q < rows) *at(p0 + q) = m8_v1_out<NB>(lt, p0 + q, a0, a1, b0, b1) ^ old[q];
+                if (p0 + q < rows) *at(p0 + q) = m8_v1_out<NB, G4>(lt, p0 + q, a0, a1, b0, b1) ^ old[q];
         }
         return;
     }
@@ -210,7 +210,7 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
     for (int p0 = 24; p0 >= 0; p0 -= 8) {
         uint32_t w[8];
 #pragma unroll
-        for (int q = 7; q >= 0; --q) w[q] = m8_v1_out<NB>(lt, p0 + q, a0, a1, b0, b1);
+        for (int q = 7; q >= 0; --q) w[q] = m8_v1_out<NB, G4>(lt, p0 + q, a0, a1, b0, b1);
 #pragma unroll
         for (int q = 7; q >= 0; --q) {
             const int32_t sl = p0 + q < rows ? slot(p0 + q) : slast;

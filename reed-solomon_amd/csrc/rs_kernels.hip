@@ -1719,10 +1719,19 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // step ahead and the raw inputs four inputs ahead, so each step waits once for loads issued a step earlier.
 // Records are the plan kernels' packed form (SynPlanArgs::pidx8); same math as k_apply_m8_v1<0>, same
 // output stage. The coordinate tables must sit at LDS address 0: lt is the kernel's only LDS array.
+// NB = 1: two nibble tables per input (gen_asm.py ps8pf_kernel, 78 VGPRs, 6 waves per SIMD); NB = 2: one table
+// over y gamma^0..3 with the high-nibble lookups in a second accumulator set (ps8pf1_kernel: 4 multiples and a
+// table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
+template <int NB>
 __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
-    __shared__ uint32_t lt[2048];
+    constexpr int G4 = 2048;  // NB = 2: gamma^4 folded into L^-1 (m8_v1_out), after the coordinate tables
+    __shared__ uint32_t lt[NB == 2 ? 3072 : 2048];
     if (uint32_t(reinterpret_cast<uintptr_t>(lt)) != 0u) __builtin_trap();  // folded away: lt is at 0
     for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    if constexpr (NB == 2) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 1024; i += 256) lt[G4 + i] = lt[1024 + (i & ~255) + gmul_g4(i & 255)];
+    }
     __syncthreads();
     const int64_t bid = blockIdx.x;
     const int64_t local = bid / a.nchunks;  // launch-local stripe
@@ -1737,21 +1746,39 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
     const u32x4s rsrc = {uint32_t(sbase), uint32_t(sbase >> 32) & 0xFFFFu, nrec, 0x20000u};
     const uint32_t* rec = a.idx + local * a.ps_idx + size_t(tile) * size_t(K) * 16;
     const int32_t* pin = a.in_idx + local * a.ps_in;
-    u32x16 a0, a1;
-    asm volatile(
+    // the output stage's operands are formed after the loop (nothing of the kernel's own lives across it)
+#define RS_PF_DST a.dst + stripe * a.dst_stripe + chunk * 1024 + int64_t(threadIdx.x) * 4, \
+                  a.out_idx + local * a.ps_out + tile * 32, min(32, R - tile * 32)
+#define RS_PF_IN                                                                                                  \
+    [rec] "s"(rec), [pin] "s"(pin), [nk] "s"(K), [sym] "s"(uint32_t(a.src_sym)), [rsrc] "s"(rsrc), [col] "v"(col)
+#define RS_PF_SGPRS                                                                                               \
+    "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55",   \
+        "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", \
+        "s72", "s73", "s74", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", \
+        "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc", "memory"
+    if constexpr (NB == 1) {
+        u32x16 a0, a1;
+        asm volatile(
 #include "gen/m8_idx_asm_ps8pf_kernel.inc"
-        : "=&{v[32:47]}"(a0), "=&{v[48:63]}"(a1)
-        : [rec] "s"(rec), [pin] "s"(pin), [nk] "s"(K), [sym] "s"(uint32_t(a.src_sym)), [rsrc] "s"(rsrc),
-          [col] "v"(col)
-        : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
-          "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
-          "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75",
-          "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54",
-          "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69",
-          "s70", "s71", "s72", "s73", "s74", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85",
-          "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "scc", "memory");
-    m8_v1_store<1>(a, lt, a.dst + stripe * a.dst_stripe + chunk * 1024 + int64_t(threadIdx.x) * 4,
-                   a.out_idx + local * a.ps_out + tile * 32, min(32, R - tile * 32), a0, a1, a0, a1);
+            : "=&{v[32:47]}"(a0), "=&{v[48:63]}"(a1)
+            : RS_PF_IN
+            : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+              "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
+              "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", RS_PF_SGPRS);
+        m8_v1_store<1>(a, lt, RS_PF_DST, a0, a1, a0, a1);
+    } else {
+        u32x16 a0, a1, b0, b1;
+        asm volatile(
+#include "gen/m8_idx_asm_ps8pf1_kernel.inc"
+            : "=&{v[16:31]}"(a0), "=&{v[32:47]}"(a1), "=&{v[48:63]}"(b0), "=&{v[64:79]}"(b1)
+            : RS_PF_IN
+            : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+              "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", RS_PF_SGPRS);
+        m8_v1_store<2, 0, G4>(a, lt, RS_PF_DST, a0, a1, b0, b1);
+    }
+#undef RS_PF_DST
+#undef RS_PF_IN
+#undef RS_PF_SGPRS
 }
 
 // Columns [col0, nbytes) (< 1 KiB) of every stripe under per-stripe plans: one lane per dword,
@@ -2386,16 +2413,20 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
-    if (kernel == 9) {  // prefetching solve: packed records, whole 1 KiB chunks only
+    if (kernel == 9 || kernel == 10) {  // prefetching solves (two / one nibble tables): packed records, whole
+                                        // 1 KiB chunks only
         if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
         V1Args f = v;
         f.nchunks = nbytes / 1024;
-        hipLaunchKernelGGL(k_apply_m8_pf, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        if (kernel == 9)
+            hipLaunchKernelGGL(k_apply_m8_pf<1>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        else
+            hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         return hipGetLastError();
     }
 #ifndef RS_AMD_DIAG
     // release build: the LDS-ring solve (0, one column chunk per workgroup), its one-table variant (3) and the
-    // prefetching solve (9, above)
+    // prefetching solves (9 / 10, above)
     if ((kernel != 0 && kernel != 3) || cpb > 1) return hipErrorInvalidValue;
 #else
     if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch

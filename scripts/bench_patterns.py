@@ -70,6 +70,10 @@ if os.environ.get("RS_PS8_ROUTE"):  # A/B of the fixed pass (option syn_route: 1
     syn.set_option("syn_route", int(os.environ["RS_PS8_ROUTE"]))
 if os.environ.get("RS_PS8_KERNEL"):  # A/B of the per-stripe solve kernel (option m8_ps_kernel)
     syn.set_option("m8_ps_kernel", int(os.environ["RS_PS8_KERNEL"]))
+if os.environ.get("RS_PS8_MASKED"):  # A/B of the masked fixed pass (option m8_syn_masked)
+    syn.set_option("m8_syn_masked", int(os.environ["RS_PS8_MASKED"]))
+if os.environ.get("RS_PS8_SCRATCH"):  # A/B of the fixed-pass scratch per chunk (option m8_syn_scratch_mib)
+    syn.set_option("m8_syn_scratch_mib", int(os.environ["RS_PS8_SCRATCH"]))
 if os.environ.get("RS_PS8_ABLATE"):  # timing ablations of the solve (diagnostic library, option m8_ps_ablate)
     syn.set_option("m8_ps_ablate", int(os.environ["RS_PS8_ABLATE"]))
 if os.environ.get("RS_PS8_CPB"):  # A/B of column chunks per workgroup of that kernel (option m8_ps_cpb)

@@ -8,6 +8,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 D=gpurun_out/${PS8:-ps8pmc}
 mkdir -p $D
+[ -n "${KERN:-}" ] && export RS_PS8_KERNEL=$KERN  # the per-stripe solve kernel (m8_ps_kernel)
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA" \
            "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
@@ -17,4 +18,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   rc=$?; echo "pass $i rc=$rc"
   case $rc in 0) ;; *) tail -3 $D/p$i.log; exit $rc;; esac
 done
-for k in "k_apply_m8_v1<0>" k_apply_m8_ps_w rs_xj_ k_plan_; do echo "== $k"; python3 scripts/pmc_summary.py $D "$k"; done
+for k in "k_apply_m8_v1<0>" k_apply_m8_pf k_apply_m8_ps_w rs_xj_ k_plan_; do echo "== $k"; python3 scripts/pmc_summary.py $D "$k"; done

@@ -671,19 +671,29 @@ def test_decode_batch_m16_per_stripe_route_chunks(chunk, ps, overlap):
 
 
 SYN_ROUTE_SHAPES = [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40), (128, 32, 32768, 1030),
-                    (20, 9, 4096 + 520, 33), (100, 70, 4096, 50)]
+                    (20, 9, 4096 + 520, 33), (60, 40, 4096, 50)]
 
 
 # release-library settings: the three routes, the LDS-ring solve with two or one nibble tables per input
 # (the A/B kernels, overlapped chunks and multi-chunk workgroups: tests/test_gpu_variants.py, diagnostic library)
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(2, 0, 0, 1), (1, 0, 0, 1), (0, 0, 0, 1), (2, 0, 3, 1), (1, 0, 3, 1),
-                                                (0, 0, 3, 1), (2, 0, 9, 1), (1, 0, 9, 1), (0, 0, 9, 1)])
+                                                (0, 0, 3, 1), (2, 0, 9, 1), (1, 0, 9, 1), (0, 0, 9, 1), (2, 0, 10, 1),
+                                                (1, 0, 10, 1)])
 @pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd, k, r, S, n, route, ovl, kern, cpb)
 
 
-def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb):
+@pytest.mark.parametrize("kern", [0, 10])
+@pytest.mark.parametrize("route", [1, 2])
+@pytest.mark.parametrize("k,r,S,n", [SYN_ROUTE_SHAPES[0], SYN_ROUTE_SHAPES[2], SYN_ROUTE_SHAPES[5]])
+def test_decode_batch_syndrome_route_unmasked(k, r, S, n, route, kern):
+    """Option m8_syn_masked 0: the plain fixed pass over the slots as they are (garbage in the erased ones) and
+    a solve that XORs g + c into the erased information slots."""
+    syndrome_route_case(rs_amd, k, r, S, n, route, 0, kern, 1, masked=0)
+
+
+def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
     the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
     first; route 2: the re-encode differences [G | I] of every slot, then a t_info x t_info Cauchy-inverse
@@ -692,9 +702,9 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb):
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
     kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
-    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>); 9: the prefetching
-    solve k_apply_m8_pf on packed records (route 0 keeps the ring kernel: survivor plans are not packed;
-    r = 70 gives three output tiles and up to 70 inputs per stripe). cpb > 1: the
+    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>); 9 / 10: the
+    prefetching solve k_apply_m8_pf<1> / <2> (two / one nibble tables) on packed records (route 0 keeps the ring kernel: survivor plans are not packed;
+    r = 40 gives two output tiles and up to 40 inputs per stripe). cpb > 1: the
     ring kernel walks that many 1 KiB column chunks per workgroup (k_apply_m8_v1<6>; 64 > chunks per symbol). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
     ends in a partial column chunk."""
     if route and S % 2048:
@@ -707,6 +717,7 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb):
     codec.set_option("m8_syn_overlap", ovl)
     codec.set_option("m8_ps_kernel", kern)  # 1: the ring-free per-stripe solve kernel (k_apply_m8_ps_w)
     codec.set_option("m8_ps_cpb", cpb)
+    codec.set_option("m8_syn_masked", masked)
     codec.encode(dev)
     pats = np.zeros((n, k + r), bool)
     for s in range(n):

@@ -21,16 +21,25 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GEN = os.path.join(HERE, "..", "reed-solomon_amd", "csrc", "gen_asm.py")
 
 
-@pytest.fixture(scope="module")
-def pf_lines(tmp_path_factory):
-    out = tmp_path_factory.mktemp("pf") / "pf.inc"
-    subprocess.check_call([sys.executable, GEN, str(out), "ps8pf_kernel"])
+def gen_lines(variant, tmp):
+    out = tmp / f"{variant}.inc"
+    subprocess.check_call([sys.executable, GEN, str(out), variant])
     lines = []
     for ln in open(out):
         m = re.match(r'^"(.*)\\n\\t"$', ln.strip())
         if m:
             lines.append(m.group(1))
     return lines
+
+
+@pytest.fixture(scope="module")
+def pf_lines(tmp_path_factory):
+    return gen_lines("ps8pf_kernel", tmp_path_factory.mktemp("pf"))
+
+
+@pytest.fixture(scope="module")
+def pf1_lines(tmp_path_factory):
+    return gen_lines("ps8pf1_kernel", tmp_path_factory.mktemp("pf1"))
 
 
 def pf_byte(L):
@@ -41,9 +50,10 @@ def xt8(m):
     return (((m << 1) & 0xFEFEFEFE) ^ (((m >> 7) & 0x01010101) * 0x1D)) & 0xFFFFFFFF
 
 
-def model(raw, lt, lo, hi):
-    """raw [K][64] input dwords, lt [1024] coordinate tables, lo / hi [K][32] nibble indices -> acc [32][64]."""
-    acc = np.zeros((32, 64), np.uint64)
+def model(raw, lt, lo, hi, one_table=False):
+    """raw [K][64] input dwords, lt [1024] coordinate tables, lo / hi [K][32] nibble indices -> acc [32][64]
+    (one_table: [64][64], the low-nibble lookups of the table over y gamma^0..3, then the high-nibble ones)."""
+    acc = np.zeros((64 if one_table else 32, 64), np.uint64)
     for i in range(raw.shape[0]):
         x = raw[i].astype(np.uint64)
         y = lt[x & 255] ^ lt[256 + ((x >> 8) & 255)] ^ lt[512 + ((x >> 16) & 255)] ^ lt[768 + (x >> 24)]
@@ -58,12 +68,28 @@ def model(raw, lt, lo, hi):
                     tl[e] = tl[e] ^ m[b]
                     th[e] = th[e] ^ m[4 + b]
         for p in range(32):
-            acc[p] ^= tl[lo[i, p]] ^ th[hi[i, p]]
+            if one_table:
+                acc[p] ^= tl[lo[i, p]]
+                acc[32 + p] ^= tl[hi[i, p]]
+            else:
+                acc[p] ^= tl[lo[i, p]] ^ th[hi[i, p]]
     return acc.astype(np.uint32)
 
 
-@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 7, 8, 9, 12, 13, 16, 17, 31, 32, 40])
+KS = [1, 2, 3, 4, 5, 7, 8, 9, 12, 13, 16, 17, 31, 32, 40]
+
+
+@pytest.mark.parametrize("K", KS)
 def test_ps8pf_loop_matches_model(pf_lines, K):
+    run_case(pf_lines, K, False)
+
+
+@pytest.mark.parametrize("K", KS)
+def test_ps8pf1_loop_matches_model(pf1_lines, K):
+    run_case(pf1_lines, K, True)
+
+
+def run_case(pf_lines, K, one_table):
     rng = np.random.default_rng(1000 + K)
     S = 4096                 # input symbol stride (bytes)
     nslots = 48
@@ -95,8 +121,8 @@ def test_ps8pf_loop_matches_model(pf_lines, K):
     assert not w.vm and not w.lg, "loads left in flight at the end of the statement"
     raw = np.stack([mem.load32(np.uint64(src_base + int(s) * S + col) + 4 * np.arange(64, dtype=np.uint64))
                     for s in slots])
-    want = model(raw, lt, lo, hi)
-    got = w.v[32:64]
+    want = model(raw, lt, lo, hi, one_table)
+    got = w.v[16:80] if one_table else w.v[32:64]
     assert np.array_equal(got, want)
 
 
