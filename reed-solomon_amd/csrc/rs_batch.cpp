@@ -239,7 +239,7 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
         if ((rc = grow(&c->d_mbits, c->mbits_cap, size_t(nset * sch) * mw * 4))) return rc;
         // the prefetching solve (m8_ps_kernel 9) needs whole 1 KiB chunks and 32-bit input offsets
-        const bool pf = (c->m8_ps_kernel == 9 || c->m8_ps_kernel == 10) && S % 1024 == 0 &&
+        const bool pf = c->m8_ps_kernel >= 9 && S % 1024 == 0 &&
                         uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull;
         hipStream_t sy = st;
         if (ovl) {

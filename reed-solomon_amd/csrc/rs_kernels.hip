@@ -1722,15 +1722,30 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // NB = 1: two nibble tables per input (gen_asm.py ps8pf_kernel, 78 VGPRs, 6 waves per SIMD); NB = 2: one table
 // over y gamma^0..3 with the high-nibble lookups in a second accumulator set (ps8pf1_kernel: 4 multiples and a
 // table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
+// NB = 3 (ps8pf2_kernel): NB = 2 with the multiples y gamma^1..3 read from three more coordinate tables
+// (gamma^j L(x) = L(gamma^j x) is linear in x's bytes: table j entry = xt8^j of table 0's) instead of computed;
+// LDS: tables j = 0..3 at dword 1024 j, L^-1 at 4096, the gamma^4 table at 5120.
 template <int NB>
 __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
-    constexpr int G4 = 2048;  // NB = 2: gamma^4 folded into L^-1 (m8_v1_out), after the coordinate tables
-    __shared__ uint32_t lt[NB == 2 ? 3072 : 2048];
+    constexpr int G4 = 2048;  // NB >= 2: gamma^4 folded into L^-1 (m8_v1_out), G4 dwords after the L^-1 base
+    constexpr int LINV = NB == 3 ? 3072 : 0;  // the output stage's table base: L^-1 at LINV + 1024
+    __shared__ uint32_t lt[NB == 3 ? 6144 : NB == 2 ? 3072 : 2048];
     if (uint32_t(reinterpret_cast<uintptr_t>(lt)) != 0u) __builtin_trap();  // folded away: lt is at 0
-    for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
-    if constexpr (NB == 2) {
+    if constexpr (NB == 3) {
+        for (int i = threadIdx.x; i < 1024; i += 256) {
+            uint32_t v = a.ltab[i];
+            lt[i] = v;
+#pragma unroll
+            for (int j = 1; j < 4; ++j) lt[1024 * j + i] = v = xt8(v);
+            lt[4096 + i] = a.ltab[1024 + i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    }
+    if constexpr (NB >= 2) {
         __syncthreads();
-        for (int i = threadIdx.x; i < 1024; i += 256) lt[G4 + i] = lt[1024 + (i & ~255) + gmul_g4(i & 255)];
+        for (int i = threadIdx.x; i < 1024; i += 256)
+            lt[LINV + G4 + i] = lt[LINV + 1024 + (i & ~255) + gmul_g4(i & 255)];
     }
     __syncthreads();
     const int64_t bid = blockIdx.x;
@@ -1766,7 +1781,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
               "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
               "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", RS_PF_SGPRS);
         m8_v1_store<1>(a, lt, RS_PF_DST, a0, a1, a0, a1);
-    } else {
+    } else if constexpr (NB == 2) {
         u32x16 a0, a1, b0, b1;
         asm volatile(
 #include "gen/m8_idx_asm_ps8pf1_kernel.inc"
@@ -1775,6 +1790,16 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
             : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
               "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", RS_PF_SGPRS);
         m8_v1_store<2, 0, G4>(a, lt, RS_PF_DST, a0, a1, b0, b1);
+    } else {
+        u32x16 a0, a1, b0, b1;
+        asm volatile(
+#include "gen/m8_idx_asm_ps8pf2_kernel.inc"
+            : "=&{v[16:31]}"(a0), "=&{v[32:47]}"(a1), "=&{v[48:63]}"(b0), "=&{v[64:79]}"(b1)
+            : RS_PF_IN
+            : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+              "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94",
+              "v95", "v96", "v97", "v98", "v99", "v100", RS_PF_SGPRS);
+        m8_v1_store<2, 0, G4>(a, lt + LINV, RS_PF_DST, a0, a1, b0, b1);
     }
 #undef RS_PF_DST
 #undef RS_PF_IN
@@ -2413,15 +2438,17 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
-    if (kernel == 9 || kernel == 10) {  // prefetching solves (two / one nibble tables): packed records, whole
-                                        // 1 KiB chunks only
+    if (kernel >= 9 && kernel <= 11) {  // prefetching solves (two / one nibble tables / one table with read
+                                        // multiples): packed records, whole 1 KiB chunks only
         if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
         V1Args f = v;
         f.nchunks = nbytes / 1024;
         if (kernel == 9)
             hipLaunchKernelGGL(k_apply_m8_pf<1>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
-        else
+        else if (kernel == 10)
             hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        else
+            hipLaunchKernelGGL(k_apply_m8_pf<3>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         return hipGetLastError();
     }
 #ifndef RS_AMD_DIAG

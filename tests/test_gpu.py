@@ -678,13 +678,13 @@ SYN_ROUTE_SHAPES = [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
 # (the A/B kernels, overlapped chunks and multi-chunk workgroups: tests/test_gpu_variants.py, diagnostic library)
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(2, 0, 0, 1), (1, 0, 0, 1), (0, 0, 0, 1), (2, 0, 3, 1), (1, 0, 3, 1),
                                                 (0, 0, 3, 1), (2, 0, 9, 1), (1, 0, 9, 1), (0, 0, 9, 1), (2, 0, 10, 1),
-                                                (1, 0, 10, 1)])
+                                                (1, 0, 10, 1), (2, 0, 11, 1), (1, 0, 11, 1)])
 @pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd, k, r, S, n, route, ovl, kern, cpb)
 
 
-@pytest.mark.parametrize("kern", [0, 10])
+@pytest.mark.parametrize("kern", [0, 10, 11])
 @pytest.mark.parametrize("route", [1, 2])
 @pytest.mark.parametrize("k,r,S,n", [SYN_ROUTE_SHAPES[0], SYN_ROUTE_SHAPES[2], SYN_ROUTE_SHAPES[5]])
 def test_decode_batch_syndrome_route_unmasked(k, r, S, n, route, kern):
@@ -702,8 +702,9 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1):
     bit-exact vs the oracle (which reads erased slots as zero), erased repair slots are left as they
     were. n = 1030 at 32 KiB spans two chunks of the syndrome scratch (and several overlapped ones).
     kern 1 / 2: the per-stripe solves on k_apply_m8_ps_w / _w2 (one / two dwords per lane) instead of the
-    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>); 9 / 10: the
-    prefetching solve k_apply_m8_pf<1> / <2> (two / one nibble tables) on packed records (route 0 keeps the ring kernel: survivor plans are not packed;
+    LDS-ring kernel; 3: the ring kernel with one nibble table per input (k_apply_m8_v1<2>); 9 / 10 / 11: the
+    prefetching solve k_apply_m8_pf<1> / <2> / <3> (two / one nibble tables / one table with the multiples read
+    from LDS) on packed records (route 0 keeps the ring kernel: survivor plans are not packed;
     r = 40 gives two output tiles and up to 40 inputs per stripe). cpb > 1: the
     ring kernel walks that many 1 KiB column chunks per workgroup (k_apply_m8_v1<6>; 64 > chunks per symbol). S = 4096 + 520 (survivor route only: the syndrome route needs whole 2 KiB columns)
     ends in a partial column chunk."""

@@ -42,6 +42,11 @@ def pf1_lines(tmp_path_factory):
     return gen_lines("ps8pf1_kernel", tmp_path_factory.mktemp("pf1"))
 
 
+@pytest.fixture(scope="module")
+def pf2_lines(tmp_path_factory):
+    return gen_lines("ps8pf2_kernel", tmp_path_factory.mktemp("pf2"))
+
+
 def pf_byte(L):
     return 4 * (2 * (L >> 3) + (L & 1)) + ((L & 7) >> 1)
 
@@ -89,7 +94,13 @@ def test_ps8pf1_loop_matches_model(pf1_lines, K):
     run_case(pf1_lines, K, True)
 
 
-def run_case(pf_lines, K, one_table):
+@pytest.mark.parametrize("K", KS)
+def test_ps8pf2_loop_matches_model(pf2_lines, K):
+    """The one-table loop reading y gamma^1..3 from three more LDS tables (table j = xt8^j of table 0)."""
+    run_case(pf2_lines, K, True, read_multiples=True)
+
+
+def run_case(pf_lines, K, one_table, read_multiples=False):
     rng = np.random.default_rng(1000 + K)
     S = 4096                 # input symbol stride (bytes)
     nslots = 48
@@ -111,8 +122,11 @@ def run_case(pf_lines, K, one_table):
     rec[K * 64:] = rng.integers(0, 256, 64, dtype=np.uint8)
     mem.b[rec_base:rec_base + rec.size] = rec
     lt = rng.integers(0, 1 << 32, 1024, dtype=np.uint64)
-    lds = np.zeros(8192, np.uint8)
-    lds[:4096] = lt.astype("<u4").view(np.uint8)
+    lds = np.zeros(24576, np.uint8)
+    tab = lt.copy()
+    for j in range(4 if read_multiples else 1):  # table j at byte 4096 j: gamma^j times table 0's entries
+        lds[4096 * j:4096 * (j + 1)] = tab.astype("<u4").view(np.uint8)
+        tab = xt8(tab)
     ops = dict(col=(col + 4 * np.arange(64)).astype(np.uint32), rec=rec_base, pin=pin_base, nk=K, sym=S,
                rsrc=(src_base, nslots * S))
     w = Wave(mem, ops, lgkm=True)
@@ -122,6 +136,8 @@ def run_case(pf_lines, K, one_table):
     raw = np.stack([mem.load32(np.uint64(src_base + int(s) * S + col) + 4 * np.arange(64, dtype=np.uint64))
                     for s in slots])
     want = model(raw, lt, lo, hi, one_table)
+    if read_multiples:
+        assert not w.v[0].any(), "T[0] must stay zero"
     got = w.v[16:80] if one_table else w.v[32:64]
     assert np.array_equal(got, want)
 
