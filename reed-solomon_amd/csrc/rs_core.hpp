@@ -313,9 +313,12 @@ struct rsg_codec {
     int m8_syn_overlap = 0;
     // option m8_ps_kernel: the per-stripe GF(256) solve's kernel: 0 k_apply_m8_v1 (LDS input ring), 1
     // k_apply_m8_ps_w (each wave loads its own inputs; no barriers), 2 k_apply_m8_ps_w2 (the same with
-    // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input), 9
-    // k_apply_m8_pf (no ring, every load issued a step or more ahead; packed records from the plan kernels)
-    int m8_ps_kernel = 0;
+    // two dwords per lane), 3 k_apply_m8_v1<2> (the ring kernel with one nibble table per input), 9 / 10 / 11
+    // k_apply_m8_pf<1 / 2 / 3> (no ring, every load issued a step or more ahead; packed records from the plan
+    // kernels; two nibble tables / one table and two accumulator sets / one table with the multiples read from
+    // LDS). Default 10 (the fastest); symbol sizes with a partial 1 KiB chunk and survivor
+    // plans take 0.
+    int m8_ps_kernel = 10;
     // option m8_syn_masked: 1 (default) the per-stripe fixed pass reads each stripe's erased slots as zero (masked
     // rs_xj) and the solve stores the erased symbols; 0 the plain pass over the slots as they are and a solve
     // that XORs its result into them (one old-value load per output)

@@ -2443,17 +2443,21 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
         if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
         V1Args f = v;
         f.nchunks = nbytes / 1024;
+#ifdef RS_AMD_DIAG  // the two-table (9) and read-multiples (11) forms: measured slower than 10, DESIGN.md 9.1
         if (kernel == 9)
             hipLaunchKernelGGL(k_apply_m8_pf<1>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
-        else if (kernel == 10)
-            hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
-        else
+        else if (kernel == 11)
             hipLaunchKernelGGL(k_apply_m8_pf<3>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        else
+#else
+        if (kernel != 10) return hipErrorInvalidValue;
+#endif
+            hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         return hipGetLastError();
     }
 #ifndef RS_AMD_DIAG
-    // release build: the LDS-ring solve (0, one column chunk per workgroup), its one-table variant (3) and the
-    // prefetching solves (9 / 10, above)
+    // release build: the prefetching solve (10, above; the default), the LDS-ring solve (0, one column chunk per
+    // workgroup) and its one-table variant (3)
     if ((kernel != 0 && kernel != 3) || cpb > 1) return hipErrorInvalidValue;
 #else
     if (kernel == 2) {  // two dwords per lane over 2 KiB chunks, the last one partial: no tail launch

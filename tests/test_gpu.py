@@ -674,17 +674,17 @@ SYN_ROUTE_SHAPES = [(128, 32, 8192, 64), (10, 4, 4096, 300), (30, 17, 2048, 40),
                     (20, 9, 4096 + 520, 33), (60, 40, 4096, 50)]
 
 
-# release-library settings: the three routes, the LDS-ring solve with two or one nibble tables per input
+# release-library settings: the three routes, the prefetching solve (10, the default) and the LDS-ring solve
+# with two or one nibble tables per input
 # (the A/B kernels, overlapped chunks and multi-chunk workgroups: tests/test_gpu_variants.py, diagnostic library)
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(2, 0, 0, 1), (1, 0, 0, 1), (0, 0, 0, 1), (2, 0, 3, 1), (1, 0, 3, 1),
-                                                (0, 0, 3, 1), (2, 0, 9, 1), (1, 0, 9, 1), (0, 0, 9, 1), (2, 0, 10, 1),
-                                                (1, 0, 10, 1), (2, 0, 11, 1), (1, 0, 11, 1)])
+                                                (0, 0, 3, 1), (2, 0, 10, 1), (1, 0, 10, 1), (0, 0, 10, 1)])
 @pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd, k, r, S, n, route, ovl, kern, cpb)
 
 
-@pytest.mark.parametrize("kern", [0, 10, 11])
+@pytest.mark.parametrize("kern", [0, 10])
 @pytest.mark.parametrize("route", [1, 2])
 @pytest.mark.parametrize("k,r,S,n", [SYN_ROUTE_SHAPES[0], SYN_ROUTE_SHAPES[2], SYN_ROUTE_SHAPES[5]])
 def test_decode_batch_syndrome_route_unmasked(k, r, S, n, route, kern):
@@ -1408,10 +1408,11 @@ def test_release_build_ignores_diagnostic_knobs():
     for name, value in ([("m8_mode", v) for v in (0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 19, 21)]
                         + [("m16_mode", 1), ("stamp_buffer", 1), ("m16_cs_col", 1024), ("m16_cs_overlap", 1),
                            ("m8_syn_overlap", 1), ("m8_ps_cpb", 2)]
-                        + [("m8_ps_kernel", v) for v in (1, 2, 4, 5, 6, 7)]):
+                        + [("m8_ps_kernel", v) for v in (1, 2, 4, 5, 6, 7, 8, 9, 11)]):
         with pytest.raises(rs_amd.RSError):
             codec.set_option(name, value)
-    for name, value in [("m8_mode", 18), ("m8_mode", 20), ("m8_ps_kernel", 0), ("m8_ps_kernel", 3), ("m16_cs_col", 256),
+    for name, value in [("m8_mode", 18), ("m8_mode", 20), ("m8_ps_kernel", 0), ("m8_ps_kernel", 3),
+                        ("m8_ps_kernel", 10), ("m16_cs_col", 256),
                         ("m16_cs_overlap", 0), ("m8_syn_overlap", 0), ("m8_ps_cpb", 1), ("xj", 0), ("xj", 1)]:
         codec.set_option(name, value)  # the production settings stay accepted
     import os

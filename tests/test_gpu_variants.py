@@ -42,10 +42,12 @@ def test_decode_matches_oracle_on_noncodewords_variants():
 
 
 # diagnostic-library settings of the GF(256) per-stripe decode: overlapped chunks (ovl), the A/B solve kernels
-# 1 (k_apply_m8_ps_w), 2 (_w2), 4 / 5 (ring-kernel table variants), several column chunks per workgroup (cpb)
+# 1 (k_apply_m8_ps_w), 2 (_w2), 4 / 5 (ring-kernel table variants), 9 / 11 (prefetching solves with two tables /
+# read multiples), several column chunks per workgroup (cpb)
 @pytest.mark.parametrize("route,ovl,kern,cpb", [(1, 1, 0, 1), (1, 0, 1, 1), (0, 0, 1, 1), (1, 0, 2, 1), (1, 1, 2, 1),
                                                 (0, 0, 2, 1), (2, 1, 0, 1), (2, 0, 2, 1), (2, 1, 2, 1), (2, 0, 0, 3),
-                                                (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2), (2, 0, 4, 1), (2, 0, 5, 1)])
+                                                (2, 1, 0, 4), (1, 0, 0, 64), (0, 0, 0, 2), (2, 0, 4, 1), (2, 0, 5, 1),
+                                                (2, 0, 9, 1), (1, 0, 9, 1), (2, 0, 11, 1), (1, 0, 11, 1), (2, 1, 10, 1)])
 @pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
 def test_decode_batch_syndrome_route_diag(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd.diag_module(), k, r, S, n, route, ovl, kern, cpb)
