@@ -61,9 +61,15 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *                  kernel, then a t_info x t solve; 0 survivor matrices. Erased slots may hold anything.
  *   "m8_syn_overlap" 0 one stream (default); [diag] 1 that route's plans + fixed pass of the next chunk on a
  *                  codec stream beside this chunk's solve (two buffer sets)
- *   "m8_ps_kernel" that route's per-stripe solve kernel: 0 LDS input ring (default), 3 the ring kernel with
- *                  one nibble table; [diag] 1 one dword per lane without the ring, 2 two dwords per lane,
- *                  4 / 5 the one-table kernel converting 2 / 4 inputs per LDS round trip
+ *   "m8_ps_kernel" that route's per-stripe solve kernel: 10 the prefetching solve (one asm loop, packed
+ *                  records, every load a step ahead, one nibble table; default), 0 LDS input ring, 3 the ring
+ *                  kernel with one nibble table; [diag] 9 / 11 the prefetching solve with two tables / with its
+ *                  multiples read from LDS, 1 one dword per lane without the ring, 2 two dwords per lane,
+ *                  4 / 5 the one-table kernel converting 2 / 4 inputs per LDS round trip. Survivor plans and
+ *                  symbol sizes with a partial 1 KiB chunk take 0.
+ *   "m8_syn_masked" 1 the fixed pass reads each stripe's erased slots as zero and the solve stores (default);
+ *                  0 the pass reads the slots as they are and the solve XORs its result into them
+ *   "m8_syn_scratch_mib" fixed-pass scratch per chunk of stripes (MiB, default 1024; sets the launch count)
  *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0: 1 (default); [diag] 2-64 walk a
  *                  stripe's chunks in one workgroup (table setup once, next chunk's ring prologue under the
  *                  outputs)
