@@ -181,9 +181,10 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
-        if (value < 0 || value > 11) return RS_ERR_INVALID;
+        if (value < 0 || value > 13) return RS_ERR_INVALID;
 #ifndef RS_AMD_DIAG  // 10: the prefetching kernel (default); 0 / 3: the ring kernels; 9, 11: other prefetching
-                     // forms and 1, 2, 4, 5: A/B kernels (diagnostic build); 6, 8: ablations (wrong results); 7: stamps
+                     // forms and 1, 2, 4, 5: A/B kernels (diagnostic build); 6, 8, 12, 13: ablations (wrong
+                     // results); 7: stamps
         if (value != 0 && value != 3 && value != 10) return RS_ERR_INVALID;
 #endif
         c->m8_ps_kernel = int(value);

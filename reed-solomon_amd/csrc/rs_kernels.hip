@@ -1729,7 +1729,7 @@ template <int NB>
 __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
     constexpr int G4 = 2048;  // NB >= 2: gamma^4 folded into L^-1 (m8_v1_out), G4 dwords after the L^-1 base
     constexpr int LINV = NB == 3 ? 3072 : 0;  // the output stage's table base: L^-1 at LINV + 1024
-    __shared__ uint32_t lt[NB == 3 ? 6144 : NB == 2 ? 3072 : 2048];
+    __shared__ uint32_t lt[NB == 3 ? 6144 : NB == 1 ? 2048 : 3072];
     if (uint32_t(reinterpret_cast<uintptr_t>(lt)) != 0u) __builtin_trap();  // folded away: lt is at 0
     if constexpr (NB == 3) {
         for (int i = threadIdx.x; i < 1024; i += 256) {
@@ -1742,7 +1742,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
     } else {
         for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
     }
-    if constexpr (NB >= 2) {
+    if constexpr (NB != 1) {
         __syncthreads();
         for (int i = threadIdx.x; i < 1024; i += 256)
             lt[LINV + G4 + i] = lt[LINV + 1024 + (i & ~255) + gmul_g4(i & 255)];
@@ -1781,14 +1781,29 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
               "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
               "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", RS_PF_SGPRS);
         m8_v1_store<1>(a, lt, RS_PF_DST, a0, a1, a0, a1);
-    } else if constexpr (NB == 2) {
+    } else if constexpr (NB == 2 || NB == 12 || NB == 13) {
         u32x16 a0, a1, b0, b1;
-        asm volatile(
+#define RS_PF1_OPS                                                                                                \
+    : "=&{v[16:31]}"(a0), "=&{v[32:47]}"(a1), "=&{v[48:63]}"(b0), "=&{v[64:79]}"(b1)                               \
+    : RS_PF_IN                                                                                                     \
+    : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v80", \
+      "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", RS_PF_SGPRS
+        if constexpr (NB == 2) {
+            asm volatile(
 #include "gen/m8_idx_asm_ps8pf1_kernel.inc"
-            : "=&{v[16:31]}"(a0), "=&{v[32:47]}"(a1), "=&{v[48:63]}"(b0), "=&{v[64:79]}"(b1)
-            : RS_PF_IN
-            : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
-              "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", RS_PF_SGPRS);
+                RS_PF1_OPS);
+#ifdef RS_AMD_DIAG
+        } else if constexpr (NB == 12) {  // timing ablation: no index switches (wrong results)
+            asm volatile(
+#include "gen/m8_idx_asm_ps8pf1_noswitch.inc"
+                RS_PF1_OPS);
+        } else {  // timing ablation: no gpr-index mode (wrong results)
+            asm volatile(
+#include "gen/m8_idx_asm_ps8pf1_plain.inc"
+                RS_PF1_OPS);
+#endif
+        }
+#undef RS_PF1_OPS
         m8_v1_store<2, 0, G4>(a, lt, RS_PF_DST, a0, a1, b0, b1);
     } else {
         u32x16 a0, a1, b0, b1;
@@ -2438,7 +2453,7 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
-    if (kernel >= 9 && kernel <= 11) {  // prefetching solves (two / one nibble tables / one table with read
+    if (kernel >= 9 && kernel <= 13) {  // prefetching solves (two / one nibble tables / one table with read
                                         // multiples): packed records, whole 1 KiB chunks only
         if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
         V1Args f = v;
@@ -2446,6 +2461,9 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
 #ifdef RS_AMD_DIAG  // the two-table (9) and read-multiples (11) forms: measured slower than 10, DESIGN.md 9.1
         if (kernel == 9)
             hipLaunchKernelGGL(k_apply_m8_pf<1>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        else if (kernel == 12 || kernel == 13)  // timing ablations of kernel 10 (wrong results)
+            hipLaunchKernelGGL(kernel == 12 ? k_apply_m8_pf<12> : k_apply_m8_pf<13>,
+                               dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 11)
             hipLaunchKernelGGL(k_apply_m8_pf<3>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         else
