@@ -312,7 +312,8 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
             RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
-        c->last_kernel = std::string(c->syn_route == 2 ? "reenc_xj" : "syn_xj") + "+apply_m8_v1_ps" + (ovl ? "(overlap)" : "");
+        c->last_kernel = std::string(c->syn_route == 2 ? "reenc_xj" : "syn_xj") + (pf ? "+apply_m8_pf" : "+apply_m8_v1_ps") +
+                         (ovl ? "(overlap)" : "");
         return scratch_release(c, st);
     }
     for (int64_t c0 = 0; c0 < nsel; c0 += chunk) {

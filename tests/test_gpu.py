@@ -270,11 +270,13 @@ def test_inflight_scalar_load_fix_on_the_kernels_run(tmp_path, monkeypatch):
         torch.cuda.synchronize()
         assert codec.last_kernel.startswith("rs_v1jit"), codec.last_kernel
         assert np.array_equal(dev.cpu().numpy(), got), (k, r)
-    # the per-stripe solve (k_apply_m8_v1<0>, re-encode route) over 2048 all-distinct stripes
+    # the per-stripe solve (k_apply_m8_v1<0>, re-encode route) over 2048 all-distinct stripes (the ring kernel
+    # by option: the default solve is the prefetching k_apply_m8_pf)
     k, r, S, n = 128, 32, 2048, 2048
     dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda")
     rs_amd.fill_info(dev, k, seed=0x52)
     codec = rs_amd.Codec(k, r, batch_plans=1)
+    codec.set_option("m8_ps_kernel", 0)
     codec.encode(dev)
     torch.cuda.synchronize()
     full = dev.clone()
@@ -285,7 +287,7 @@ def test_inflight_scalar_load_fix_on_the_kernels_run(tmp_path, monkeypatch):
     dev[torch.from_numpy(pats).cuda()] = 0
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
-    assert "apply_m8_v1_ps" in codec.last_kernel, codec.last_kernel
+    assert codec.last_kernel.endswith("+apply_m8_v1_ps"), codec.last_kernel
     assert torch.equal(dev, full)
     objs = [os.path.join(tmp_path, f) for f in os.listdir(tmp_path) if f.startswith("v1_") and f.endswith(".co")]
     assert len(objs) >= 2, os.listdir(tmp_path)
@@ -381,7 +383,8 @@ def test_decode_batch_per_stripe_patterns(S, plans, n):
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
     if plans == 2:
-        assert ("apply_m8_v1_ps" in codec.last_kernel) == (n == 100), codec.last_kernel
+        lk = codec.last_kernel
+        assert ("apply_m8_v1_ps" in lk or "apply_m8_pf" in lk) == (n == 100), lk
     got = dev.cpu().numpy()
     for s in range(n):
         want = poisoned[s].copy()
@@ -735,8 +738,9 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1):
     assert codec.decode_batch(dev, pats) == 0
     torch.cuda.synchronize()
     fixed = {1: "syn_xj", 2: "reenc_xj"}.get(route)
+    solve = "+apply_m8_pf" if kern >= 9 and S % 1024 == 0 else "+apply_m8_v1_ps"
     assert codec.last_kernel == ("apply_m8_v1_ps" if not route else
-                                 fixed + "+apply_m8_v1_ps" + ("(overlap)" if ovl else "")), codec.last_kernel
+                                 fixed + solve + ("(overlap)" if ovl else "")), codec.last_kernel
     assert torch.equal(dev[:, :k], full[:, :k])
     rep_er = mask.clone()
     rep_er[:, :k] = False
