@@ -238,9 +238,12 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
         if ((rc = grow(&c->d_pout, c->pout_cap, size_t(nset * sch * out_stride) * 4))) return rc;
         if ((rc = grow(&c->d_pidx, c->pidx_cap, size_t(nset * sch * idx_stride) * 4))) return rc;
         if ((rc = grow(&c->d_mbits, c->mbits_cap, size_t(nset * sch) * mw * 4))) return rc;
-        // the prefetching solve (m8_ps_kernel 9) needs whole 1 KiB chunks and 32-bit input offsets
-        const bool pf = c->m8_ps_kernel >= 9 && S % 1024 == 0 &&
-                        uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull;
+        // the prefetching solves (m8_ps_kernel 9-11) need whole 1 KiB chunks, 32-bit input offsets, and slot lists
+        // 19 entries longer than K: their slot blocks of 8 are loaded up to two blocks ahead (K + 18 at most;
+        // in_stride = n + 16, K <= min(k, r) on the re-encode route, <= r on the syndrome route)
+        const int kmax = c->syn_route == 2 ? std::min<int>(c->k, c->r) : int(c->r);
+        const bool pf = c->m8_ps_kernel >= 9 && S % 1024 == 0 && uint64_t(sch) * uint64_t(per) <= 0xFFFFFFFFull &&
+                        int64_t(kmax) + 19 <= in_stride;
         hipStream_t sy = st;
         if (ovl) {
             if ((rc = overlap_objects(c))) return rc;

@@ -1718,7 +1718,10 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // which the next input's packed record (one SMEM load of 16 dwords) and coordinate-table reads are issued a
 // step ahead and the raw inputs four inputs ahead, so each step waits once for loads issued a step earlier.
 // Records are the plan kernels' packed form (SynPlanArgs::pidx8); same math as k_apply_m8_v1<0>, same
-// output stage. The coordinate tables must sit at LDS address 0: lt is the kernel's only LDS array.
+// output stage. The coordinate tables must sit at LDS address 0: lt is the kernel's only LDS array. Reads
+// past the stripe's lists: records up to K (one record of prefetch; the record array has room), slot entries
+// up to K + 18 (blocks of 8, two ahead; the host requires K + 19 <= ps_in), raw inputs of the zero-padded slots
+// (slot 0, a valid offset); all are drained before the asm statement ends.
 // NB = 1: two nibble tables per input (gen_asm.py ps8pf_kernel, 78 VGPRs, 6 waves per SIMD); NB = 2: one table
 // over y gamma^0..3 with the high-nibble lookups in a second accumulator set (ps8pf1_kernel: 4 multiples and a
 // table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
