@@ -54,13 +54,13 @@ def test_m16_v1_step_matches_gf_multiply(tmp_path):
     text = "\n".join(step_lines(str(tmp_path)))
     text = (text.replace("%[t0]", "v200").replace("%[t1]", "v201").replace("%[y0]", "v202")
             .replace("%[k2d]", "v203").replace("%[cp]", "s[90:91]"))
-    w = Wave(mem, {})
+    w = Wave(mem, {}, lgkm=True)
     w.v[202] = x
     w.v[203] = 0x002D002D
     w.v[72:136] = acc0
     w.s[90], w.s[91] = 1024, 0
     w.run(["s_load_dwordx16 s[40:55], s[90:91], 0x0"] + text.splitlines(), [])  # the kernel's first-plane load
-    w.retire(0)  # the next step (or the kernel) waits for these loads before use
+    w.drain()  # the next step (or the kernel) waits for these loads before use
     lo, hi = x & 0xFFFF, x >> 16
     for p in range(64):
         want = (gf_mul(lo, coef[p]) | (gf_mul(hi, coef[p]) << 16)) ^ acc0[p]
@@ -101,13 +101,13 @@ def test_m8_v1_step_matches_gf256_multiply(tmp_path):
     text = "\n".join(lines)
     text = (text.replace("%[t0]", "v200").replace("%[t1]", "v201").replace("%[y0]", "v202")
             .replace("%[k1d]", "v203").replace("%[cp]", "s[90:91]"))
-    w = Wave(mem, {})
+    w = Wave(mem, {}, lgkm=True)
     w.v[202] = y
     w.v[203] = 0x1D1D1D1D
     w.v[40:72] = acc0
     w.s[90], w.s[91] = 1024, 0
     w.run(text.splitlines(), [])
-    w.retire(0)  # the next step (or the kernel) waits for these loads before use
+    w.drain()  # the next step (or the kernel) waits for these loads before use
     for p in range(32):
         assert np.array_equal(w.v[40 + p], gf256_mul_bytes(y, coef[p]) ^ acc0[p]), p
 
@@ -150,7 +150,7 @@ def test_cs16_step_circulant_xor(tmp_path, variant):
         text = "\n".join(lines)
         text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[92:93]").replace("%[rsrc]", "s[96:99]")
                 .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
-        w = Wave(mem, {})
+        w = Wave(mem, {}, lgkm=True)
         w.v[136:152] = f
         w.v[72:136] = acc0
         lane = (np.arange(64) * 4 + 256).astype(np.uint32)
@@ -160,7 +160,7 @@ def test_cs16_step_circulant_xor(tmp_path, variant):
         w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
         w.s[76:92] = offs.astype(np.uint64)
         w.run([f"s_load_dwordx16 s[{cur}:{cur + 15}], s[100:101], 0x0"] + text.splitlines(), [])
-        w.retire(0)  # the next step (or the kernel) waits for these loads before use
+        w.drain()  # the next step (or the kernel) waits for these loads before use
         for c in range(4):
             for t in range(16):
                 want = acc0[16 * c + t].copy()
@@ -206,7 +206,7 @@ def test_bs16_step_binary_accumulation(tmp_path):
     text = "\n".join(lines)
     text = (text.replace("%[cp]", "s[100:101]").replace("%[gp]", "s[92:93]").replace("%[rsrc]", "s[96:99]")
             .replace("%[lane]", "v230").replace("%[t0]", "v231").replace("%[t1]", "v232"))
-    w = Wave(mem, {})
+    w = Wave(mem, {}, lgkm=True)
     w.v[136:152] = f
     w.v[72:136] = acc0
     w.v[230] = (np.arange(64) * 4).astype(np.uint32)
@@ -215,7 +215,7 @@ def test_bs16_step_binary_accumulation(tmp_path):
     w.s[96], w.s[97], w.s[98], w.s[99] = 32768, 0, 16384, 0x20000
     w.s[76:92] = offs.astype(np.uint64)
     w.run(["s_load_dwordx16 s[40:55], s[100:101], 0x0"] + text.splitlines(), [])
-    w.retire(0)  # the next step (or the kernel) waits for these loads before use
+    w.drain()  # the next step (or the kernel) waits for these loads before use
     for c in range(4):
         for t in range(16):
             want = acc0[16 * c + t].copy()
@@ -303,7 +303,7 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
         mem.b[4160:4224] = rng.integers(0, 2 ** 31, 16).astype("<u4").view(np.uint8)  # the group after next
         f = rng.integers(0, 2 ** 32, (16, 64), dtype=np.uint64).astype(np.uint32)
         acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
-        w = Wave(mem, {})
+        w = Wave(mem, {}, lgkm=True)
         w.v[F:F + 16] = f  # this group's inputs, loaded by the previous step
         w.v[A:A + 16 * cw] = acc0
         w.s[108] = 512  # the wave's byte column
@@ -325,7 +325,7 @@ def test_cs16t_threaded_step_circulant_xor(tmp_path):
                 break
         assert visited == list(rec), (visited, list(rec))
         w.run(lines, [], entry="L_cst_ret%=")  # back in the step: the next group's loads
-        w.retire(0)
+        w.drain()
         assert np.array_equal(w.v[A:A + 16 * cw], _circulant(acc0, f, z, cw)), trial
         words = data.view("<u4")
         lane = (np.arange(64) * 4 + 512).astype(np.uint32)
@@ -380,7 +380,7 @@ def test_cs16t_kernel_loop_over_groups(tmp_path):
         mem.b[R0:R0 + rec.size * 4] = rec.astype("<u4").view(np.uint8).reshape(-1)
         data = rng.integers(0, 256, 32768, dtype=np.uint8)
         mem.b[DATA:DATA + 32768] = data
-        w = Wave(mem, {})
+        w = Wave(mem, {}, lgkm=True)
         acc0 = rng.integers(0, 2 ** 32, (16 * cw, 64), dtype=np.uint64).astype(np.uint32)
         w.v[A:A + 16 * cw] = acc0
         w.s[102], w.s[103] = G0, 0

@@ -98,6 +98,11 @@ class Wave:
             elif r is not None:
                 self.v[r] = data
 
+    def drain(self):
+        """Every load in flight lands (the wait a following step or the kernel end performs)."""
+        self.retire(0)
+        self.retire_lgkm(0)
+
     def retire_lgkm(self, n):
         """s_waitcnt lgkmcnt(n) under the lgkm model."""
         if n == 0 or not any(k == "s" for k, _, _ in self.lg):
@@ -425,7 +430,7 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, 
             for i, w in enumerate(masks):
                 ops[f"mw{i}"] = int(w)
             ops["zb"] = int(zero)
-        wave = Wave(mem, ops)
+        wave = Wave(mem, ops, lgkm=True)
         wave.lds = lds
         waves.append(wave)
         seg = [[]]  # the block's waves run in lockstep between s_barriers
