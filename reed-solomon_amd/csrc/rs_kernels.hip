@@ -1507,8 +1507,9 @@ __global__ void __launch_bounds__(256) k_plan_m8(PlanArgs a) {
 // sum_{e in E} X_e^j d_e = S_j, j < t, over the syndromes of fft_transform_cycl (fft.c:39-100, erased
 // slots read as zero). Its inverse is W[p][j] = q_{p,j} / Q_p(X_p), q_p the coefficients of
 // Q_p(x) = P(x) / (x + X_p) (Lagrange): the same linear map, so results are bit-identical. Erased slots are
-// not zeroed: their old contents g enter the syndromes, the solve yields g + c for the erased information
-// slots, and the apply XORs that into g (V1Args::xor_dst). Erased repair slots only shift their own unknowns.
+// never zeroed: the masked fixed pass reads them as zero and the solve stores c (default), or the plain pass
+// sees their old contents g, the solve yields g + c and the apply XORs that into g (V1Args::xor_dst, option
+// m8_syn_masked 0). Erased repair slots only shift their own unknowns.
 // Byte of lookup L in a packed k_apply_m8_pf record (gen_asm.py ps8pf_kernel): L = 8 m + 2 k + d sits in byte
 // k of dword 2 m + d, so one s_lshr_b64 of a dword pair brings the next byte of both dwords down.
 __device__ __forceinline__ int pf_byte(int L) { return 4 * (2 * (L >> 3) + (L & 1)) + ((L & 7) >> 1); }
@@ -1614,14 +1615,15 @@ __global__ void __launch_bounds__(256) k_plan_syn_m8(SynPlanArgs a) {
 
 // Re-encode plans (SynPlanArgs, syn_route 2). The codec's fixed pass computes, for every repair slot P,
 //   S'_P = (G rcv_info)_P + rcv_P          (G the encode matrix: [G | I] on the bit-plane XOR kernel)
-// which is zero for a codeword. With d the differences on the erased slots (erased information slots hold
-// their old contents g, d_Q = g_Q + c_Q; erased repair slots likewise), S'_P = sum_{Q in E_i} G[P][Q] d_Q for
+// which is zero for a codeword. With d the differences on the erased slots (the masked pass reads them as zero,
+// d_Q = c_Q; the plain pass reads their old contents g, d_Q = g_Q + c_Q), S'_P = sum_{Q in E_i} G[P][Q] d_Q for
 // every surviving repair slot P. The first t_i = |E_i| of them (R', in slot order; t <= r leaves enough)
 // give a square system, and because G[P][Q] = L_E(Y_Q) / (L_E'(X_P) (X_P + Y_Q)) (gf16.cpp:solve_matrix, E
 // = the repair positions) is a scaled Cauchy matrix, its inverse is again of that form:
 //   W[Q][P] = L_T(X_P) / ((X_P + Y_Q) L_T'(Y_Q)),   T = E_i + (repair slots not in R'), |T| = r,
 // i.e. solve_matrix with targets T, emitted rows E_i, sources R' -- the same evaluation as k_plan_m8.
-// d = W S'_{R'} is then XORed into the erased information slots (V1Args::xor_dst). A t_i x t_i solve from
+// d = W S'_{R'} is then stored into the erased information slots (masked pass) or XORed into them
+// (V1Args::xor_dst, plain pass). A t_i x t_i solve from
 // t_i rows of a pattern-independent pass over k + r inputs whose matrix is G plus an identity, against the
 // syndrome route's t_i x t solve after a pass of r x (k + r) Vandermonde rows.
 __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
@@ -1711,7 +1713,8 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
     }
 }
 
-// Per-stripe solve with every load issued ahead of its use (m8_ps_kernel 9). The ring kernel's waves spend
+// Per-stripe solve with every load issued ahead of its use (m8_ps_kernel 9 / 10 / 11; 10 = NB 2 is the default,
+// and 12 / 13 = NB 12 / 13 are its diagnostic timing ablations). The ring kernel's waves spend
 // about half their cycles waiting (SMEM record halves fetched inside each step, a slot read per batch, one
 // barrier per 4 inputs; profiles/r4/ps8_route2.md); here each wave runs its own 256-byte column with no
 // barrier after the table copy, and the whole input loop is one asm statement (gen_asm.py ps8pf_kernel) in
@@ -1727,7 +1730,8 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
 // NB = 3 (ps8pf2_kernel): NB = 2 with the multiples y gamma^1..3 read from three more coordinate tables
 // (gamma^j L(x) = L(gamma^j x) is linear in x's bytes: table j entry = xt8^j of table 0's) instead of computed;
-// LDS: tables j = 0..3 at dword 1024 j, L^-1 at 4096, the gamma^4 table at 5120.
+// LDS: tables j = 0..3 at dword 1024 j, L^-1 at 4096, the gamma^4 table at 5120. NB = 2 issues fastest (the
+// loop is VALU-issue bound), so 9 and 11 are diagnostic-build only.
 template <int NB>
 __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
     constexpr int G4 = 2048;  // NB >= 2: gamma^4 folded into L^-1 (m8_v1_out), G4 dwords after the L^-1 base
