@@ -202,12 +202,14 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
         }
         return;
     }
-    // Branch-free: outputs are stored from p = 31 down, and every p >= rows goes to output rows - 1's address
-    // first, so that output's own store (same lane, same address, later in program order) is the one that
-    // stays; straight-line groups of 8 conversions keep 32 LDS reads in flight.
+    // Outputs are stored from p = 31 down in groups of 8: a group past the tile's rows is skipped (one uniform
+    // branch), and in the group holding row rows - 1 every p >= rows goes to that row's address first, so that
+    // output's own store (same lane, same address, later in program order) is the one that stays; each group is
+    // straight-line code with 32 LDS reads in flight.
     const int32_t slast = sload(out + (rows - 1));
 #pragma unroll
     for (int p0 = 24; p0 >= 0; p0 -= 8) {
+        if (p0 >= rows) continue;  // a whole group past the tile's rows (uniform): not converted
         uint32_t w[8];
 #pragma unroll
         for (int q = 7; q >= 0; --q) w[q] = m8_v1_out<NB, G4>(lt, p0 + q, a0, a1, b0, b1);
