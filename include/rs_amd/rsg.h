@@ -70,6 +70,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m8_syn_masked" 1 the fixed pass reads each stripe's erased slots as zero and the solve stores (default);
  *                  0 the pass reads the slots as they are and the solve XORs its result into them
  *   "m8_syn_scratch_mib" fixed-pass scratch per chunk of stripes (MiB, default 1024; sets the launch count)
+ *   "m8_syn_coord" 1 (default) with the masked pass and solve 10: the pass stores its outputs in GF(256)^2
+ *                  coordinates and the solve reads them as they are; 0 the solve converts its inputs
  *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0: 1 (default); [diag] 2-64 walk a
  *                  stripe's chunks in one workgroup (table setup once, next chunk's ring prologue under the
  *                  outputs)
@@ -224,8 +226,9 @@ int64_t rsg_symbol_pool_cap(int64_t bytes);
  * NULL and are written only when it applies. Host only. */
 int rsg_bs16_dump(uint16_t k, uint16_t r, const bool* is_erased, uint16_t t, int32_t* info, uint8_t* rec,
                   int32_t* fin, int32_t* fin_off);
-/* Source of the masked (masked = 1) or plain XOR kernel of the GF(256) per-stripe route's fixed pass over all
- * k + r slots: route 1 the r syndromes, 2 the re-encode differences [G | I]. The masked form reads every
+/* Source of the masked (masked = 1), masked with outputs in GF(256)^2 coordinates (2, the form the default
+ * prefetching solve reads) or plain (0) XOR kernel of the GF(256) per-stripe route's fixed pass over all
+ * k + r slots: route 1 the r syndromes, 2 the re-encode differences [G | I]. The masked forms read every
  * slot whose bit is set in its stripe's mask words as zero. RS_ERR_INVALID when the route does not apply
  * (m = 16 codes, K * R past the XOR kernel's bound). Host only (emulator tests). */
 int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len);

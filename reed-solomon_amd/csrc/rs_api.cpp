@@ -180,6 +180,12 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         c->dec_lru.clear();
         return 0;
     }
+    // the per-stripe fixed pass's form follows these options: a change rebuilds it at the next call
+    auto syn_reform = [c]() {
+        if (c->syn && c->syn->xj) (void)hipDeviceSynchronize();  // the old pass may still be queued
+        c->syn.reset();
+        c->syn_failed = false;
+    };
     if (!std::strcmp(name, "m8_ps_kernel")) {  // per-stripe GF(256) solve kernel (results identical)
         if (value < 0 || value > 13) return RS_ERR_INVALID;
 #ifndef RS_AMD_DIAG  // 10: the prefetching kernel (default); 0 / 3: the ring kernels; 9, 11: other prefetching
@@ -187,17 +193,20 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
                      // results); 7: stamps
         if (value != 0 && value != 3 && value != 10) return RS_ERR_INVALID;
 #endif
+        if ((int(value) == 10) != (c->m8_ps_kernel == 10)) syn_reform();  // the coordinate form goes with 10
         c->m8_ps_kernel = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m8_syn_masked")) {  // per-stripe fixed pass masked (1) or plain + XOR solve (0)
         if (value < 0 || value > 1) return RS_ERR_INVALID;
-        if (int(value) != c->m8_syn_masked) {
-            if (c->syn && c->syn->xj) (void)hipDeviceSynchronize();  // the old pass may still be queued
-            c->syn.reset();  // rebuilt in the other form at the next call
-            c->syn_failed = false;
-        }
+        if (int(value) != c->m8_syn_masked) syn_reform();
         c->m8_syn_masked = int(value);
+        return 0;
+    }
+    if (!std::strcmp(name, "m8_syn_coord")) {  // fixed pass stores coordinates for solve 10 (1) or not (0)
+        if (value < 0 || value > 1) return RS_ERR_INVALID;
+        if (int(value) != c->m8_syn_coord) syn_reform();
+        c->m8_syn_coord = int(value);
         return 0;
     }
     if (!std::strcmp(name, "m8_ps_cpb")) {  // per-stripe GF(256) solve: column chunks per workgroup

@@ -87,8 +87,13 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
             c->syn_failed = true;
             return false;
         }
-        // the masked form (default): each stripe's erased slots read as zero (XJArgs::masks)
-        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, c->m8_syn_masked != 0) || !p->xj) {
+        // the masked form (default): each stripe's erased slots read as zero (XJArgs::masks); with the prefetching
+        // solve 10 (whose slot lists need 19 entries past K: K <= min(k, r) or r), its outputs stored in
+        // coordinates (form 2), so the solve reads them as they are
+        const int kmax = c->syn_route == 2 ? std::min<int>(c->k, c->r) : int(c->r);
+        const bool coord = c->m8_syn_masked && c->m8_syn_coord && c->m8_ps_kernel == 10 && kmax + 3 <= n;
+        if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, c->m8_syn_masked ? (coord ? 2 : 1) : 0) ||
+            !p->xj) {
             std::fprintf(stderr, "librs_amd: syndrome XOR kernel unavailable; per-stripe survivor plans\n");
             c->syn_failed = true;
             return false;
@@ -120,6 +125,7 @@ static int syn_fixed_pass(rsg_codec_t* c, const uint8_t* base, int64_t stripe_st
         x.masks = d_mbits;
         x.zero = static_cast<const uint8_t*>(c->d_zero);
     }
+    if (p.xj->coord) x.tab = reinterpret_cast<const uint16_t*>(c->d_ltab);  // its outputs' coordinate tables
     c->last_kernel = p.xj->name;
     const int rc = xj_launch(*p.xj, x, cn, int64_t(S / 2048) * (2048 / kXjChunk), st);
     const int rc2 = p.note_use(st);
@@ -310,8 +316,10 @@ int decode_batch_device_plans(rsg_codec_t* c, uint8_t* base, int64_t stripe_stri
 #endif
             v.stamps = c->stamps;  // diagnostic builds, m8_ps_kernel 7
             v.src_bytes = cn * per;
-            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st,
-                                       pf ? c->m8_ps_kernel : c->m8_ps_kernel >= 9 ? 0 : c->m8_ps_kernel, c->m8_ps_cpb));
+            // the coordinate-output pass pairs only with the prefetching solve on coordinate inputs (14)
+            const int kern = c->syn->xj->coord ? 14 : pf ? c->m8_ps_kernel : c->m8_ps_kernel >= 9 ? 0 : c->m8_ps_kernel;
+            if (c->syn->xj->coord && !pf) return RS_ERR_INVALID;  // not reached: the route needs whole 2 KiB chunks
+            HIP_TRY(launch_apply_m8_ps(v, cn, int64_t(S), tiles, st, kern, c->m8_ps_cpb));
             RS_CHECKPOINT(c, c->syn.get(), "per-stripe GF(256) solve (apply_m8_ps, syndrome / re-encode route)", uint64_t(cn), S);
             if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
         }
@@ -980,7 +988,9 @@ extern "C" int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route) {
     std::vector<int32_t> in(static_cast<size_t>(n)), out(static_cast<size_t>(r));
     for (int i = 0; i < n; ++i) in[size_t(i)] = i;
     for (int j = 0; j < r; ++j) out[size_t(j)] = j;
-    return xj_precompile(syn_fixed_matrix(pos, k, r, route), n, r, in, out, true);
+    // the codec's default form: masked, coordinate outputs when the prefetching solve takes them
+    const int kmax = route == 2 ? std::min<int>(k, r) : int(r);
+    return xj_precompile(syn_fixed_matrix(pos, k, r, route), n, r, in, out, kmax + 3 <= n ? 2 : 1);
 }
 
 extern "C" int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len) {
@@ -992,7 +1002,7 @@ extern "C" int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked
     std::vector<int32_t> in(static_cast<size_t>(n)), out(static_cast<size_t>(r));
     for (int i = 0; i < n; ++i) in[size_t(i)] = i;
     for (int j = 0; j < r; ++j) out[size_t(j)] = j;
-    const std::string src = xj_source(syn_fixed_matrix(pos, k, r, route), n, r, in, out, true, masked != 0);
+    const std::string src = xj_source(syn_fixed_matrix(pos, k, r, route), n, r, in, out, true, masked);
     if (len) *len = src.size();
     if (buf && cap) {
         const size_t m = std::min(cap - 1, src.size());

@@ -1728,6 +1728,8 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // NB = 1: two nibble tables per input (gen_asm.py ps8pf_kernel, 78 VGPRs, 6 waves per SIMD); NB = 2: one table
 // over y gamma^0..3 with the high-nibble lookups in a second accumulator set (ps8pf1_kernel: 4 multiples and a
 // table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
+// NB = 4 (ps8pf1c_kernel, launched as 14): NB = 2 over inputs the fixed pass stored in coordinates already
+// (rs_xj masked form 2, which converts its 32 outputs with the same LDS tables): no coordinate reads per step.
 // NB = 3 (ps8pf2_kernel): NB = 2 with the multiples y gamma^1..3 read from three more coordinate tables
 // (gamma^j L(x) = L(gamma^j x) is linear in x's bytes: table j entry = xt8^j of table 0's) instead of computed;
 // LDS: tables j = 0..3 at dword 1024 j, L^-1 at 4096, the gamma^4 table at 5120. NB = 2 issues fastest (the
@@ -1746,10 +1748,10 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
             for (int j = 1; j < 4; ++j) lt[1024 * j + i] = v = xt8(v);
             lt[4096 + i] = a.ltab[1024 + i];
         }
-    } else {
-        for (int i = threadIdx.x; i < 2048; i += 256) lt[i] = a.ltab[i];
+    } else {  // NB = 2 / 12 / 13: the gamma^4 table comes precomputed after L and L^-1 (device_tables)
+        for (int i = threadIdx.x; i < (NB == 1 ? 2048 : 3072); i += 256) lt[i] = a.ltab[i];
     }
-    if constexpr (NB != 1) {
+    if constexpr (NB == 3) {
         __syncthreads();
         for (int i = threadIdx.x; i < 1024; i += 256)
             lt[LINV + G4 + i] = lt[LINV + 1024 + (i & ~255) + gmul_g4(i & 255)];
@@ -1788,7 +1790,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
               "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
               "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", RS_PF_SGPRS);
         m8_v1_store<1>(a, lt, RS_PF_DST, a0, a1, a0, a1);
-    } else if constexpr (NB == 2 || NB == 12 || NB == 13) {
+    } else if constexpr (NB == 2 || NB == 4 || NB == 12 || NB == 13) {
         u32x16 a0, a1, b0, b1;
 #define RS_PF1_OPS                                                                                                \
     : "=&{v[16:31]}"(a0), "=&{v[32:47]}"(a1), "=&{v[48:63]}"(b0), "=&{v[64:79]}"(b1)                               \
@@ -1798,6 +1800,10 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
         if constexpr (NB == 2) {
             asm volatile(
 #include "gen/m8_idx_asm_ps8pf1_kernel.inc"
+                RS_PF1_OPS);
+        } else if constexpr (NB == 4) {  // inputs already in coordinates (the fixed pass's masked form 2)
+            asm volatile(
+#include "gen/m8_idx_asm_ps8pf1c_kernel.inc"
                 RS_PF1_OPS);
 #ifdef RS_AMD_DIAG
         } else if constexpr (NB == 12) {  // timing ablation: no index switches (wrong results)
@@ -2460,7 +2466,7 @@ hipError_t launch_plan_syn_m8(const SynPlanArgs& a, int64_t n_sel, hipStream_t s
 hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, int tiles, hipStream_t st, int kernel,
                               int cpb) {
     if (n_sel <= 0 || tiles <= 0) return hipSuccess;
-    if (kernel >= 9 && kernel <= 13) {  // prefetching solves (two / one nibble tables / one table with read
+    if (kernel >= 9 && kernel <= 14) {  // prefetching solves (14: kernel 10 on coordinate inputs) (two / one nibble tables / one table with read
                                         // multiples): packed records, whole 1 KiB chunks only
         if (nbytes % 1024 || v.src_sym > 0xFFFFFFFFll) return hipErrorInvalidValue;
         V1Args f = v;
@@ -2475,8 +2481,11 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
             hipLaunchKernelGGL(k_apply_m8_pf<3>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         else
 #else
-        if (kernel != 10) return hipErrorInvalidValue;
+        if (kernel != 10 && kernel != 14) return hipErrorInvalidValue;
 #endif
+        if (kernel == 14)
+            hipLaunchKernelGGL(k_apply_m8_pf<4>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
+        else
             hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         return hipGetLastError();
     }

@@ -8,7 +8,7 @@ using namespace rsamd;
 namespace rsamd {
 
 struct DeviceTables {
-    uint32_t* d_ltab = nullptr;  // 2048 dwords, see ApplyArgs::ltab
+    uint32_t* d_ltab = nullptr;  // 3072 dwords, see ApplyArgs::ltab (+ the gamma^4 table of the one-table solves)
     uint16_t* d_log = nullptr;   // [65536] discrete log (device-built plans)
     uint16_t* d_exp = nullptr;   // [65536] alpha^i (entry 65535 = 1)
     uint8_t* d_g8 = nullptr;     // [256] gamma-basis byte of alpha^(257 e), e < 255
@@ -22,7 +22,7 @@ int device_tables(int device, const uint32_t** out) {
     DeviceTables& t = g_dev[device];
     if (!t.d_ltab) {
         const Gamma8& g = gamma8();
-        std::vector<uint32_t> h(2048);
+        std::vector<uint32_t> h(3072);
         for (int b = 0; b < 256; ++b) {
             h[b] = g.lbyte[0][b];
             h[256 + b] = g.lbyte[1][b];
@@ -32,6 +32,13 @@ int device_tables(int device, const uint32_t** out) {
             h[1280 + b] = g.ibyte[1][b];
             h[1536 + b] = uint32_t(g.ibyte[0][b]) << 16;
             h[1792 + b] = uint32_t(g.ibyte[1][b]) << 16;
+        }
+        // [2048, 3072): L^-1 of gamma^4 times each coordinate byte (the device's gmul_g4 / V1H_G4 table), so the
+        // one-table solves copy it instead of building it per workgroup
+        for (int i = 0; i < 1024; ++i) {
+            uint32_t v = uint32_t(i & 255);
+            for (int j = 0; j < 4; ++j) v = ((v << 1) & 0xFEu) ^ ((v >> 7) * 0x1Du);
+            h[2048 + i] = h[1024 + (i & ~255) + v];
         }
         void* p = nullptr;
         HIP_TRY(hipMalloc(&p, h.size() * 4));

@@ -13,7 +13,7 @@ struct V1Args {
     uint8_t* dst;
     int64_t dst_stripe, dst_sym;
     const int32_t* out_idx;  // [ntiles * 32] output symbol slots
-    const uint32_t* ltab;    // [2048] GF(256)^2 coordinate byte tables (L, L^-1)
+    const uint32_t* ltab;    // [3072] GF(256)^2 coordinate byte tables (L, L^-1, L^-1 of gamma^4 x)
     const uint32_t* idx;     // AOT: [ntiles][K][64] nibble indices (lo p, hi 32 + p)
     const int32_t* boff;     // JIT: [ntiles][K] byte offset of each input's lookup block
     int32_t K, R;

@@ -172,6 +172,8 @@ struct XjConfig {
     int masked = 0;    // 1 (set_masked; the per-stripe fixed pass of rsg_decode_batch): every input slot whose
                        // bit is set in the launch-local stripe's mask words reads a zero buffer instead
                        // (s_bitcmp1 + s_cselect_b64 on the load's base pair): erased slots count as zero
+    int coord = 0;     // 1 (set_masked(2)): the outputs are stored in GF(256)^2 coordinates (the L byte tables of
+                       // XJArgs::tab in LDS, four reads per output), the form the per-stripe solve consumes
     // env: read the RS_XJ_* generation knobs (experiments, the emulator tests through rsg_xj_source, the
     // diagnostic build). The kernels the release library launches are generated with the defaults
     // whatever the environment says, so no deployment's environment changes the shipped kernel.
@@ -222,8 +224,9 @@ struct XjConfig {
     }
     // masked loads exist for the default layout only (global loads with an SGPR base pair per input, one
     // column per block, plain block order)
-    void set_masked() {
+    void set_masked(int mode = 1) {
         masked = 1;
+        coord = mode == 2 ? 1 : 0;
         buffer = lds = lfin = share = xcd = spread = 0;
         cpb = 1;
         ring = 2;
@@ -253,7 +256,7 @@ struct XjConfig {
         if (splitwait) s += " splitwait";
         if (inlinefin) s += " inlinefin";
         if (prio) s += " prio";
-        if (masked) s += " masked";
+        if (masked) s += coord ? " masked coord" : " masked";
         return cpb > 1 ? s + " cpb" + std::to_string(cpb) + (cpb_sync ? " sync" : "") : s;
     }
 };
@@ -770,6 +773,31 @@ std::vector<std::string> role_block(const XjConfig& C, int w, const std::vector<
     } else {  // keep the network live: store accumulator 0 of each output
         for (int q = 0; q < nq; ++q) E.f("v_mov_b32 v%d, v%d", C.fin(q), C.acc(q, 0));
     }
+    if (C.coord) {
+        // outputs into GF(256)^2 coordinates: y = L0[b0] ^ L1[b1] ^ L2[b2] ^ L3[b3] over the bytes of each result
+        // (table k at LDS byte 1024 k, entry b at 4 b; the kernel's only LDS array, at 0), two outputs per round
+        // of 8 reads; the accumulators are dead after the finish and serve as address / read registers
+        for (int q0 = 0; q0 < nq; q0 += 2) {
+            const int nb = std::min(2, nq - q0);
+            for (int j = 0; j < nb; ++j) {
+                const int f = C.fin(q0 + j), t = C.acc(0, 0) + 4 * j;
+                E.f("v_lshlrev_b32 v%d, 2, v%d", t, f);
+                E.f("v_and_b32 v%d, 0x3fc, v%d", t, t);
+                for (int k = 1; k < 4; ++k) {
+                    E.f("v_lshrrev_b32 v%d, %d, v%d", t + k, 8 * k - 2, f);
+                    E.f("v_and_b32 v%d, 0x3fc, v%d", t + k, t + k);
+                }
+                E.f("ds_read_b32 v%d, v%d", t, t);
+                for (int k = 1; k < 4; ++k) E.f("ds_read_b32 v%d, v%d offset:%d", t + k, t + k, 1024 * k);
+            }
+            E.e("s_waitcnt lgkmcnt(0)");
+            for (int j = 0; j < nb; ++j) {
+                const int f = C.fin(q0 + j), t = C.acc(0, 0) + 4 * j;
+                E.f("v_xor_b32 v%d, v%d, v%d", f, t, t + 1);
+                E.f("v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96", f, f, t + 2, t + 3);
+            }
+        }
+    }
     for (int q0 = 0; q0 < nq; q0 += 8) {  // stores in batches of 8 address registers
         const int nb = std::min(8, nq - q0);
         for (int j = 0; j < nb; ++j) {
@@ -820,9 +848,9 @@ static void count_insts(const std::vector<std::string>& L, uint64_t mult, uint64
 }
 
 static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-               const std::vector<int32_t>& out_slots, bool masked, uint64_t* valu, uint64_t* salu) {
+               const std::vector<int32_t>& out_slots, int masked, uint64_t* valu, uint64_t* salu) {
     XjConfig C(R);
-    if (masked) C.set_masked();
+    if (masked) C.set_masked(masked);
     C.set_k(K);
     const XjBasis& B = xj_basis(C.horner);
     std::vector<uint8_t> cb(M.size());
@@ -838,9 +866,9 @@ static void xj_counts(const std::vector<uint16_t>& M, int K, int R, const std::v
 }
 
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots, bool env_knobs, bool masked) {
+                      const std::vector<int32_t>& out_slots, bool env_knobs, int masked) {
     XjConfig C(R, env_knobs);
-    if (masked) C.set_masked();
+    if (masked) C.set_masked(masked);
     C.set_k(K);
     int nmw = 0;  // mask words the loads test (slot / 32 < nmw)
     for (int32_t v : in_slots) nmw = std::max(nmw, v / 32 + 1);
@@ -878,8 +906,12 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
              "  const uint32_t col = chunk * 256u + (threadIdx.x & 63u) * 4u;\n";
     } else {
         o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds["
-          << (C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
+          << (C.coord ? 1024 : C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
+          << (C.coord ? "  if ((uint32_t)(unsigned long)xj_lds != 0u) return;\n"  // the reads address it absolutely
+                        "  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) xj_lds[i] = ((const uint32_t*)a.tab)[i];\n"
+                        "  __syncthreads();\n"
+                      : "")
           << (C.xcd ? "  const uint32_t xl = blockIdx.x + blockIdx.y * gridDim.x, xw = gridDim.x >> 3, xk = xl >> 3;\n"
                       "  const uint32_t by = xk / xw, bx = (xl & 7u) * xw + xk % xw;\n"
                       "  const uint64_t stripe = a.ids ? (uint64_t)a.ids[by] : (uint64_t)by;\n"
@@ -956,7 +988,7 @@ int xj_pairs(int R) {
 // (rocprofv3 Kernel_Name) tell the encode and decode kernels of one run apart; the same hash names
 // the kernel in rsg_last_kernel ("rs_xj[RxK:<hash>]").
 static std::string xj_named_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                                   const std::vector<int32_t>& out_slots, std::string* fname, bool masked = false) {
+                                   const std::vector<int32_t>& out_slots, std::string* fname, int masked = 0) {
     std::string src = xj_source(M, K, R, in_slots, out_slots, false, masked);
     char nm[32];
     std::snprintf(nm, sizeof nm, "rs_xj_%08llx", static_cast<unsigned long long>(jit_hash(src) & 0xffffffff));
@@ -968,7 +1000,7 @@ static std::string xj_named_source(const std::vector<uint16_t>& M, int K, int R,
 }
 
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                  const std::vector<int32_t>& out_slots, bool masked) {
+                  const std::vector<int32_t>& out_slots, int masked) {
     if (!xj_supported(8, K, R)) return 0;
     std::string fname;
     const std::string src = xj_named_source(M, K, R, in_slots, out_slots, &fname, masked);
@@ -977,7 +1009,7 @@ int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vecto
 }
 
 int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, bool masked) {
+             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, int masked) {
     out.reset();
     if (!xj_supported(8, K, R)) return 0;
     std::string fname;
@@ -989,10 +1021,11 @@ int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int
     k->mod = mod;
     (void)hipGetDevice(&k->device);
     k->roles = xj_roles(R);
-    k->masked = masked;
+    k->masked = masked != 0;
+    k->coord = masked == 2;
     {
         XjConfig C(R);
-        if (masked) C.set_masked();
+        if (masked) C.set_masked(masked);
         C.set_k(K);
         k->cpb = C.cpb;
         k->pairs = C.lfin ? xj_pairs(R) : 0;

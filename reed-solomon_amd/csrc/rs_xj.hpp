@@ -33,7 +33,8 @@ struct XJArgs {
     int64_t dst_stripe;
     int32_t src_sym, dst_sym;  // symbol strides (slot * stride < 2^31)
     const int32_t* ids;        // optional [n_stripes] stripe indices; null = 0..n-1
-    const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch)
+    const uint16_t* tab;       // persistent form (fin = 1): device table T[w] = gamma * w (set by xj_launch);
+                               // coordinate outputs (masked form 2): the 1024-dword L byte tables (ApplyArgs::ltab)
     uint32_t nchunks, ncols;   // chunks per stripe (set by xj_launch); persistent form: chunks in the launch
     uint32_t dst_local;        // 1: dst indexed by the launch-local stripe (ids only select the source)
     // masked kernels (xj_build(..., masked)): input slot i of launch-local stripe s reads the zero buffer when
@@ -53,6 +54,7 @@ struct XjKernel {
     int pairs = 0;  // > 0: persistent kernel (LDS finish), columns per workgroup in flight, grid <= CUs
     int cpb = 1;    // consecutive 256-byte columns per workgroup (column loop), grid.x = chunks / cpb
     bool masked = false;  // per-stripe input masks (XJArgs::masks)
+    bool coord = false;   // outputs stored in GF(256)^2 coordinates (masked form 2; XJArgs::tab = the L tables)
     std::string name;
     // wave instructions per 256-byte column, all role waves together, counted in the generated asm
     // (the XOR network, the finish once per role, loads / stores / addressing); the compiler's few
@@ -92,13 +94,14 @@ int xj_fin();                // generation setting (RS_XJ_FIN, default 0)
 int xj_pairs(int R);         // columns per workgroup (1 unless the LDS-table finish is on)
 // M: R x K GF(2^16) matrix (entries in GF(256)); in_slots[K] / out_slots[R] symbol slots.
 // env_knobs: honour the RS_XJ_* generation knobs (inspection / emulator tests; the launched kernels never do)
-// masked: the per-stripe input-mask form (XjConfig::masked, XJArgs::masks), default layout only
+// masked: 1 the per-stripe input-mask form (XjConfig::masked, XJArgs::masks), default layout only; 2 the same
+// with the outputs stored in GF(256)^2 coordinates (XjConfig::coord)
 std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                      const std::vector<int32_t>& out_slots, bool env_knobs = false, bool masked = false);
+                      const std::vector<int32_t>& out_slots, bool env_knobs = false, int masked = 0);
 int xj_build(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, bool masked = false);
+             const std::vector<int32_t>& out_slots, std::unique_ptr<XjKernel>& out, int masked = 0);
 int xj_precompile(const std::vector<uint16_t>& M, int K, int R, const std::vector<int32_t>& in_slots,
-                  const std::vector<int32_t>& out_slots, bool masked = false);
+                  const std::vector<int32_t>& out_slots, int masked = 0);
 // Launches over the first `nchunks` 256-byte column chunks of every stripe.
 int xj_launch(const XjKernel& k, const XJArgs& a, int64_t n_stripes, int64_t nchunks, hipStream_t st);
 

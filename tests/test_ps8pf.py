@@ -43,6 +43,11 @@ def pf1_lines(tmp_path_factory):
 
 
 @pytest.fixture(scope="module")
+def pf1c_lines(tmp_path_factory):
+    return gen_lines("ps8pf1c_kernel", tmp_path_factory.mktemp("pf1c"))
+
+
+@pytest.fixture(scope="module")
 def pf2_lines(tmp_path_factory):
     return gen_lines("ps8pf2_kernel", tmp_path_factory.mktemp("pf2"))
 
@@ -55,13 +60,13 @@ def xt8(m):
     return (((m << 1) & 0xFEFEFEFE) ^ (((m >> 7) & 0x01010101) * 0x1D)) & 0xFFFFFFFF
 
 
-def model(raw, lt, lo, hi, one_table=False):
+def model(raw, lt, lo, hi, one_table=False, preconverted=False):
     """raw [K][64] input dwords, lt [1024] coordinate tables, lo / hi [K][32] nibble indices -> acc [32][64]
     (one_table: [64][64], the low-nibble lookups of the table over y gamma^0..3, then the high-nibble ones)."""
     acc = np.zeros((64 if one_table else 32, 64), np.uint64)
     for i in range(raw.shape[0]):
         x = raw[i].astype(np.uint64)
-        y = lt[x & 255] ^ lt[256 + ((x >> 8) & 255)] ^ lt[512 + ((x >> 16) & 255)] ^ lt[768 + (x >> 24)]
+        y = x if preconverted else lt[x & 255] ^ lt[256 + ((x >> 8) & 255)] ^ lt[512 + ((x >> 16) & 255)] ^ lt[768 + (x >> 24)]
         m = [y]
         for _ in range(7):
             m.append(xt8(m[-1]))
@@ -95,12 +100,18 @@ def test_ps8pf1_loop_matches_model(pf1_lines, K):
 
 
 @pytest.mark.parametrize("K", KS)
+def test_ps8pf1c_loop_matches_model(pf1c_lines, K):
+    """The one-table loop over inputs already in coordinates (the fixed pass's masked form 2): y = the raw dword."""
+    run_case(pf1c_lines, K, True, preconverted=True)
+
+
+@pytest.mark.parametrize("K", KS)
 def test_ps8pf2_loop_matches_model(pf2_lines, K):
     """The one-table loop reading y gamma^1..3 from three more LDS tables (table j = xt8^j of table 0)."""
     run_case(pf2_lines, K, True, read_multiples=True)
 
 
-def run_case(pf_lines, K, one_table, read_multiples=False):
+def run_case(pf_lines, K, one_table, read_multiples=False, preconverted=False):
     rng = np.random.default_rng(1000 + K)
     S = 4096                 # input symbol stride (bytes)
     nslots = 48
@@ -135,7 +146,7 @@ def run_case(pf_lines, K, one_table, read_multiples=False):
     assert not w.vm and not w.lg, "loads left in flight at the end of the statement"
     raw = np.stack([mem.load32(np.uint64(src_base + int(s) * S + col) + 4 * np.arange(64, dtype=np.uint64))
                     for s in slots])
-    want = model(raw, lt, lo, hi, one_table)
+    want = model(raw, lt, lo, hi, one_table, preconverted)
     if read_multiples:
         assert not w.v[0].any(), "T[0] must stay zero"
     got = w.v[16:80] if one_table else w.v[32:64]

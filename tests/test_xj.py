@@ -241,3 +241,15 @@ def test_xj_masked_fixed_pass(k, r, kind, route):
         info[k:] = 0
         assert oracle_encode(k, r, info) == 0
         assert np.array_equal(got, info[k:] ^ zeroed[k:])
+    # masked form 2: the same outputs, each dword converted through the four byte tables at LDS 0 (the kernel's
+    # prologue copies XJArgs::tab there; any table checks the conversion wiring)
+    coord = xj_fixed_source(k, r, route, 2)
+    assert "masked coord" in coord and "ds_read_b32" in coord
+    tab = rng.integers(0, 1 << 32, 1024, dtype=np.uint64).astype(np.uint32)
+    mem2 = Memory(zero + S)
+    mem2.b[:n * S] = rcv.reshape(-1)
+    run_block(coord, mem2, 0, S, n * S, S, masks=words, zero=zero, lds_init=tab.astype("<u4").view(np.uint8))
+    x = got.reshape(r, S // 4, 4).copy().view("<u4").reshape(r, S // 4).astype(np.uint64)
+    want = tab[x & 255] ^ tab[256 + ((x >> 8) & 255)] ^ tab[512 + ((x >> 16) & 255)] ^ tab[768 + (x >> 24)]
+    got2 = mem2.b[n * S:(n + r) * S].reshape(r, S).copy().view("<u4").reshape(r, S // 4)
+    assert np.array_equal(got2, want.astype(np.uint32))

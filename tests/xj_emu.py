@@ -405,7 +405,8 @@ class Memory:
         self.b[idx.reshape(-1)] = np.ascontiguousarray(val, dtype="<u4").view(np.uint8)
 
 
-def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, gx=1, masks=None, zero=None):
+def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, gx=1, masks=None, zero=None,
+              lds_init=None):
     """Runs every role wave of block (chunk, stripe 0) of the generated kernel over `mem`
     (LDS base address 0; each role's ring region at role * region bytes). Column-loop kernels (cpb > 1)
     process `ncols` columns from `chunk`, `gx` (the grid's x size) columns apart. Masked kernels take the
@@ -418,6 +419,9 @@ def run_block(src, mem, src_base, src_sym, dst_base, dst_sym, chunk=0, ncols=1, 
         lds = gamma_table().copy()
     if "ds_write_b32" in src:  # shared table exchange between the roles
         lds = np.zeros(1 << 16, np.uint8)
+    if lds_init is not None:  # LDS contents the kernel's C prologue copies in (coordinate tables at 0)
+        lds = np.zeros(max(lds.size, lds_init.size), np.uint8)
+        lds[:lds_init.size] = lds_init
     col = (chunk * 256 + np.arange(64) * 4).astype(np.uint32)
     waves, segments = [], []
     for w, lines in enumerate(roles):
