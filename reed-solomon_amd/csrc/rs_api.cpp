@@ -205,6 +205,9 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     if (!std::strcmp(name, "m8_syn_coord")) {  // fixed pass stores coordinates for solve 10 (1) or not (0)
         if (value < 0 || value > 1) return RS_ERR_INVALID;
+#ifndef RS_AMD_DIAG
+        if (value) return RS_ERR_INVALID;  // measured slower: diagnostic build
+#endif
         if (int(value) != c->m8_syn_coord) syn_reform();
         c->m8_syn_coord = int(value);
         return 0;

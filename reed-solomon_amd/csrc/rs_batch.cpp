@@ -87,9 +87,9 @@ bool syn_prepare(rsg_codec_t* c, uint64_t S, int64_t symbol_stride) {
             c->syn_failed = true;
             return false;
         }
-        // the masked form (default): each stripe's erased slots read as zero (XJArgs::masks); with the prefetching
-        // solve 10 (whose slot lists need 19 entries past K: K <= min(k, r) or r), its outputs stored in
-        // coordinates (form 2), so the solve reads them as they are
+        // the masked form (default): each stripe's erased slots read as zero (XJArgs::masks); option m8_syn_coord
+        // (diagnostic): with the prefetching solve 10 (whose slot lists need 19 entries past K: K <= min(k, r) or
+        // r), its outputs stored in coordinates (form 2), which the solve then reads as they are
         const int kmax = c->syn_route == 2 ? std::min<int>(c->k, c->r) : int(c->r);
         const bool coord = c->m8_syn_masked && c->m8_syn_coord && c->m8_ps_kernel == 10 && kmax + 3 <= n;
         if (xj_build(p->matrix, p->K, p->R, p->in_slots, p->out_slots, p->xj, c->m8_syn_masked ? (coord ? 2 : 1) : 0) ||
@@ -988,9 +988,7 @@ extern "C" int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route) {
     std::vector<int32_t> in(static_cast<size_t>(n)), out(static_cast<size_t>(r));
     for (int i = 0; i < n; ++i) in[size_t(i)] = i;
     for (int j = 0; j < r; ++j) out[size_t(j)] = j;
-    // the codec's default form: masked, coordinate outputs when the prefetching solve takes them
-    const int kmax = route == 2 ? std::min<int>(k, r) : int(r);
-    return xj_precompile(syn_fixed_matrix(pos, k, r, route), n, r, in, out, kmax + 3 <= n ? 2 : 1);
+    return xj_precompile(syn_fixed_matrix(pos, k, r, route), n, r, in, out, 1);  // the codec's default form
 }
 
 extern "C" int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf, size_t cap, size_t* len) {

@@ -323,9 +323,11 @@ struct rsg_codec {
     // rs_xj) and the solve stores the erased symbols; 0 the plain pass over the slots as they are and a solve
     // that XORs its result into them (one old-value load per output)
     int m8_syn_masked = 1;
-    // option m8_syn_coord: 1 (default) with the masked pass and solve 10, the fixed pass stores its outputs in
-    // GF(256)^2 coordinates and the solve reads them as they are (k_apply_m8_pf<4>); 0 the solve converts
-    int m8_syn_coord = 1;
+    // option m8_syn_coord (diagnostic build): 1 with the masked pass and solve 10, the fixed pass stores its
+    // outputs in GF(256)^2 coordinates and the solve reads them as they are (k_apply_m8_pf<4>); 0 (default) the
+    // solve converts. Measured 5-10 % slower: the tiny XOR-kernel workgroups each copy the tables and wait on
+    // their reads
+    int m8_syn_coord = 0;
     // option m8_syn_scratch_mib: fixed-pass output scratch of the GF(256) per-stripe route per chunk of stripes
     // (r x S bytes per stripe; the chunk count sets the launch count)
     int64_t syn_scratch_mib = 1024;

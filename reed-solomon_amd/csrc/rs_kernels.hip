@@ -1728,8 +1728,9 @@ __global__ void __launch_bounds__(256) k_plan_reenc_m8(SynPlanArgs a) {
 // NB = 1: two nibble tables per input (gen_asm.py ps8pf_kernel, 78 VGPRs, 6 waves per SIMD); NB = 2: one table
 // over y gamma^0..3 with the high-nibble lookups in a second accumulator set (ps8pf1_kernel: 4 multiples and a
 // table less per input, 5 waves per SIMD), the output stage adding gamma^4 times it through a third LDS table.
-// NB = 4 (ps8pf1c_kernel, launched as 14): NB = 2 over inputs the fixed pass stored in coordinates already
-// (rs_xj masked form 2, which converts its 32 outputs with the same LDS tables): no coordinate reads per step.
+// NB = 4 (ps8pf1c_kernel, launched as 14; diagnostic build, option m8_syn_coord): NB = 2 over inputs the fixed
+// pass stored in coordinates already (rs_xj masked form 2, which converts its outputs with the same LDS tables):
+// no coordinate reads per step, but the pass's conversion costs more than the solve saves.
 // NB = 3 (ps8pf2_kernel): NB = 2 with the multiples y gamma^1..3 read from three more coordinate tables
 // (gamma^j L(x) = L(gamma^j x) is linear in x's bytes: table j entry = xt8^j of table 0's) instead of computed;
 // LDS: tables j = 0..3 at dword 1024 j, L^-1 at 4096, the gamma^4 table at 5120. NB = 2 issues fastest (the
@@ -2479,13 +2480,12 @@ hipError_t launch_apply_m8_ps(const V1Args& v, int64_t n_sel, int64_t nbytes, in
                                dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         else if (kernel == 11)
             hipLaunchKernelGGL(k_apply_m8_pf<3>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
-        else
-#else
-        if (kernel != 10 && kernel != 14) return hipErrorInvalidValue;
-#endif
-        if (kernel == 14)
+        else if (kernel == 14)  // coordinate inputs (option m8_syn_coord)
             hipLaunchKernelGGL(k_apply_m8_pf<4>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         else
+#else
+        if (kernel != 10) return hipErrorInvalidValue;
+#endif
             hipLaunchKernelGGL(k_apply_m8_pf<2>, dim3(unsigned(n_sel * f.nchunks), unsigned(tiles)), dim3(256), 0, st, f);
         return hipGetLastError();
     }

@@ -72,6 +72,8 @@ if os.environ.get("RS_PS8_KERNEL"):  # A/B of the per-stripe solve kernel (optio
     syn.set_option("m8_ps_kernel", int(os.environ["RS_PS8_KERNEL"]))
 if os.environ.get("RS_PS8_MASKED"):  # A/B of the masked fixed pass (option m8_syn_masked)
     syn.set_option("m8_syn_masked", int(os.environ["RS_PS8_MASKED"]))
+if os.environ.get("RS_PS8_COORD"):  # A/B of the coordinate-output fixed pass (option m8_syn_coord)
+    syn.set_option("m8_syn_coord", int(os.environ["RS_PS8_COORD"]))
 if os.environ.get("RS_PS8_SCRATCH"):  # A/B of the fixed-pass scratch per chunk (option m8_syn_scratch_mib)
     syn.set_option("m8_syn_scratch_mib", int(os.environ["RS_PS8_SCRATCH"]))
 if os.environ.get("RS_PS8_ABLATE"):  # timing ablations of the solve (diagnostic library, option m8_ps_ablate)

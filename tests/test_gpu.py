@@ -696,7 +696,8 @@ def test_decode_batch_syndrome_route_unmasked(k, r, S, n, route, kern):
     syndrome_route_case(rs_amd, k, r, S, n, route, 0, kern, 1, masked=0)
 
 
-def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1):
+
+def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1, coord=0):
     """Device-built per-stripe decodes through the syndrome route (route 1: r syndromes of every slot on
     the XOR kernel, then each stripe's t_info x t solve XORed into the erased slots, which are not zeroed
     first; route 2: the re-encode differences [G | I] of every slot, then a t_info x t_info Cauchy-inverse
@@ -722,6 +723,8 @@ def syndrome_route_case(lib, k, r, S, n, route, ovl, kern, cpb, masked=1):
     codec.set_option("m8_ps_kernel", kern)  # 1: the ring-free per-stripe solve kernel (k_apply_m8_ps_w)
     codec.set_option("m8_ps_cpb", cpb)
     codec.set_option("m8_syn_masked", masked)
+    if coord:
+        codec.set_option("m8_syn_coord", coord)
     codec.encode(dev)
     pats = np.zeros((n, k + r), bool)
     for s in range(n):
@@ -1411,7 +1414,7 @@ def test_release_build_ignores_diagnostic_knobs():
     # ablations / stamps, and (round 5) the option-only A/B families, overlap variants and block layouts
     for name, value in ([("m8_mode", v) for v in (0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 15, 16, 17, 19, 21)]
                         + [("m16_mode", 1), ("stamp_buffer", 1), ("m16_cs_col", 1024), ("m16_cs_overlap", 1),
-                           ("m8_syn_overlap", 1), ("m8_ps_cpb", 2)]
+                           ("m8_syn_overlap", 1), ("m8_ps_cpb", 2), ("m8_syn_coord", 1)]
                         + [("m8_ps_kernel", v) for v in (1, 2, 4, 5, 6, 7, 8, 9, 11)]):
         with pytest.raises(rs_amd.RSError):
             codec.set_option(name, value)

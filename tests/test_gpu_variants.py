@@ -53,6 +53,14 @@ def test_decode_batch_syndrome_route_diag(k, r, S, n, route, ovl, kern, cpb):
     syndrome_route_case(rs_amd.diag_module(), k, r, S, n, route, ovl, kern, cpb)
 
 
+@pytest.mark.parametrize("route", [1, 2])
+@pytest.mark.parametrize("k,r,S,n", SYN_ROUTE_SHAPES)
+def test_decode_batch_syndrome_route_coord(k, r, S, n, route):
+    """Option m8_syn_coord 1 (diagnostic library): the masked fixed pass stores GF(256)^2 coordinates and the
+    prefetching solve reads them as they are (k_apply_m8_pf<4>)."""
+    syndrome_route_case(rs_amd.diag_module(), k, r, S, n, route, 0, 10, 1, coord=1)
+
+
 @pytest.mark.parametrize("k,r,S,n", [(1000, 200, 2048, 37), (300, 64, 3072, 16)])
 def test_cs16_overlapped_chunks_match_serial(k, r, S, n):
     cs16_overlapped_case(k, r, S, n)

@@ -93,7 +93,7 @@ def _kernel_names(path):
 DIAG_ONLY = ("k_apply_m8ILi", "k_apply_m8_lds", "k_apply_m8_ps_w", "k_apply_m8_idxILi0ELi8E", "k_apply_m8_idxILi4E",
              "k_apply_m8_v1ILi1E", "k_apply_m8_v1ILi3E", "k_apply_m8_v1ILi4E", "k_apply_m8_v1ILi5E", "k_apply_m8_v1ILi6E",
              "k_apply_m16_v1ILi1E", "k_apply_m8_pfILi1E", "k_apply_m8_pfILi3E", "k_apply_m8_pfILi12E",
-             "k_apply_m8_pfILi13E")
+             "k_apply_m8_pfILi13E", "k_apply_m8_pfILi4E")
 # every production kernel (the release library carries exactly these)
 PRODUCTION = ("k_apply_m8_v1ILi0E", "k_apply_m8_v1ILi2E", "k_apply_m8_idxILi0ELi4E", "k_apply_m8_ps_tail", "k_apply_m8_pf", "k_xor_slices",
               "k_apply_m16ILi16E", "k_apply_m16ILi32E", "k_apply_m16ILi64E", "k_apply_m16_v1ILi0E", "k_cs16E", "k_cs16tE",
