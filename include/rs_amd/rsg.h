@@ -70,8 +70,8 @@ int rsg_codec_subfield(const rsg_codec_t* c);
  *   "m8_syn_masked" 1 the fixed pass reads each stripe's erased slots as zero and the solve stores (default);
  *                  0 the pass reads the slots as they are and the solve XORs its result into them
  *   "m8_syn_scratch_mib" fixed-pass scratch per chunk of stripes (MiB, default 1024; sets the launch count)
- *   "m8_syn_coord" 1 (default) with the masked pass and solve 10: the pass stores its outputs in GF(256)^2
- *                  coordinates and the solve reads them as they are; 0 the solve converts its inputs
+ *   "m8_syn_coord" 0 the solve converts its inputs (default); [diag] 1 with the masked pass and solve 10: the
+ *                  pass stores its outputs in GF(256)^2 coordinates and the solve reads them as they are
  *   "m8_ps_cpb"    1 KiB column chunks per workgroup of solve kernel 0: 1 (default); [diag] 2-64 walk a
  *                  stripe's chunks in one workgroup (table setup once, next chunk's ring prologue under the
  *                  outputs)
