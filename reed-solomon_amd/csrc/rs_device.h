@@ -221,6 +221,50 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
     }
 }
 
+// The one-table solves' store stage (k_apply_m8_pf, stored outputs): output p = L^-1(A_p) ^ G4(B_p) as eight LDS
+// reads folded by three-input XORs (v_bitop3: 4 VALU instead of 7), stored at base + slot * dst_sym + voff with the
+// row address formed in SGPRs (base and the slots are uniform) and the lane's byte offset as the store's VGPR
+// offset, so a store costs no VALU. Same order and same-address rule as m8_v1_store's store path.
+template <int G4>
+__device__ __forceinline__ uint32_t m8_v1h_out(const uint32_t* lt, uint32_t x, uint32_t y) {
+    const uint32_t* li = lt + 1024;
+    const uint32_t* g = lt + G4;
+    const uint32_t r0 = li[x & 255u], r1 = li[256 + ((x >> 8) & 255u)], r2 = li[512 + ((x >> 16) & 255u)],
+                   r3 = li[768 + (x >> 24)];
+    const uint32_t r4 = g[y & 255u], r5 = g[256 + ((y >> 8) & 255u)], r6 = g[512 + ((y >> 16) & 255u)],
+                   r7 = g[768 + (y >> 24)];
+    uint32_t w = __builtin_amdgcn_bitop3_b32(r0, r1, r2, 0x96);
+    w = __builtin_amdgcn_bitop3_b32(w, r3, r4, 0x96);
+    w = __builtin_amdgcn_bitop3_b32(w, r5, r6, 0x96);
+    return w ^ r7;
+}
+
+template <int G4>
+__device__ __forceinline__ void m8_v1h_store(const V1Args& a, const uint32_t* lt, uint8_t* base, uint32_t voff,
+                                             const int32_t* out, int rows, const u32x16& a0, const u32x16& a1,
+                                             const u32x16& b0, const u32x16& b1) {
+    i32x16s o0, o1;
+    sload32(out, o0, o1);
+    auto slot = [&](int p) { return p < 16 ? o0[p & 15] : o1[p & 15]; };
+    const int32_t slast = sload(out + (rows - 1));
+#pragma unroll
+    for (int p0 = 24; p0 >= 0; p0 -= 8) {
+        if (p0 >= rows) continue;  // a whole group past the tile's rows (uniform): not converted
+        uint32_t w[8];
+#pragma unroll
+        for (int q = 7; q >= 0; --q) {
+            const int p = p0 + q;
+            w[q] = m8_v1h_out<G4>(lt, p < 16 ? a0[p & 15] : a1[p & 15], p < 16 ? b0[p & 15] : b1[p & 15]);
+        }
+#pragma unroll
+        for (int q = 7; q >= 0; --q) {
+            const int32_t sl = p0 + q < rows ? slot(p0 + q) : slast;
+            uint8_t* d = base + int64_t(uint32_t(RS_SLOT_OK(a, sl, 2, p0 + q) ? sl : 0)) * a.dst_sym;  // slots >= 0
+            asm volatile("global_store_dword %0, %1, %2" ::"v"(voff), "v"(w[q]), "s"(d) : "memory");
+        }
+    }
+}
+
 // Block = 256 lanes x 4 B = one 1 KiB column chunk of one stripe, 32 output rows of tile
 // blockIdx.y. Per batch of 4 inputs: wave (i % 4) issues input i's DMA RING_B batches ahead; every
 // wave reads its 4 dwords from the ring, maps them to GF(256)^2 coordinates (LDS byte tables) and

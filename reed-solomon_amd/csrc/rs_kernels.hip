@@ -1774,6 +1774,19 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
     // the output stage's operands are formed after the loop (nothing of the kernel's own lives across it)
 #define RS_PF_DST a.dst + stripe * a.dst_stripe + chunk * 1024 + int64_t(threadIdx.x) * 4, \
                   a.out_idx + local * a.ps_out + tile * 32, min(32, R - tile * 32)
+    // stored outputs (the masked pass): the SGPR-addressed store stage; XORed outputs (and the diagnostic output
+    // ablation) through m8_v1_store
+#ifdef RS_AMD_DIAG
+    const bool plain_store = !a.xor_dst && !(a.ablate & 2);
+#else
+    const bool plain_store = !a.xor_dst;
+#endif
+#define RS_PF_STORE(LT)                                                                                           \
+    if (plain_store)                                                                                              \
+        m8_v1h_store<G4>(a, LT, a.dst + stripe * a.dst_stripe + chunk * 1024, threadIdx.x * 4u,                   \
+                         a.out_idx + local * a.ps_out + tile * 32, min(32, R - tile * 32), a0, a1, b0, b1);       \
+    else                                                                                                          \
+        m8_v1_store<2, 0, G4>(a, LT, RS_PF_DST, a0, a1, b0, b1)
 #define RS_PF_IN                                                                                                  \
     [rec] "s"(rec), [pin] "s"(pin), [nk] "s"(K), [sym] "s"(uint32_t(a.src_sym)), [rsrc] "s"(rsrc), [col] "v"(col)
 #define RS_PF_SGPRS                                                                                               \
@@ -1818,7 +1831,7 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
 #endif
         }
 #undef RS_PF1_OPS
-        m8_v1_store<2, 0, G4>(a, lt, RS_PF_DST, a0, a1, b0, b1);
+        RS_PF_STORE(lt);
     } else {
         u32x16 a0, a1, b0, b1;
         asm volatile(
@@ -1828,8 +1841,9 @@ __global__ void __launch_bounds__(256) k_apply_m8_pf(V1Args a) {
             : "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
               "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94",
               "v95", "v96", "v97", "v98", "v99", "v100", RS_PF_SGPRS);
-        m8_v1_store<2, 0, G4>(a, lt + LINV, RS_PF_DST, a0, a1, b0, b1);
+        RS_PF_STORE(lt + LINV);
     }
+#undef RS_PF_STORE
 #undef RS_PF_DST
 #undef RS_PF_IN
 #undef RS_PF_SGPRS
