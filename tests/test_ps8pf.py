@@ -4,7 +4,8 @@ The generated asm statement runs in the instruction emulator (tests/xj_emu.py) w
 reads landing only at the waits that retire them, so a register named while its load is in flight fails
 the test, as does a wrong wait count on the raw-input ring. The accumulators it leaves are compared with a
 numpy model of the V = 1 step (coordinate lookup, gamma multiples, nibble tables, lookups), for input counts
-that end the loop at every step position and past the slot-block and record-bank turnovers.
+that end the loop at every step position and past the slot-block and record-bank turnovers. The accumulators
+start as garbage (the statement must zero them itself).
 """
 import os
 import re
@@ -142,6 +143,8 @@ def run_case(pf_lines, K, one_table, read_multiples=False, preconverted=False):
                rsrc=(src_base, nslots * S))
     w = Wave(mem, ops, lgkm=True)
     w.lds = lds
+    # accumulators hold garbage on entry: the statement zeroes them first
+    w.v[16:80] = rng.integers(0, 1 << 32, w.v[16:80].shape, dtype=np.uint64).astype(w.v.dtype)
     w.run(pf_lines, [])
     assert not w.vm and not w.lg, "loads left in flight at the end of the statement"
     raw = np.stack([mem.load32(np.uint64(src_base + int(s) * S + col) + 4 * np.arange(64, dtype=np.uint64))
