@@ -188,20 +188,22 @@ void orc_positions(uint16_t k, uint16_t r, uint16_t* positions) {
 }
 
 /* ---------------------------------------------------------------- symbol-wide ops ----------
- * gf_add / gf_mul / gf_madd: src/rs/gf65536.c:155-219 (little-endian uint16 words). */
+ * gf_add / gf_mul / gf_madd: src/rs/gf65536.c:155-219 (little-endian uint16 words), with the
+ * reference's cost structure: gf_add is a 64-bit XOR loop with a 16-bit tail (:161-169), gf_mul /
+ * gf_madd read and write whole 16-bit words through pow_table shifted by log(c), skipping zero
+ * words (:186-193, :211-218). The word types are alias-safe and alignment-free, so any byte offset
+ * works (x86-64 and the compilers here do unaligned word access natively). */
+typedef uint64_t __attribute__((may_alias, aligned(1))) u64w;
+typedef uint16_t __attribute__((may_alias, aligned(1))) u16w;
+
 static void sym_xor(uint8_t* a, const uint8_t* b, size_t S) {
+    u64w* x = (u64w*)a;
+    const u64w* y = (const u64w*)b;
     size_t n8 = S / 8, i;
-    for (i = 0; i < n8; ++i) {
-        uint64_t x, y;
-        memcpy(&x, a + 8 * i, 8);
-        memcpy(&y, b + 8 * i, 8);
-        x ^= y;
-        memcpy(a + 8 * i, &x, 8);
-    }
-    for (i = n8 * 8; i + 1 < S; i += 2) {
-        a[i] ^= b[i];
-        a[i + 1] ^= b[i + 1];
-    }
+    for (i = 0; i < n8; ++i) x[i] ^= y[i];
+    u16w* x2 = (u16w*)(a + 8 * n8);
+    const u16w* y2 = (const u16w*)(b + 8 * n8);
+    for (i = 0; i < (S - 8 * n8) / 2; ++i) x2[i] ^= y2[i];
 }
 
 static void sym_madd(uint8_t* a, uint16_t c, const uint8_t* b, size_t S) {
@@ -211,12 +213,11 @@ static void sym_madd(uint8_t* a, uint16_t c, const uint8_t* b, size_t S) {
         return;
     }
     const uint16_t* shifted = g_exp + g_log[c];
-    for (size_t i = 0; i + 1 < S; i += 2) {
-        uint16_t w = (uint16_t)(b[i] | (b[i + 1] << 8));
-        if (!w) continue;
-        uint16_t p = shifted[g_log[w]];
-        a[i] ^= (uint8_t)p;
-        a[i + 1] ^= (uint8_t)(p >> 8);
+    u16w* x = (u16w*)a;
+    const u16w* y = (const u16w*)b;
+    for (size_t i = 0, n = S / 2; i < n; ++i) {
+        uint16_t w = y[i];
+        if (w) x[i] ^= shifted[g_log[w]];
     }
 }
 
@@ -227,12 +228,10 @@ static void sym_scale(uint8_t* a, uint16_t c, size_t S) {
         return;
     }
     const uint16_t* shifted = g_exp + g_log[c];
-    for (size_t i = 0; i + 1 < S; i += 2) {
-        uint16_t w = (uint16_t)(a[i] | (a[i + 1] << 8));
-        if (!w) continue;
-        uint16_t p = shifted[g_log[w]];
-        a[i] = (uint8_t)p;
-        a[i + 1] = (uint8_t)(p >> 8);
+    u16w* x = (u16w*)a;
+    for (size_t i = 0, n = S / 2; i < n; ++i) {
+        uint16_t w = x[i];
+        if (w) x[i] = shifted[g_log[w]];
     }
 }
 
@@ -240,31 +239,43 @@ static void sym_scale(uint8_t* a, uint16_t c, size_t S) {
  * Syndromes S_j = sum_i f_i * alpha^(pos_i * j), j < L, by the cyclotomic FFT of
  * src/rs/fft.c:39-100: for every coset {s, 2s, 4s, ...} of a syndrome index, accumulate each
  * input into the normal-basis slots u_t selected by the bits of alpha^(s*pos_i), then combine
- * S_(2^j s) = sum_t nb_((j+t) mod m) * u_t. scratch holds 16 symbols. */
-static void syndromes(const uint8_t* const* f, const uint16_t* pos, size_t nf, size_t S, uint8_t* const* res,
-                      size_t L, uint8_t* scratch) {
+ * S_(2^j s) = sum_t nb_((j+t) mod m) * u_t; u is a 16-symbol sequence per call (fft.c:53). */
+static uint8_t** seq_alloc(size_t n, size_t S);
+static void seq_free(uint8_t** v, size_t n);
+
+static int syndromes(const uint8_t* const* f, const uint16_t* pos, size_t nf, size_t S, uint8_t* const* res,
+                     size_t L) {
     uint8_t* done = calloc(L ? L : 1, 1);
+    uint8_t** u = seq_alloc(16, S);
+    if (!done || !u) {
+        free(done);
+        seq_free(u, 16);
+        return 1;
+    }
     for (size_t s = 0; s < L; ++s) {
         if (done[s]) continue;
         uint8_t m = orc_coset_size((uint16_t)s);
         const uint16_t* nb = nb_of(m);
-        memset(scratch, 0, (size_t)m * S);
+        const uint16_t* repr = g_nrepr[lg2m(m)];
+        for (int t = 0; t < m; ++t) memset(u[t], 0, S);
         for (size_t i = 0; i < nf; ++i) {
-            uint16_t bits = orc_normal_repr(m, (uint16_t)(((uint32_t)s * pos[i]) % ORC_N));
+            uint16_t bits = repr[((uint32_t)s * pos[i]) % ORC_N];
             for (int t = 0; t < m; ++t)
-                if (bits & (1u << t)) sym_xor(scratch + (size_t)t * S, f[i], S);
+                if (bits & (1u << t)) sym_xor(u[t], f[i], S);
         }
         uint32_t idx = (uint32_t)s;
         for (int j = 0; j < m; ++j) {
             if (idx < L) {
                 memset(res[idx], 0, S);
-                for (int t = 0; t < m; ++t) sym_madd(res[idx], nb[(j + t) % m], scratch + (size_t)t * S, S);
+                for (int t = 0; t < m; ++t) sym_madd(res[idx], nb[(j + t) % m], u[t], S);
                 done[idx] = 1;
             }
             idx = dbl((uint16_t)idx);
         }
     }
     free(done);
+    seq_free(u, 16);
+    return 0;
 }
 
 /* Locator Lambda(x) = prod_e (1 + X_e x): src/rs/reed_solomon.c:83-102 (for the repair set the
@@ -298,6 +309,26 @@ static uint16_t forney(const uint16_t* lam, size_t d, uint16_t p) {
 }
 
 /* ---------------------------------------------------------------- encode / decode ----------*/
+/* Temporaries allocated as the reference allocates them: seq_create callocs every symbol on its own
+ * (src/memory/seq.c:17-46, symbol.c:17-32), per call (reed_solomon.c:384-402, fft.c:53,143), so the
+ * port pays the same allocation and first-touch cost as the reference. */
+static void seq_free(uint8_t** v, size_t n) {
+    if (!v) return;
+    for (size_t i = 0; i < n; ++i) free(v[i]);
+    free(v);
+}
+
+static uint8_t** seq_alloc(size_t n, size_t S) {
+    uint8_t** v = calloc(n ? n : 1, sizeof(uint8_t*));
+    if (!v) return NULL;
+    for (size_t i = 0; i < n; ++i)
+        if (!(v[i] = calloc(S ? S : 1, 1))) {
+            seq_free(v, n);
+            return NULL;
+        }
+    return v;
+}
+
 static uint8_t** carve(uint8_t* base, size_t n, size_t S) {
     uint8_t** v = malloc((n ? n : 1) * sizeof(uint8_t*));
     if (!v) return NULL;
@@ -314,47 +345,44 @@ int orc_encode(uint16_t k, uint16_t r, size_t S, const uint8_t* const* info, uin
     uint16_t ci = orc_cosets_upper(k), cr = orc_cosets_upper(r);
     uint16_t *il = calloc(ci + 1, 2), *rl = calloc(cr + 1, 2);
     uint8_t *is = calloc(ci + 1, 1), *rsz = calloc(cr + 1, 1);
-    uint8_t* mem = calloc(((size_t)2 * r + 16) * S + 1, 1);
-    uint8_t **syn = NULL, **om = NULL;
-    if (!pos || !lam || !il || !rl || !is || !rsz || !mem) goto out;
-    syn = carve(mem, r, S);
-    om = carve(mem + (size_t)r * S, r, S);
-    if (!syn || !om) goto out;
-    uint8_t* scratch = mem + (size_t)2 * r * S;
+    uint8_t **syn = seq_alloc(r, S), **om = seq_alloc(r, S), **u = NULL;
+    if (!pos || !lam || !il || !rl || !is || !rsz || !syn || !om) goto out;
 
     uint16_t ni = 0, nr = 0;
     orc_select_cosets(k, r, il, is, &ni, rl, rsz, &nr);
     expand(il, ni, pos, k);
     expand(rl, nr, pos + k, r);
 
-    syndromes(info, pos, k, S, syn, r, scratch);
+    if (syndromes(info, pos, k, S, syn, r)) goto out;
     locator(pos + k, r, lam);
     evaluator(syn, lam, r, S, om);
 
     /* _rs_get_repair_symbols (:260-286) via fft_partial_transform_cycl (fft.c:126-177):
      * evaluate Omega at alpha^(-L*2^j) per repair coset with normal-basis slots, then Forney. */
+    if (!(u = seq_alloc(16, S))) goto out;
     size_t o = 0;
     for (uint16_t c = 0; c < nr; ++c) {
         uint8_t m = rsz[c];
         const uint16_t* nb = nb_of(m);
+        const uint16_t* repr = g_nrepr[lg2m(m)];
         uint32_t s = ORC_N - rl[c];
-        memset(scratch, 0, (size_t)m * S);
+        for (int t = 0; t < m; ++t) memset(u[t], 0, S);
         for (uint32_t i = 0; i < r; ++i) {
-            uint16_t bits = orc_normal_repr(m, (uint16_t)((s * i) % ORC_N));
+            uint16_t bits = repr[(s * i) % ORC_N];
             for (int t = 0; t < m; ++t)
-                if (bits & (1u << t)) sym_xor(scratch + (size_t)t * S, om[i], S);
+                if (bits & (1u << t)) sym_xor(u[t], om[i], S);
         }
         for (int j = 0; j < m; ++j, ++o) {
             memset(rep[o], 0, S);
-            for (int t = 0; t < m; ++t) sym_madd(rep[o], nb[(j + t) % m], scratch + (size_t)t * S, S);
+            for (int t = 0; t < m; ++t) sym_madd(rep[o], nb[(j + t) % m], u[t], S);
         }
     }
     for (size_t i = 0; i < r; ++i) sym_scale(rep[i], forney(lam, r, pos[k + i]), S);
     rc = 0;
 out:
-    free(syn);
-    free(om);
-    free(mem);
+    seq_free(syn, r);
+    seq_free(om, r);
+    seq_free(u, 16);
     free(pos);
     free(lam);
     free(il);
@@ -375,15 +403,11 @@ int orc_decode(uint16_t k, uint16_t r, size_t S, uint8_t* const* rcv, const bool
     uint16_t* pos = calloc(n + 1, sizeof(uint16_t));
     uint16_t* epos = calloc((size_t)t + 1, sizeof(uint16_t));
     uint16_t* lam = calloc((size_t)t + 2, sizeof(uint16_t));
-    uint8_t* mem = calloc(((size_t)2 * t + 16) * S + 1, 1);
-    uint8_t **syn = NULL, **om = NULL;
-    if (!pos || !epos || !lam || !mem) goto out;
-    syn = carve(mem, t, S);
-    om = carve(mem + (size_t)t * S, t, S);
-    if (!syn || !om) goto out;
+    uint8_t **syn = seq_alloc(t, S), **om = seq_alloc(t, S);
+    if (!pos || !epos || !lam || !syn || !om) goto out;
 
     orc_positions(k, r, pos);
-    syndromes((const uint8_t* const*)rcv, pos, n, S, syn, t, mem + (size_t)2 * t * S);
+    if (syndromes((const uint8_t* const*)rcv, pos, n, S, syn, t)) goto out;
     size_t ne = 0;
     for (size_t i = 0; i < n && ne < t; ++i)
         if (erased[i]) epos[ne++] = pos[i];
@@ -401,9 +425,8 @@ int orc_decode(uint16_t k, uint16_t r, size_t S, uint8_t* const* rcv, const bool
     }
     rc = 0;
 out:
-    free(syn);
-    free(om);
-    free(mem);
+    seq_free(syn, t);
+    seq_free(om, t);
     free(pos);
     free(epos);
     free(lam);
