@@ -182,7 +182,8 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
     }
     // the per-stripe fixed pass's form follows these options: a change rebuilds it at the next call
     auto syn_reform = [c]() {
-        if (c->syn && c->syn->xj) (void)hipDeviceSynchronize();  // the old pass may still be queued
+        if (c->syn && c->syn->xj && hipSetDevice(c->device) == hipSuccess)
+            (void)hipDeviceSynchronize();  // the old pass may still be queued (on the codec's device)
         c->syn.reset();
         c->syn_failed = false;
     };
@@ -221,6 +222,11 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
         return 0;
     }
 #ifdef RS_AMD_DIAG
+    if (!std::strcmp(name, "inject_fail_group")) {  // failure injection: rsg_decode_batch's grouping path
+        if (value < -1 || value > 65535) return RS_ERR_INVALID;
+        c->inject_fail_group = value;
+        return 0;
+    }
     if (!std::strcmp(name, "m8_ps_ablate")) {  // timing ablations of the per-stripe solve (wrong results)
         if (value < 0 || value > 3) return RS_ERR_INVALID;
         c->m8_ps_ablate = int(value);
@@ -652,6 +658,26 @@ int scratch_release(rsg_codec_t* c, hipStream_t st) {
     c->scratch_pending = true;
     c->scratch_stream = st;
     return 0;
+}
+
+// A route that fails after its first launch returns with work still queued (on st, and on the codec's side
+// and syndrome streams for the per-stripe routes) and without marking the scratch busy: join those streams
+// into st and mark the scratch as used by st, so the next call (on any stream) waits for the orphaned kernels
+// before it overwrites lists, records or syndromes they may still read. Best effort: rc, the call's own
+// error, is what gets reported.
+int scratch_fence(rsg_codec_t* c, hipStream_t st, int rc) {
+    if (!rc) return 0;
+    for (hipStream_t s : {c->ps_side, c->ps_synst}) {
+        if (!s) continue;
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(e, s) == hipSuccess) (void)hipStreamWaitEvent(st, e, 0);
+            (void)hipEventDestroy(e);
+        }
+    }
+    (void)scratch_release(c, st);
+    (void)hipGetLastError();
+    return rc;
 }
 
 // ---------------------------------------------------------------- host-memory batches (PCIe)

@@ -864,30 +864,6 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
 
 }  // namespace rsamd
 
-namespace rsamd {
-
-// A per-stripe route that fails after its first launch returns with work still queued on the codec's side
-// and syndrome streams, and without marking the scratch busy: join those streams into the caller's stream
-// and mark the scratch as used by it, so the next call (on any stream) waits for the orphaned kernels
-// before it overwrites lists, records or syndromes they may still read. Best effort: the call's own error
-// is what gets reported.
-static int fenced(rsg_codec_t* c, hipStream_t st, int rc) {
-    if (!rc) return 0;
-    for (hipStream_t s : {c->ps_side, c->ps_synst}) {
-        if (!s) continue;
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
-            if (hipEventRecord(e, s) == hipSuccess) (void)hipStreamWaitEvent(st, e, 0);
-            (void)hipEventDestroy(e);
-        }
-    }
-    (void)scratch_release(c, st);
-    (void)hipGetLastError();
-    return rc;
-}
-
-}  // namespace rsamd
-
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
@@ -934,12 +910,12 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (dev_m8 && (c->batch_plans == 1 || groups.size() > kHostPlanGroups))
-        return fenced(c, st,
+        return scratch_fence(c, st,
                       decode_batch_device_plans(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
                                                 int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st));
     // GF(2^16): more than one pattern -> per-stripe plans on the syndrome route (one shared syndrome pass)
     if (dev_m16 && (c->batch_plans == 1 || groups.size() > 1))
-        return fenced(c, st,
+        return scratch_fence(c, st,
                       decode_batch_m16_ps(c, static_cast<uint8_t*>(d_rcv), int64_t(stripe_stride),
                                           int64_t(symbol_stride), n_stripes, symbol_size, is_erased, tr.data(), st));
     std::vector<int32_t> ids;
@@ -949,35 +925,43 @@ extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_str
         ids.insert(ids.end(), g.ids.begin(), g.ids.end());
     }
     if (int rc = scratch_acquire(c, st)) return rc;
-    if (ids.size() > c->ids_cap) {
-        if (c->d_ids) (void)hipFree(c->d_ids);
-        c->d_ids = nullptr;
-        c->ids_cap = 0;
-        HIP_TRY(hipMalloc(&c->d_ids, ids.size() * 4));
-        c->ids_cap = ids.size();
-    }
-    if (int rc = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}})) return rc;
-    uint8_t* base = static_cast<uint8_t*>(d_rcv);
-    // GF(2^16) codes with many patterns: one plan rebuilt on the stream per pattern (batch_plan_m16)
-    const bool stream_plans = c->m > 8 && c->m16_plans != 0 &&
-                              (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups));
-    size_t gi = 0;
-    for (auto& g : groups) {
-        std::unique_ptr<bool[]> er(new bool[n]);
-        uint16_t t = 0;
-        for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.key[i] != 0));
-        DevPlan* p = nullptr;
-        int rc = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
-        if (rc) return rc;
-        // a pattern shared by every stripe, in order: no stripe-id list (the GF(2^16) route and the re-encode
-        // decode cover only that form)
-        const bool all = g.ids.size() == n_stripes && g.ids.front() == 0 && g.ids.back() == int32_t(n_stripes - 1);
-        rc = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
-                      int64_t(symbol_stride), g.ids.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
-        if (rc) return rc;
-        ++gi;
-    }
-    return scratch_release(c, st);
+    // from here on every failure goes through scratch_fence(): group kernels launched before it may still read
+    // d_ids, so the scratch is marked busy on st and the next call (on any stream) waits for them
+    const int rc = [&]() -> int {
+        if (ids.size() > c->ids_cap) {
+            if (c->d_ids) (void)hipFree(c->d_ids);
+            c->d_ids = nullptr;
+            c->ids_cap = 0;
+            HIP_TRY(hipMalloc(&c->d_ids, ids.size() * 4));
+            c->ids_cap = ids.size();
+        }
+        if (int e = stage_lists(c, st, {{c->d_ids, ids.data(), ids.size() * 4}})) return e;
+        uint8_t* base = static_cast<uint8_t*>(d_rcv);
+        // GF(2^16) codes with many patterns: one plan rebuilt on the stream per pattern (batch_plan_m16)
+        const bool stream_plans = c->m > 8 && c->m16_plans != 0 &&
+                                  (c->batch_plans == 1 || (c->batch_plans == 2 && groups.size() > kHostPlanGroups));
+        size_t gi = 0;
+        for (auto& g : groups) {
+            std::unique_ptr<bool[]> er(new bool[n]);
+            uint16_t t = 0;
+            for (size_t i = 0; i < n; ++i) t = uint16_t(t + (er[i] = g.key[i] != 0));
+            DevPlan* p = nullptr;
+#ifdef RS_AMD_DIAG
+            if (int64_t(gi) == c->inject_fail_group) return RS_ERR_DEVICE;  // failure injection (tests)
+#endif
+            int e = stream_plans ? batch_plan_m16(c, er.get(), int(gi & 1), st, &p) : decode_plan(c, er.get(), t, &p, st);
+            if (e) return e;
+            // a pattern shared by every stripe, in order: no stripe-id list (the GF(2^16) route and the re-encode
+            // decode cover only that form)
+            const bool all = g.ids.size() == n_stripes && g.ids.front() == 0 && g.ids.back() == int32_t(n_stripes - 1);
+            e = run_plan(c, *p, base, int64_t(stripe_stride), int64_t(symbol_stride), base, int64_t(stripe_stride),
+                         int64_t(symbol_stride), g.ids.size(), symbol_size, st, all ? nullptr : c->d_ids + first[gi]);
+            if (e) return e;
+            ++gi;
+        }
+        return 0;
+    }();
+    return rc ? scratch_fence(c, st, rc) : scratch_release(c, st);
 }
 
 extern "C" int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route) {

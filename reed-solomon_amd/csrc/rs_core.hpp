@@ -337,6 +337,9 @@ struct rsg_codec {
     // diagnostic builds: option m8_ps_ablate, timing ablations of the per-stripe solve (wrong results): 1 no
     // table copy, 2 no output conversion
     int m8_ps_ablate = 0;
+    // diagnostic builds: option inject_fail_group, rsg_decode_batch's host-plan grouping path fails with
+    // RS_ERR_DEVICE at that group (after the earlier groups' launches; tests of the failure fence)
+    int64_t inject_fail_group = -1;
     std::unique_ptr<rsamd::DevPlan> syn;  // syndrome matrix S_j = sum_i X_i^j rcv_i, j < r
     bool syn_failed = false;
     void* d_syn = nullptr;  // [chunk][r][S] syndromes
@@ -439,6 +442,7 @@ int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out
 // codec scratch shared by launches on different streams: wait for / mark the last user
 int scratch_acquire(rsg_codec_t* c, hipStream_t st);
 int scratch_release(rsg_codec_t* c, hipStream_t st);
+int scratch_fence(rsg_codec_t* c, hipStream_t st, int rc);  // release after a failed route (returns rc)
 
 // ------------------------------------------------------------------ rs_batch.cpp
 // the fixed r x (k + r) matrix of the GF(256) per-stripe route (1 syndromes, 2 re-encode differences [G | I])

@@ -177,15 +177,15 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
     i32x16s o0, o1;
     sload32(out, o0, o1);
     auto slot = [&](int p) { return p < 16 ? o0[p & 15] : o1[p & 15]; };
-    auto at = [&](int p) {
-        const int32_t s = slot(p);
-        return reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, s, 2, p) ? s : 0) * a.dst_sym);
-    };
+    auto at = [&](int p) { return reinterpret_cast<uint32_t*>(dst + int64_t(slot(p)) * a.dst_sym); };
+    // diagnostic builds: a slot outside the codec's range is recorded and its store (and old-value load)
+    // skipped, so a violation never writes another slot's data; release builds: always true
+    auto ok = [&](int p) { return RS_SLOT_OK(a, slot(p), 2, p); };
 #if defined(RS_AMD_DIAG) && !defined(RS_JIT_SOURCE)
     if (a.ablate & 2) {  // timing ablation: raw accumulators, no L^-1 conversion (wrong results)
 #pragma unroll
         for (int p = 0; p < 32; ++p)
-            if (p < rows) *at(p) = p < 16 ? a0[p & 15] : a1[p & 15];
+            if (p < rows && ok(p)) *at(p) = p < 16 ? a0[p & 15] : a1[p & 15];
         return;
     }
 #endif
@@ -195,10 +195,10 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
         for (int p0 = 0; p0 < 32; p0 += LB) {
             uint32_t old[LB];
 #pragma unroll
-            for (int q = 0; q < LB; ++q) old[q] = p0 + q < rows ? *at(p0 + q) : 0u;
+            for (int q = 0; q < LB; ++q) old[q] = p0 + q < rows && ok(p0 + q) ? *at(p0 + q) : 0u;
 #pragma unroll
             for (int q = 0; q < LB; ++q)
-                if (p0 + q < rows) *at(p0 + q) = m8_v1_out<NB, G4>(lt, p0 + q, a0, a1, b0, b1) ^ old[q];
+                if (p0 + q < rows && ok(p0 + q)) *at(p0 + q) = m8_v1_out<NB, G4>(lt, p0 + q, a0, a1, b0, b1) ^ old[q];
         }
         return;
     }
@@ -216,7 +216,7 @@ __device__ __forceinline__ void m8_v1_store(const V1Args& a, const uint32_t* lt,
 #pragma unroll
         for (int q = 7; q >= 0; --q) {
             const int32_t sl = p0 + q < rows ? slot(p0 + q) : slast;
-            *reinterpret_cast<uint32_t*>(dst + int64_t(RS_SLOT_OK(a, sl, 2, p0 + q) ? sl : 0) * a.dst_sym) = w[q];
+            if (RS_SLOT_OK(a, sl, 2, p0 + q)) *reinterpret_cast<uint32_t*>(dst + int64_t(sl) * a.dst_sym) = w[q];
         }
     }
 }
@@ -259,7 +259,8 @@ __device__ __forceinline__ void m8_v1h_store(const V1Args& a, const uint32_t* lt
 #pragma unroll
         for (int q = 7; q >= 0; --q) {
             const int32_t sl = p0 + q < rows ? slot(p0 + q) : slast;
-            uint8_t* d = base + int64_t(uint32_t(RS_SLOT_OK(a, sl, 2, p0 + q) ? sl : 0)) * a.dst_sym;  // slots >= 0
+            if (!RS_SLOT_OK(a, sl, 2, p0 + q)) continue;  // diagnostic builds: recorded, not stored
+            uint8_t* d = base + int64_t(uint32_t(sl)) * a.dst_sym;  // slots >= 0
             asm volatile("global_store_dword %0, %1, %2" ::"v"(voff), "v"(w[q]), "s"(d) : "memory");
         }
     }

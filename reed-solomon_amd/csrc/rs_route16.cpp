@@ -503,98 +503,102 @@ int run_cs(rsg_codec_t* c, DevPlan& p, const uint8_t* src, int64_t src_stripe, i
     // d_goff is codec scratch like d_cs: a launch on another stream may still read it (a route encode on
     // stream A, then a route decode on stream B rewrites it), so wait for that before overwriting it
     if (int rc = scratch_acquire(c, st)) return rc;
-    const int ngo = (cs.ngroups + 3) * 16;
-    if (int rc = grow(&c->d_goff[cs.kind], c->goff_cap[cs.kind], size_t(ngo) * 4)) return rc;
-    HIP_TRY(launch_cs16_goff(groups ? groups : cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
-    Cs16Args a{};
-    a.src_stripe = src_stripe;
-    a.src_sym = src_sym;
-    a.goff = static_cast<const uint32_t*>(c->d_goff[cs.kind]);
-    a.in_bytes = uint32_t(cs.max_slot * src_sym + int64_t(S));
-    a.rec = cs.rec;
-    a.fin = cs.fin;
-    a.fin_off = cs.fin_off;
-    a.fin_stride = cs.fin_stride;
-    a.dst_sym = int64_t(S);
-    a.logt = logt;
-    a.expt = expt;
-    for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
-    a.ngroups = cs.ngroups;
-    a.ntiles = cs.ntiles;
-    a.colw = c->m16_cs_col == 1024 ? 1024 : 256;
-    a.nchunks = int64_t(S) / a.colw;
-    const uint64_t waves_per_unit = uint64_t(a.colw / 256);  // per tile
-    if (cs.kind == 1) {  // straight into the outputs
-        a.src = src;
-        a.dst = dst;
-        a.dst_stripe = dst_stripe;
-        a.dst_sym = dst_sym;
-        a.units = int64_t(n_stripes) * a.nchunks;
-        HIP_TRY(launch_bs16(a, st));
-        RS_CHECKPOINT(c, &p, "GF(2^16) route k_bs16", n_stripes, S);
-        const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
-        c->work_valu += steps * kValu_bs16;
-        c->work_salu += steps * kSalu_bs16;
-        c->last_kernel = "bs16";
-        return scratch_release(c, st);
-    }
-    const bool thr = c->m16_cs_thread && cs.rec_t;
-    if (thr) {  // k_cs16t's own tiling
-        a.rec = cs.rec_t;
-        a.fin = cs.fin_t;
-        a.fin_off = cs.fin_off_t;
-        a.fin_stride = cs.fin_stride_t;
-        a.ntiles = cs.ntiles_t;
-        a.cw = kCs16tCw;
-    }
-    const int64_t per = int64_t(cs.D) * int64_t(S);
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
-    // option m16_cs_overlap: at least kCsOverlapChunks chunks, chunk i + 1's syndromes on the codec's
-    // syndrome stream (other buffer) beside chunk i's second stage on st
-    const bool ovl = c->cs_overlap && int64_t(n_stripes) >= kCsOverlapMinStripes;
-    if (ovl) chunk = std::min<int64_t>(chunk, (int64_t(n_stripes) + kCsOverlapChunks - 1) / kCsOverlapChunks);
-    if (int rc = grow(&c->d_cs, c->cs_cap, size_t((ovl ? 2 : 1) * chunk * per))) return rc;
-    hipStream_t sy = st;
-    if (ovl) {
-        if (int rc = overlap_objects(c)) return rc;
-        sy = c->ps_synst;
-        HIP_TRY(hipEventRecord(c->ps_ev_entry, st));  // after the d_goff upload above
-        HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
-    }
-    std::string second;
-    for (int64_t c0 = 0, ci = 0; c0 < int64_t(n_stripes); c0 += chunk, ++ci) {
-        const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
-        const int set = int(ci & 1);
-        uint8_t* csb = static_cast<uint8_t*>(c->d_cs) + (ovl ? set * chunk * per : 0);
-        if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));  // buffer read by chunk ci - 2
-        a.src = src + c0 * src_stripe;
-        a.dst = csb;
-        a.dst_stripe = per;
-        a.units = cn * a.nchunks;
-        if (thr) {
-            HIP_TRY(launch_cs16t(a, sy));
-            RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16t", uint64_t(cn), S);
-            c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
-            c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSaluStepCs16t;
-        } else {
-            HIP_TRY(launch_cs16(a, sy));
-            RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16", uint64_t(cn), S);
+    // a failure after the first launch goes through scratch_fence: the scratch stays marked busy on st
+    const int rc = [&]() -> int {
+        const int ngo = (cs.ngroups + 3) * 16;
+        if (int rc = grow(&c->d_goff[cs.kind], c->goff_cap[cs.kind], size_t(ngo) * 4)) return rc;
+        HIP_TRY(launch_cs16_goff(groups ? groups : cs.groups, static_cast<uint32_t*>(c->d_goff[cs.kind]), ngo, src_sym, st));
+        Cs16Args a{};
+        a.src_stripe = src_stripe;
+        a.src_sym = src_sym;
+        a.goff = static_cast<const uint32_t*>(c->d_goff[cs.kind]);
+        a.in_bytes = uint32_t(cs.max_slot * src_sym + int64_t(S));
+        a.rec = cs.rec;
+        a.fin = cs.fin;
+        a.fin_off = cs.fin_off;
+        a.fin_stride = cs.fin_stride;
+        a.dst_sym = int64_t(S);
+        a.logt = logt;
+        a.expt = expt;
+        for (int t = 0; t < 16; ++t) a.nblog[t] = cs.nblog[t];
+        a.ngroups = cs.ngroups;
+        a.ntiles = cs.ntiles;
+        a.colw = c->m16_cs_col == 1024 ? 1024 : 256;
+        a.nchunks = int64_t(S) / a.colw;
+        const uint64_t waves_per_unit = uint64_t(a.colw / 256);  // per tile
+        if (cs.kind == 1) {  // straight into the outputs
+            a.src = src;
+            a.dst = dst;
+            a.dst_stripe = dst_stripe;
+            a.dst_sym = dst_sym;
+            a.units = int64_t(n_stripes) * a.nchunks;
+            HIP_TRY(launch_bs16(a, st));
+            RS_CHECKPOINT(c, &p, "GF(2^16) route k_bs16", n_stripes, S);
             const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
-            c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
-            c->work_salu += steps * kSalu_cs16a;
+            c->work_valu += steps * kValu_bs16;
+            c->work_salu += steps * kSalu_bs16;
+            c->last_kernel = "bs16";
+            return 0;
         }
+        const bool thr = c->m16_cs_thread && cs.rec_t;
+        if (thr) {  // k_cs16t's own tiling
+            a.rec = cs.rec_t;
+            a.fin = cs.fin_t;
+            a.fin_off = cs.fin_off_t;
+            a.fin_stride = cs.fin_stride_t;
+            a.ntiles = cs.ntiles_t;
+            a.cw = kCs16tCw;
+        }
+        const int64_t per = int64_t(cs.D) * int64_t(S);
+        int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(int64_t(n_stripes), (int64_t(1) << 30) / per));
+        // option m16_cs_overlap: at least kCsOverlapChunks chunks, chunk i + 1's syndromes on the codec's
+        // syndrome stream (other buffer) beside chunk i's second stage on st
+        const bool ovl = c->cs_overlap && int64_t(n_stripes) >= kCsOverlapMinStripes;
+        if (ovl) chunk = std::min<int64_t>(chunk, (int64_t(n_stripes) + kCsOverlapChunks - 1) / kCsOverlapChunks);
+        if (int rc = grow(&c->d_cs, c->cs_cap, size_t((ovl ? 2 : 1) * chunk * per))) return rc;
+        hipStream_t sy = st;
         if (ovl) {
-            HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
-            HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+            if (int rc = overlap_objects(c)) return rc;
+            sy = c->ps_synst;
+            HIP_TRY(hipEventRecord(c->ps_ev_entry, st));  // after the d_goff upload above
+            HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_entry, 0));
         }
-        if (int rc = run_plan(c, *p.second, csb, per, int64_t(S), dst + c0 * dst_stripe, dst_stripe, dst_sym,
-                              uint64_t(cn), S, st))
-            return rc;
-        if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
-        second = c->last_kernel;
-    }
-    c->last_kernel = (thr ? "cs16t+" : "cs16+") + second;
-    return scratch_release(c, st);
+        std::string second;
+        for (int64_t c0 = 0, ci = 0; c0 < int64_t(n_stripes); c0 += chunk, ++ci) {
+            const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
+            const int set = int(ci & 1);
+            uint8_t* csb = static_cast<uint8_t*>(c->d_cs) + (ovl ? set * chunk * per : 0);
+            if (ovl && ci >= 2) HIP_TRY(hipStreamWaitEvent(sy, c->ps_ev_used[set], 0));  // buffer read by chunk ci - 2
+            a.src = src + c0 * src_stripe;
+            a.dst = csb;
+            a.dst_stripe = per;
+            a.units = cn * a.nchunks;
+            if (thr) {
+                HIP_TRY(launch_cs16t(a, sy));
+                RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16t", uint64_t(cn), S);
+                c->work_valu += uint64_t(a.units) * waves_per_unit * cs.valu_t;
+                c->work_salu += uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles_t) * uint64_t(cs.ngroups) * kSaluStepCs16t;
+            } else {
+                HIP_TRY(launch_cs16(a, sy));
+                RS_CHECKPOINT(c, &p, "GF(2^16) route syndromes k_cs16", uint64_t(cn), S);
+                const uint64_t steps = uint64_t(a.units) * waves_per_unit * uint64_t(cs.ntiles) * uint64_t(cs.ngroups);
+                c->work_valu += steps * kValu_cs16a;  // cs16a and cs16b issue the same counts
+                c->work_salu += steps * kSalu_cs16a;
+            }
+            if (ovl) {
+                HIP_TRY(hipEventRecord(c->ps_ev_syn[set], sy));
+                HIP_TRY(hipStreamWaitEvent(st, c->ps_ev_syn[set], 0));
+            }
+            if (int rc = run_plan(c, *p.second, csb, per, int64_t(S), dst + c0 * dst_stripe, dst_stripe, dst_sym,
+                                  uint64_t(cn), S, st))
+                return rc;
+            if (ovl) HIP_TRY(hipEventRecord(c->ps_ev_used[set], st));
+            second = c->last_kernel;
+        }
+        c->last_kernel = (thr ? "cs16t+" : "cs16+") + second;
+        return 0;
+    }();
+    return rc ? scratch_fence(c, st, rc) : scratch_release(c, st);
 }
 
 // The re-encode decode (DevPlan::Reenc) over a chunk loop: the encode route over U into scratch rows
@@ -606,25 +610,28 @@ int run_reenc(rsg_codec_t* c, DevPlan& p, uint8_t* base, int64_t stripe_stride, 
     const int64_t k = c->k, r = c->r, per = r * int64_t(S);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>({int64_t(n_stripes), (int64_t(1) << 30) / per, 65535}));
     if (int rc = scratch_acquire(c, st)) return rc;
-    if (int rc = grow(&c->d_reenc, c->reenc_cap, size_t(chunk * per))) return rc;
-    uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
-    std::string k1, k2;
-    for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
-        const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
-        uint8_t* b = base + c0 * stripe_stride;
-        if (int rc = run_cs(c, E, b, stripe_stride, sym, y, per, int64_t(S), uint64_t(cn), S, st, p.reenc->groups))
-            return rc;
-        k1 = c->last_kernel;  // the encode route over U: "cs16t+bs16" / "cs16+bs16"
-        HIP_TRY(launch_xor_rows(y, per, int64_t(S), b + k * sym, stripe_stride, sym, r, int64_t(S), cn, st));
-        if (int rc = run_plan(c, *p.reenc->drep, y, per, int64_t(S), b, stripe_stride, sym, uint64_t(cn), S, st))
-            return rc;
-        k2 = c->last_kernel;
-    }
-    c->last_kernel = k1 + "+xor+" + k2;
-    // the encode plan's records were read by these launches: its guard must cover them (run_plan does
-    // this for the plans it launches; E is launched through run_cs directly)
-    if (int rc = E.note_use(st)) return rc;
-    return scratch_release(c, st);
+    const int rc = [&]() -> int {
+        if (int rc = grow(&c->d_reenc, c->reenc_cap, size_t(chunk * per))) return rc;
+        uint8_t* y = static_cast<uint8_t*>(c->d_reenc);
+        std::string k1, k2;
+        for (int64_t c0 = 0; c0 < int64_t(n_stripes); c0 += chunk) {
+            const int64_t cn = std::min<int64_t>(chunk, int64_t(n_stripes) - c0);
+            uint8_t* b = base + c0 * stripe_stride;
+            if (int rc = run_cs(c, E, b, stripe_stride, sym, y, per, int64_t(S), uint64_t(cn), S, st, p.reenc->groups))
+                return rc;
+            k1 = c->last_kernel;  // the encode route over U: "cs16t+bs16" / "cs16+bs16"
+            HIP_TRY(launch_xor_rows(y, per, int64_t(S), b + k * sym, stripe_stride, sym, r, int64_t(S), cn, st));
+            if (int rc = run_plan(c, *p.reenc->drep, y, per, int64_t(S), b, stripe_stride, sym, uint64_t(cn), S, st))
+                return rc;
+            k2 = c->last_kernel;
+        }
+        c->last_kernel = k1 + "+xor+" + k2;
+        // the encode plan's records were read by these launches: its guard must cover them (run_plan does
+        // this for the plans it launches; E is launched through run_cs directly)
+        if (int rc = E.note_use(st)) return rc;
+        return 0;
+    }();
+    return rc ? scratch_fence(c, st, rc) : scratch_release(c, st);
 }
 
 }  // namespace rsamd

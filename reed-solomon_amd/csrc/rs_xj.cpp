@@ -891,7 +891,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
         // addresses it absolutely); every workgroup copies it once, then loops over columns
         o << "  __shared__ __attribute__((aligned(16))) uint16_t xj_tab[65536];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
-          << "  if ((uint32_t)(unsigned long)xj_tab != 0u) return;\n"
+          << "  if ((uint32_t)(unsigned long)xj_tab != 0u) __builtin_trap();\n"  // a layout change faults, never wrong data
              "  for (uint32_t i = threadIdx.x; i < 8192u; i += blockDim.x)\n"
              "    ((xj_u4*)xj_tab)[i] = ((const xj_u4*)a.tab)[i];\n"
              "  __syncthreads();\n"
@@ -908,7 +908,7 @@ std::string xj_source(const std::vector<uint16_t>& M, int K, int R, const std::v
         o << "  __shared__ __attribute__((aligned(16))) uint32_t xj_lds["
           << (C.coord ? 1024 : C.share ? 4096 : std::max(1, roles * C.lds * 512)) << "];\n"
           << "  asm volatile(\n" << as_string_literals(finish_block(C)) << "  ::: \"memory\");\n"
-          << (C.coord ? "  if ((uint32_t)(unsigned long)xj_lds != 0u) return;\n"  // the reads address it absolutely
+          << (C.coord ? "  if ((uint32_t)(unsigned long)xj_lds != 0u) __builtin_trap();\n"  // the reads address it absolutely
                         "  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) xj_lds[i] = ((const uint32_t*)a.tab)[i];\n"
                         "  __syncthreads();\n"
                       : "")

@@ -22,6 +22,14 @@ next instruction is reached only by jumps):
     retired by vmcnt(N) (N = ops allowed outstanding, stores included in the count).
 Any operand of a later instruction that overlaps an in-flight destination is reported.
 
+Second check (`valu_sgpr_hazards`): an SGPR written by a VALU instruction (v_readfirstlane / v_readlane, a
+VALU compare or carry-out into an SGPR) and read by a vector memory instruction (its saddr, srsrc or
+soffset) fewer than 5 wait states later. gfx9 does not interlock this; the compiler inserts s_nop for its
+own code, but not inside inline asm (the SGPR-addressed stores of m8_v1h_store, the s_cselect-chosen load
+bases of the masked rs_xj pass). Wait states are counted per instruction (s_nop N counts N + 1), in
+address order; a branch, s_endpgm or a branch target ends the window (conservative at joins only by
+restarting, which the kernels here never need).
+
 Usage: isa_hazards.py <code object or .so or disassembly .s> [...]; exit 1 if anything is found.
 Importable: hazards(text) -> list of (function, address, instruction, registers).
 """
@@ -213,12 +221,65 @@ def hazards(text):
     return found
 
 
+_VMEM = re.compile(r"(global|buffer|flat|scratch)_(load|store|atomic)")
+
+
+def _sregs(text):
+    return {i for kind, i in _regs(text) if kind == "s"}
+
+
+def valu_sgpr_hazards(text, window=5):
+    """(function, address, instruction, sgprs) for every VMEM instruction that reads an SGPR a VALU
+    instruction wrote fewer than `window` wait states before it."""
+    found = []
+    for func, body in _functions(text):
+        targets = set()
+        for addr, op, args, word in body:
+            if _BRANCH.match(op):
+                simm = word & 0xFFFF
+                targets.add(addr + 4 + 4 * (simm - 0x10000 if simm & 0x8000 else simm))
+        recent = []  # [sgprs, wait states still needed]
+        for addr, op, args, word in body:
+            if addr in targets:
+                recent = []
+            if _VMEM.match(op):
+                ops = _split_ops(args)
+                reads = set()
+                for o in ops:
+                    reads |= _sregs(o)
+                hit = set()
+                for regs, left in recent:
+                    if left > 0:
+                        hit |= regs & reads
+                if hit:
+                    found.append((func, f"{addr:X}", f"{op} {args}".strip(), sorted(("s", r) for r in hit)))
+            cost = 1
+            if op == "s_nop":
+                m = re.match(r"\s*(0x[0-9a-fA-F]+|\d+)", args or "0")
+                cost = int(m.group(1), 0) + 1 if m else 1
+            recent = [[regs, left - cost] for regs, left in recent if left - cost > 0]
+            if op.startswith("v_"):
+                ops = _split_ops(args)
+                dst = _sregs(ops[0]) if ops else set()
+                if len(ops) > 1 and ("_co_" in op or op.startswith(("v_div_scale", "v_add_co", "v_sub_co"))):
+                    dst |= _sregs(ops[1])
+                if dst:
+                    recent.append([dst, window])
+            if op in ("s_branch", "s_setpc_b64") or op.startswith("s_endpgm"):
+                recent = []
+    return found
+
+
 def main(argv):
     bad = 0
     for p in argv[1:]:
-        for func, addr, insn, regs in hazards(disassemble(p)):
+        text = disassemble(p)
+        for func, addr, insn, regs in hazards(text):
             bad += 1
             print(f"{p}: {func} @{addr}: {insn}   in flight: {regs}")
+        for func, addr, insn, regs in valu_sgpr_hazards(text):
+            bad += 1
+            print(f"{p}: {func} @{addr}: {insn}   VALU-written SGPR within 5 wait states: {regs}")
     print(f"{bad} hazard(s)")
     return 1 if bad else 0
 

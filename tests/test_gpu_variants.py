@@ -8,6 +8,7 @@ input (v1 / v1h), and the GF(2^16) route on the gpr-indexed k_cs16 (cs_idx). Dia
 kernel (idx), the compiler-indexed reference kernels (table / mask), the per-stripe solve A/B kernels,
 overlapped chunks, multi-chunk workgroups and the 1 KiB route block layout. Same checks as the production
 tests: reference goldens, C2 every stripe vs the oracle, C3-shape round trips, non-codeword decodes."""
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -72,3 +73,62 @@ def test_cs16_overlapped_chunks_match_serial(k, r, S, n):
 def test_m16_kernel_shapes_route_layout_1k(k, r, S, route):
     """The GF(2^16) shapes with the route kernels' 1 KiB block layout (m16_cs_col 1024, diagnostic build)."""
     m16_shapes_case(rs_amd.diag_module(), k, r, S, route, 1024)
+
+
+def test_failed_group_fences_scratch_for_next_stream():
+    """rsg_decode_batch's host-plan grouping path (<= 16 distinct patterns) failing after some group kernels
+    were launched (diagnostic option inject_fail_group: the n-th group's plan fails with RS_ERR_DEVICE): the
+    call must still mark the codec scratch (the stripe-id list those kernels read) busy on its stream, so a
+    following call on another stream waits for the orphaned kernels before it restages the list. Checks: the
+    second call returns only after the first stream's kernels are done, the launched groups restored their
+    stripes bit-exactly (their id list was not overwritten under them), the failed group's stripes are
+    untouched, and the second batch is correct."""
+    k, r, S, per = 128, 32, 65536, 512
+    groups = 4
+    n = groups * per
+    diag = rs_amd.diag_module()
+    codec = diag.Codec(k, r)
+    codec.set_option("inject_fail_group", groups - 1)
+    dev = torch.empty((n, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(dev, k, seed=0x6A11)
+    rs_amd.Codec(k, r).encode(dev)
+    ref = torch.zeros(n, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(dev, 0, k, ref)
+    rng = np.random.default_rng(61)
+    pats = np.zeros((n, k + r), bool)
+    for g in range(groups):  # stripes interleaved over the groups: every launch goes through the id list
+        p = np.zeros(k + r, bool)
+        p[rng.choice(k, r, replace=False)] = True
+        pats[g::groups] = p
+    mask = torch.from_numpy(pats).cuda()
+    dev.masked_fill_(mask[:, :, None], 0)
+    small = torch.empty((8, k + r, S), dtype=torch.uint8, device="cuda")
+    rs_amd.fill_info(small, k, seed=0x6A12)
+    rs_amd.Codec(k, r).encode(small)
+    small_ref = torch.zeros(8, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(small, 0, k, small_ref)
+    spats = np.zeros((8, k + r), bool)
+    for s in range(8):
+        spats[s, rng.choice(k, 3, replace=False)] = True
+    small.masked_fill_(torch.from_numpy(spats).cuda()[:, :, None], 0)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    rc = codec.decode_batch(dev, pats, stream=sa, check=False)
+    assert rc == rs_amd.RS_ERR_DEVICE, rc
+    done_a = torch.cuda.Event()
+    done_a.record(sa)
+    codec.set_option("inject_fail_group", -1)
+    assert codec.decode_batch(small, spats, stream=sb) == 0
+    assert done_a.query(), "the call on the second stream returned before the failed call's kernels finished"
+    torch.cuda.synchronize()
+    fp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(dev, 0, k, fp)
+    launched = np.array([s % groups != groups - 1 for s in range(n)])
+    idx = torch.from_numpy(np.nonzero(launched)[0]).cuda()
+    assert torch.equal(fp[idx], ref[idx]), "a launched group restored wrong bytes"
+    lost = torch.from_numpy(np.nonzero(pats[groups - 1])[0]).cuda()
+    assert int(dev[groups - 1::groups][:, lost].count_nonzero()) == 0, "the failed group's stripes were written"
+    sfp = torch.zeros(8, dtype=torch.int64, device="cuda")
+    rs_amd.fingerprint(small, 0, k, sfp)
+    torch.cuda.synchronize()
+    assert torch.equal(sfp, small_ref)

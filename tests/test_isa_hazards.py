@@ -28,8 +28,35 @@ PKG = os.path.join(REPO, "reed-solomon_amd")
 
 
 def _check(path):
-    found = isa_hazards.hazards(isa_hazards.disassemble(path))
+    text = isa_hazards.disassemble(path)
+    found = isa_hazards.hazards(text)
     assert not found, "\n".join(f"{f} @{a}: {i}  in flight {r}" for f, a, i, r in found)
+    found = isa_hazards.valu_sgpr_hazards(text)
+    assert not found, "\n".join(f"{f} @{a}: {i}  VALU-written SGPR {r}" for f, a, i, r in found)
+
+
+def test_checker_flags_valu_written_sgpr_read_by_vmem():
+    """The second check: an SGPR from v_readfirstlane used as a store's saddr two instructions later (gfx9
+    needs 5 wait states; inline asm gets no s_nop from the compiler), and the same with an s_nop 4 between."""
+    bad = """
+0000000000000000 <k3>:
+\tv_readfirstlane_b32 s4, v1                                  // 000000000000: 7E080501
+\tv_xor_b32_e32 v5, v4, v5                                   // 000000000004: 2A0A0B04
+\tglobal_store_dword v2, v3, s[4:5]                          // 000000000008: DC708000 00040302
+"""
+    found = isa_hazards.valu_sgpr_hazards(bad)
+    assert len(found) == 1 and found[0][3] == [("s", 4)], found
+    good = bad.replace("\tv_xor_b32_e32 v5, v4, v5                                   // 000000000004: 2A0A0B04",
+                       "\ts_nop 4                                                   // 000000000004: BF800004")
+    assert not isa_hazards.valu_sgpr_hazards(good)
+    # a VALU compare into an SGPR pair, then a buffer load with that pair as its soffset's neighbour
+    cmp = """
+0000000000000000 <k4>:
+\tv_cmp_eq_u32_e64 s[6:7], v1, v2                            // 000000000000: D0CA0006 00020501
+\tbuffer_load_dword v3, v4, s[8:11], s6 offen                // 000000000008: E0501000 06020304
+"""
+    found = isa_hazards.valu_sgpr_hazards(cmp)
+    assert len(found) == 1 and found[0][3] == [("s", 6)], found
 
 
 def test_checker_flags_the_round4_pattern():
