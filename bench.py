@@ -86,7 +86,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra legs (N=1 only: host-memory path, per-stripe patterns, C2 / C5 configs)")
-    ap.add_argument("--extras", default="end_to_end,per_stripe_decode,configs",
+    ap.add_argument("--extras", default="end_to_end,per_stripe_decode,configs,symbol_ops",
                     help="comma list of extra legs to run after the headline (N=1, never part of `value`)")
     ap.add_argument("--ps-stripes", type=int, default=4096, help="per_stripe_decode leg: stripes, each its own pattern")
     ap.add_argument("--host-stripes", type=int, default=256, help="end_to_end leg: pinned host stripes")
@@ -575,6 +575,59 @@ def config_leg(k, r, S, n, steps, warmup, dev, stream, oracle_decode_check):
     return line
 
 
+def symbol_ops_leg(dev, stream):
+    """The secondary surface batched (rsg_symbol_ops; ref src/rs/gf65536.c:155-219, one synchronous GPU round
+    trip per gf_* call otherwise): chains of gf_madd accumulating into targets, as the reference's evaluator /
+    restore loops do, ONE call per batch. Per-op device time (HIP events on the stream, median of 5 calls) and
+    the call's host time. Check: every target against the ops applied one after another with numpy."""
+    import torch
+    import rs_amd
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from _util import gf_tables
+    exp, log = gf_tables()
+    out = {}
+    rng = np.random.default_rng(SEED)
+    for S, n_t, per_t in ((1024, 128, 32), (65536, 32, 32)):
+        src = torch.from_numpy(rng.integers(0, 256, (per_t, S), dtype=np.uint8)).to(dev)
+        tgt = torch.zeros((n_t, S), dtype=torch.uint8, device=dev)
+        coefs = rng.integers(2, 65536, (n_t, per_t))
+        ops = np.zeros(n_t * per_t, rs_amd.SYMBOL_OP_DTYPE)
+        ops["op"] = rs_amd.OP_MADD
+        ops["a"] = tgt.data_ptr() + np.repeat(np.arange(n_t, dtype=np.uint64), per_t) * S
+        ops["b"] = src.data_ptr() + np.tile(np.arange(per_t, dtype=np.uint64), n_t) * S
+        ops["coef"] = coefs.reshape(-1)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+        host = []
+        for e0, e1 in ev:
+            tgt.zero_()
+            torch.cuda.synchronize()
+            torch.cuda._sleep(2_000_000)  # the stream waits ~1 ms: the events bracket the op-list copy + kernel only
+            e0.record(stream)
+            t0 = time.perf_counter()
+            rs_amd.symbol_ops(ops, S, device=dev.index, stream=stream)
+            host.append(time.perf_counter() - t0)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = float(np.median([a.elapsed_time(b) for a, b in ev[1:]]))
+        got = tgt.cpu().numpy().view("<u2").astype(np.int64)
+        ws = src.cpu().numpy().view("<u2").astype(np.int64)
+        want = np.zeros_like(got)
+        for j in range(per_t):
+            lw = np.where(ws[j] != 0, log[ws[j]], -1)
+            prod = np.where(lw[None, :] >= 0, exp[(lw[None, :] + log[coefs[:, j]][:, None]) % 65535], 0)
+            want ^= prod
+        n_ops = n_t * per_t
+        out[f"S{S}"] = {"ops": n_ops, "targets": n_t, "ops_per_target": per_t, "call_ms": round(ms, 4),
+                        "us_per_op": round(ms * 1e3 / n_ops, 4), "host_us_per_call": round(float(np.median(host[1:])) * 1e6, 1),
+                        "host_us_per_op": round(float(np.median(host[1:])) * 1e6 / n_ops, 4),
+                        "source_GBps": round(n_ops * S / ms / 1e6, 1), "parity": "ok" if np.array_equal(got, want) else "MISMATCH"}
+    out["note"] = ("gf_madd chains in one rsg_symbol_ops call (SYMBOL_OP_DTYPE array); call_ms = HIP events around the "
+                   "op-list copy + kernel (stream held by a spin kernel while the call is queued); host_us = the C call's "
+                   "host time (validation, chains, staging). The per-call gf_madd on host symbols is a synchronous round "
+                   "trip of ~16-23 us (DESIGN.md section 9)")
+    return out
+
+
 def extra_legs(args, stripes, fp_ref, erased, stream, dev):
     """The legs VERDICT r5 asked the driver to measure beside the headline (N = 1, after its timed region and
     checks; never part of `value`). A leg that raises is reported as such; the headline line still prints."""
@@ -582,7 +635,8 @@ def extra_legs(args, stripes, fp_ref, erased, stream, dev):
     out = {}
     t_all = time.perf_counter()
     for name, fn in (("per_stripe_decode", lambda: per_stripe_leg(args, stripes, fp_ref, stream, dev)),
-                     ("end_to_end", lambda: host_path_leg(args, stripes, erased, dev))):
+                     ("end_to_end", lambda: host_path_leg(args, stripes, erased, dev)),
+                     ("symbol_ops", lambda: symbol_ops_leg(dev, stream))):
         if name in wanted:
             t0 = time.perf_counter()
             try:

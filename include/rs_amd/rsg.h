@@ -235,6 +235,26 @@ int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf
 /* Compiles the masked fixed-pass kernel of that route into the JIT cache, like rsg_jit_precompile (0 when the
  * route does not apply). Host only. */
 int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route);
+/* Batched symbol operations: the reference's gf_add / gf_mul / gf_madd (rs/gf65536.h:146-167,
+ * src/rs/gf65536.c:155-219) over many symbols in ONE launch, asynchronous on `stream` -- the form a loop of
+ * gf_* calls takes on the GPU (each gf_* call of rs/gf65536.h is one synchronous round trip, ~15 us).
+ *   RSG_OP_ADD   a ^= b            RSG_OP_MUL   a = coef * a            RSG_OP_MADD  a ^= coef * b
+ * All symbols are `symbol_size` bytes (little-endian GF(2^16) words; an odd last byte is not touched, as
+ * the reference's Release build) at device-accessible addresses (hipMalloc memory, or the device address
+ * of page-locked host memory), 4-byte aligned. Ops on the same target `a` are applied in array order
+ * (b == a reads the target's current value); ops on different targets run in parallel, so no op may read
+ * (as b) another op's target, and targets may not overlap: RS_ERR_INVALID, nothing queued. The op array is
+ * copied before the call returns (the caller may reuse it); synchronise `stream` before reading results.
+ * `device` is the HIP device the symbols live on (the caller's current device is restored). */
+enum { RSG_OP_ADD = 0, RSG_OP_MUL = 1, RSG_OP_MADD = 2 };
+typedef struct rsg_symbol_op {
+    void* a;        /* target symbol, read and written */
+    const void* b;  /* source symbol (RSG_OP_ADD / RSG_OP_MADD; ignored for RSG_OP_MUL) */
+    uint16_t coef;  /* GF(2^16) coefficient (RSG_OP_MUL / RSG_OP_MADD) */
+    uint16_t op;    /* RSG_OP_* */
+    uint32_t reserved;
+} rsg_symbol_op_t;
+int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n_ops, uint64_t symbol_size, void* stream);
 const char* rsg_version(void);
 /* 1 when checked launches are on (environment RS_AMD_CHECK set and not "0" at the first call of the
  * process), else 0. In checked mode every launch group is followed by a device wait and an error read: a

@@ -341,6 +341,136 @@ extern "C" void gf_madd(GF_t* gf, void* a, element_t coef, const void* b, size_t
     if (int rc = symbol_op(coef == 1 ? 0 : 2, a, coef, b, symbol_size)) symbol_op_failed("gf_madd", rc);
 }
 
+// ============================================================================ batched symbol ops
+// rsg_symbol_ops (include/rs_amd/rsg.h): many gf_add / gf_mul / gf_madd triples on device-accessible
+// symbols in one launch, asynchronous on the caller's stream. The op list goes to the device through one
+// of kOpSlots page-locked staging slots per device (each reused only after the launch that read it is
+// done: its event), so a call returns as soon as the copy and the kernel are queued.
+namespace rsamd {
+namespace {
+constexpr int kOpSlots = 4;
+struct OpSlot {
+    uint8_t* h = nullptr;  // page-locked staging
+    uint8_t* d = nullptr;  // device copy read by the kernel
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+};
+struct OpStage {
+    std::mutex mu;
+    OpSlot slot[kOpSlots];
+    int next = 0;
+};
+OpStage& op_stage(int device) {
+    static std::mutex mu;
+    static std::map<int, OpStage*>* m = new std::map<int, OpStage*>();  // never destroyed (outlives HIP teardown)
+    std::lock_guard<std::mutex> lk(mu);
+    OpStage*& p = (*m)[device];
+    if (!p) p = new OpStage();
+    return *p;
+}
+
+struct DeviceScope {  // restores the caller's current device
+    int prev = -1;
+    DeviceScope() { (void)hipGetDevice(&prev); }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+}  // namespace
+
+}  // namespace rsamd
+
+extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n_ops, uint64_t symbol_size,
+                              void* stream) {
+    if (n_ops && !ops) return RS_ERR_INVALID;
+    const uint64_t nwords = symbol_size / 2, span = nwords * 2;  // an odd last byte is not touched
+    // chains: the ops of each target in array order; every pointer 4-byte aligned (dword kernel)
+    std::vector<SymChain> chains;
+    std::vector<std::vector<SymOpRec>> per;
+    std::unordered_map<uintptr_t, uint32_t> by_target;
+    for (uint64_t i = 0; i < n_ops; ++i) {
+        const rsg_symbol_op_t& o = ops[i];
+        if (o.op > RSG_OP_MADD || !o.a || (uintptr_t(o.a) & 3)) return RS_ERR_INVALID;
+        const bool src = o.op != RSG_OP_MUL;
+        if (src && (!o.b || (uintptr_t(o.b) & 3))) return RS_ERR_INVALID;
+        auto it = by_target.find(uintptr_t(o.a));
+        if (it == by_target.end()) {
+            if (chains.size() >= 0xFFFFFFFFu) return RS_ERR_INVALID;
+            it = by_target.emplace(uintptr_t(o.a), uint32_t(chains.size())).first;
+            chains.push_back(SymChain{static_cast<uint8_t*>(o.a), 0, 0});
+            per.emplace_back();
+        }
+        const bool self = src && o.b == o.a;
+        per[it->second].push_back(SymOpRec{static_cast<const uint8_t*>(src ? o.b : nullptr), o.coef,
+                                           uint32_t(o.op) | (self ? kSymOpSelf : 0u)});
+    }
+    // targets must not overlap each other, and no op may read another op's target (the chains run side
+    // by side): both rejected, nothing is queued
+    std::vector<uintptr_t> tg;
+    tg.reserve(chains.size());
+    for (const SymChain& c : chains) tg.push_back(uintptr_t(c.a));
+    std::sort(tg.begin(), tg.end());
+    for (size_t i = 1; i < tg.size(); ++i)
+        if (tg[i - 1] + span > tg[i]) return RS_ERR_INVALID;
+    if (span) {
+        for (size_t ci = 0; ci < chains.size(); ++ci)
+            for (const SymOpRec& r : per[ci]) {
+                if (!r.b || (r.flags & kSymOpSelf)) continue;
+                const uintptr_t b = uintptr_t(r.b);
+                auto hi = std::upper_bound(tg.begin(), tg.end(), b + span - 1);  // first target past the source
+                if (hi != tg.begin() && *(hi - 1) + span > b) return RS_ERR_INVALID;
+            }
+    }
+    if (chains.empty() || !nwords) return 0;
+    if (device < 0) return RS_ERR_INVALID;
+    DeviceScope scope;
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t nc = chains.size();
+    uint64_t at = 0;
+    for (size_t ci = 0; ci < nc; ++ci) {
+        chains[ci].start = uint32_t(at);
+        chains[ci].count = uint32_t(per[ci].size());
+        at += per[ci].size();
+    }
+    if (at > 0xFFFFFFFFull) return RS_ERR_INVALID;
+    const size_t bytes = nc * sizeof(SymChain) + at * sizeof(SymOpRec);
+    OpStage& S = op_stage(device);
+    std::lock_guard<std::mutex> lk(S.mu);
+    OpSlot& sl = S.slot[S.next];
+    S.next = (S.next + 1) % kOpSlots;
+    if (sl.pending) HIP_TRY(hipEventSynchronize(sl.ev));  // the launch that read this slot is done
+    sl.pending = false;
+    if (!sl.ev) HIP_TRY(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    if (bytes > sl.cap) {
+        if (sl.h) (void)hipHostFree(sl.h);
+        if (sl.d) (void)hipFree(sl.d);
+        sl.h = sl.d = nullptr;
+        sl.cap = 0;
+        const size_t cap = std::max<size_t>(bytes, 64 << 10);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.h), cap, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.d), cap));
+        sl.cap = cap;
+    }
+    SymChain* hc = reinterpret_cast<SymChain*>(sl.h);
+    SymOpRec* ho = reinterpret_cast<SymOpRec*>(sl.h + nc * sizeof(SymChain));
+    std::memcpy(hc, chains.data(), nc * sizeof(SymChain));
+    for (size_t ci = 0; ci < nc; ++ci)
+        if (!per[ci].empty()) std::memcpy(ho + chains[ci].start, per[ci].data(), per[ci].size() * sizeof(SymOpRec));
+    HIP_TRY(hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st));
+    const SymChain* dc = reinterpret_cast<const SymChain*>(sl.d);
+    const SymOpRec* dops = reinterpret_cast<const SymOpRec*>(sl.d + nc * sizeof(SymChain));
+    hipError_t e = hipSuccess;
+    for (size_t c0 = 0; c0 < nc && e == hipSuccess; c0 += 65535)
+        e = launch_symbol_chains(dc + c0, dops, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st);
+    // the slot is reused after this event, whatever happened to the launches
+    HIP_TRY(hipEventRecord(sl.ev, st));
+    sl.pending = true;
+    if (e != hipSuccess) return hip_fail(e, "k_symbol_chains");
+    return 0;
+}
+
 // DFT matrix of fft_transform / fft_transform_cycl: M[j][i] = alpha^(positions[i] * j)
 static std::vector<uint16_t> dft_matrix(const symbol_seq_t* f, const uint16_t* positions, const symbol_seq_t* res) {
     const size_t K = f->length, R = res->length;

@@ -135,7 +135,14 @@ class SymbolStatsT(ctypes.Structure):  # include/rs_amd/rsg.h rsg_symbol_stats_t
         "stuck_bytes", "pinned_bytes")]
 
 
+class SymbolOpT(ctypes.Structure):  # include/rs_amd/rsg.h rsg_symbol_op_t
+    _fields_ = [("a", P), ("b", P), ("coef", u16), ("op", u16), ("reserved", u32)]
+
+
+OP_ADD, OP_MUL, OP_MADD = 0, 1, 2  # RSG_OP_*
+
 _sig("rsg_symbol_stats", ctypes.c_int, ctypes.POINTER(SymbolStatsT))
+_sig("rsg_symbol_ops", ctypes.c_int, ctypes.c_int, ctypes.POINTER(SymbolOpT), u64, u64, P)
 _sig("rsg_symbol_pool_cap", i64, i64)
 _sig("rsg_version", ctypes.c_char_p)
 _sig("rsg_check_enabled", ctypes.c_int)
@@ -437,6 +444,34 @@ def fft(kind, f, res, arg, gf=None):
           "partial": _lib.fft_partial_transform}[kind]
     rc = fn(gf, ctypes.byref(a.seq), _np_ptr(v), ctypes.byref(b.seq))
     return 0 if rc is None else rc
+
+
+# numpy layout of rsg_symbol_op_t (a, b, coef, op, reserved: 24 bytes)
+SYMBOL_OP_DTYPE = np.dtype([("a", "<u8"), ("b", "<u8"), ("coef", "<u2"), ("op", "<u2"), ("reserved", "<u4")])
+assert SYMBOL_OP_DTYPE.itemsize == ctypes.sizeof(SymbolOpT)
+
+
+def symbol_op_array(ops):
+    """rsg_symbol_op_t array from a sequence of (op, a, b, coef) tuples (a / b device addresses as ints, b
+    ignored for OP_MUL), or a SYMBOL_OP_DTYPE array as it is."""
+    if isinstance(ops, np.ndarray) and ops.dtype == SYMBOL_OP_DTYPE:
+        return np.ascontiguousarray(ops)
+    t = np.array([(int(o), int(a), int(b or 0), int(c)) for o, a, b, c in ops], dtype=np.uint64).reshape(-1, 4)
+    arr = np.zeros(len(t), SYMBOL_OP_DTYPE)
+    arr["op"], arr["a"], arr["b"], arr["coef"] = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+    return arr
+
+
+def symbol_ops(ops, symbol_size, device=0, stream=None, check=True):
+    """Batched gf_add / gf_mul / gf_madd on device-accessible symbols (rsg_symbol_ops): `ops` is a sequence
+    of (op, a, b, coef) with op in OP_ADD / OP_MUL / OP_MADD, or a SYMBOL_OP_DTYPE array. Ops on one target
+    apply in order; asynchronous on `stream`. Returns the C rc."""
+    arr = symbol_op_array(ops)
+    rc = _lib.rsg_symbol_ops(device, arr.ctypes.data_as(ctypes.POINTER(SymbolOpT)), len(arr), symbol_size,
+                             _stream_ptr(stream))
+    if check and rc:
+        raise RSError(rc, "rsg_symbol_ops")
+    return rc
 
 
 # ------------------------------------------------------------------------------ device engine

@@ -1622,3 +1622,112 @@ def test_edge_empty_batches_and_no_erasures(k, r):
     assert codec.decode(dev[:0], er) == 0
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), poisoned)
+
+
+# ------------------------------------------------------------------ batched symbol ops (rsg_symbol_ops)
+def _ops_numpy(mem, ops, S):
+    """Sequential restatement of a batch (reference gf65536.c:155-219 per op): mem maps address -> uint8 array."""
+    from _util import gf_tables
+    exp, log = gf_tables()
+    nw = S // 2
+
+    def mul(c, w):
+        return np.where(w != 0, exp[(log[w] + log[c]) % 65535], 0) if c else np.zeros_like(w)
+    for op, a, b, c in ops:
+        wa = mem[a][:2 * nw].view("<u2").astype(np.int64)
+        if op == rs_amd.OP_MUL:
+            wa = mul(c, wa)
+        else:
+            wb = mem[b][:2 * nw].view("<u2").astype(np.int64)
+            wa = wa ^ (wb if op == rs_amd.OP_ADD else mul(c, wb))
+        mem[a][:2 * nw] = wa.astype("<u2").view(np.uint8)
+
+
+def test_symbol_ops_batch_vs_goldens():
+    """Every gf_add / gf_mul / gf_madd golden of the reference (coefficients 0, 1 and general; odd symbol
+    sizes leave the last byte untouched) through ONE rsg_symbol_ops batch per symbol size, on device memory."""
+    from _util import extra_inputs
+    by_size = {}
+    for name in EXTRA_CASES:
+        c = case(name)
+        if c["op"].startswith("gf_"):
+            by_size.setdefault(c["S"], []).append(c)
+    for S, cases in by_size.items():
+        P = (S + 15) // 16 * 16
+        dev = torch.zeros((2 * len(cases), P), dtype=torch.uint8, device="cuda")
+        ops = []
+        for i, c in enumerate(cases):
+            a, b = extra_inputs(c)
+            dev[2 * i, :S] = torch.from_numpy(a)
+            dev[2 * i + 1, :S] = torch.from_numpy(b)
+            kind = {"gf_add": rs_amd.OP_ADD, "gf_mul": rs_amd.OP_MUL, "gf_madd": rs_amd.OP_MADD}[c["op"]]
+            ops.append((kind, dev[2 * i].data_ptr(), dev[2 * i + 1].data_ptr(), c["t"]))
+        rs_amd.symbol_ops(ops, S)
+        torch.cuda.synchronize()
+        out = dev.cpu().numpy()
+        for i, c in enumerate(cases):
+            check_golden(c, out[2 * i, :S].tobytes())
+
+
+@pytest.mark.parametrize("S", [4096, 4096 + 2, 1024 + 6, 65536, 9])
+def test_symbol_ops_chains_vs_numpy(S):
+    """Random batches shaped like the reference's loops over gf_* (_rs_get_evaluator_poly, _rs_restore_erased:
+    many madds accumulating into few targets), with gf_mul / gf_add in the chains, sources equal to their own
+    target, coefficients 0 and 1, targets and sources interleaved in one buffer: bit-exact against the ops
+    applied one after another on the CPU."""
+    rng = np.random.default_rng(S)
+    n_t, n_s, n_ops = 24, 40, 600
+    P = (S + 15) // 16 * 16
+    host = rng.integers(0, 256, (n_t + n_s, P), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    addr = [dev[i].data_ptr() for i in range(n_t + n_s)]
+    ops = []
+    for _ in range(n_ops):
+        t = int(rng.integers(n_t))
+        kind = int(rng.choice([rs_amd.OP_ADD, rs_amd.OP_MUL, rs_amd.OP_MADD], p=[0.15, 0.1, 0.75]))
+        src = t if rng.random() < 0.05 else n_t + int(rng.integers(n_s))
+        coef = int(rng.choice([0, 1, int(rng.integers(2, 65536))], p=[0.05, 0.05, 0.9]))
+        ops.append((kind, addr[t], addr[src], coef))
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    mem = {addr[i]: host[i].copy() for i in range(n_t + n_s)}
+    _ops_numpy(mem, ops, S)
+    want = np.stack([mem[addr[i]] for i in range(n_t + n_s)])
+    assert np.array_equal(got, want)
+
+
+def test_symbol_ops_back_to_back_calls_and_streams():
+    """More calls than staging slots, on two streams, before any synchronisation (each call's op list must
+    survive until its kernel read it), then a reference-style evaluator loop Omega = S * Lambda mod x^r as one
+    batch on the result."""
+    S, n = 2048, 12
+    rng = np.random.default_rng(3)
+    host = rng.integers(0, 256, (2 * n, S), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    mem = {dev[i].data_ptr(): host[i].copy() for i in range(2 * n)}
+    all_ops = []
+    for call in range(10):
+        i = call % n
+        ops = [(rs_amd.OP_MADD, dev[i].data_ptr(), dev[n + j].data_ptr(), int(rng.integers(1, 65536)))
+               for j in range(n)]
+        st = streams[call % 2]
+        st.wait_stream(streams[(call + 1) % 2])  # calls on one target are ordered by the caller
+        rs_amd.symbol_ops(ops, S, stream=st)
+        all_ops += ops
+    torch.cuda.synchronize()
+    _ops_numpy(mem, all_ops, S)
+    assert np.array_equal(dev.cpu().numpy(), np.stack([mem[dev[i].data_ptr()] for i in range(2 * n)]))
+    # evaluator: om[i + j] ^= lam[i] * syn[j] (reference reed_solomon.c:235-245), targets om, sources syn
+    r = 8
+    syn = torch.from_numpy(rng.integers(0, 256, (r, S), dtype=np.uint8)).cuda()
+    om = torch.zeros((r, S), dtype=torch.uint8, device="cuda")
+    lam = [int(x) for x in rng.integers(0, 65536, r)]
+    ops = [(rs_amd.OP_MADD, om[i + j].data_ptr(), syn[j].data_ptr(), lam[i]) for i in range(r) for j in range(r - i)]
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+    m2 = {om[i].data_ptr(): np.zeros(S, np.uint8) for i in range(r)}
+    m2.update({syn[j].data_ptr(): syn[j].cpu().numpy() for j in range(r)})
+    _ops_numpy(m2, ops, S)
+    assert np.array_equal(om.cpu().numpy(), np.stack([m2[om[i].data_ptr()] for i in range(r)]))

@@ -477,3 +477,26 @@ def test_checked_launch_mode_switch(value, want):
             % os.path.join(REPO, "reed-solomon_amd"))
     out = subprocess.check_output([sys.executable, "-c", code], env=env, text=True)
     assert out.strip().splitlines()[-1] == str(want)
+
+
+def test_symbol_ops_validation_without_gpu():
+    """rsg_symbol_ops rejects a batch before anything is queued (RS_ERR_INVALID, no device touched): an
+    unknown op, a null or misaligned pointer, overlapping targets, a source that is another op's target
+    (chains run side by side). An empty batch, or one of zero-word symbols, is a no-op (rc 0)."""
+    A, B, C = 0x10000, 0x20000, 0x30000  # fake 4-byte aligned addresses: never dereferenced here
+    S = 4096
+    inval = [
+        [(3, A, B, 1)],                                    # unknown op
+        [(rs_amd.OP_ADD, 0, B, 0)],                        # null target
+        [(rs_amd.OP_MADD, A, 0, 5)],                       # null source
+        [(rs_amd.OP_ADD, A + 2, B, 0)],                    # misaligned target
+        [(rs_amd.OP_MADD, A, B + 1, 7)],                   # misaligned source
+        [(rs_amd.OP_ADD, A, B, 0), (rs_amd.OP_ADD, A + S - 4, C, 0)],  # overlapping targets
+        [(rs_amd.OP_ADD, A, B, 0), (rs_amd.OP_MADD, C, A, 9)],        # reads another chain's target
+        [(rs_amd.OP_ADD, A, B, 0), (rs_amd.OP_MADD, C, A + 100, 9)],  # reads inside another chain's target
+        [(rs_amd.OP_MUL, B, 0, 3), (rs_amd.OP_ADD, A, B - S + 2, 0)],  # source overlaps a target's start
+    ]
+    for ops in inval:
+        assert rs_amd.symbol_ops(ops, S, stream=0, check=False) == rs_amd.RS_ERR_INVALID, ops
+    assert rs_amd.symbol_ops([], S, stream=0) == 0
+    assert rs_amd.symbol_ops([(rs_amd.OP_ADD, A, B, 0)], 1, stream=0) == 0  # no whole word: nothing to do
