@@ -6,7 +6,7 @@ pattern per stripe (device-built plans; for GF(2^16) codes, "batch16", one plan 
 per pattern), the GF(2^16) syndrome route ("route": k_cs16 + k_bs16 / second stage), the per-call
 drop-in API on seq_create arenas ("dropin"); round 3: the per-stripe GF(2^16) route ("ps16"), decode
 patterns closed under a Frobenius power ("orbit": the k_bs16 stage over row orbits) and the per-call API
-on registered symbol_create buffers ("dropin_reg"). Prints one JSON line per case and a summary.
+on registered symbol_create buffers ("dropin_reg"); round 6: batched symbol ops (rsg_symbol_ops, "symops"). Prints one JSON line per case and a summary.
 usage: fuzz_parity.py [seed] [seconds] [family,family,...]"""
 import json
 import os
@@ -202,7 +202,46 @@ def one_orbit():
     return dict(family="orbit", k=k, r=r, S=S, stripes=n, t=int(er.sum()), step=step, decode=kern, ok=ok)
 
 
+def one_symops():
+    """rsg_symbol_ops: random chains of gf_add / gf_mul / gf_madd (coefficients 0, 1 and general, sources equal
+    to their own target) over random symbol sizes (odd word counts, odd byte counts), against the ops applied
+    one after another with numpy (GF(2^16) exp / log tables)."""
+    from _util import gf_tables
+    exp, log = gf_tables()
+    S = int(rng.choice([2, 6, 9, 1024, 1030, 4096, 65536])) + 2 * int(rng.integers(0, 8)) * int(rng.integers(0, 2))
+    n_t, n_s = int(rng.integers(1, 40)), int(rng.integers(1, 40))
+    P = (S + 15) // 16 * 16
+    host = rng.integers(0, 256, (n_t + n_s, P), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    addr = [dev[i].data_ptr() for i in range(n_t + n_s)]
+    ops = []
+    for _ in range(int(rng.integers(1, 400))):
+        t = int(rng.integers(n_t))
+        kind = int(rng.choice([0, 1, 2], p=[0.2, 0.1, 0.7]))
+        src = t if rng.random() < 0.05 else n_t + int(rng.integers(n_s))
+        coef = int(rng.choice([0, 1, int(rng.integers(2, 65536))], p=[0.05, 0.05, 0.9]))
+        ops.append((kind, addr[t], addr[src], coef))
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    nw = S // 2
+    want = host.copy()
+    idx = {a: i for i, a in enumerate(addr)}
+    for kind, a, b, c in ops:
+        wa = want[idx[a], :2 * nw].view("<u2").astype(np.int64)
+        x = wa if kind == 1 else want[idx[b], :2 * nw].view("<u2").astype(np.int64)
+        y = x if (kind == 0 or (kind == 2 and c == 1)) else (
+            np.where(x != 0, exp[(log[x] + log[c]) % 65535], 0) if c else np.zeros_like(x))
+        if kind == 1 and c == 1:
+            y = x
+        wa = y if kind == 1 else wa ^ y
+        want[idx[a], :2 * nw] = wa.astype("<u2").view(np.uint8)
+    return dict(family="symops", S=S, targets=n_t, sources=n_s, ops=len(ops), ok=bool(np.array_equal(got, want)))
+
+
 def one(family):
+    if family == "symops":
+        return one_symops()
     if family == "dropin":
         return one_dropin()
     if family == "dropin_reg":
@@ -286,7 +325,7 @@ def one(family):
 
 if __name__ == "__main__":
     families = sys.argv[3].split(",") if len(sys.argv) > 3 else ["xj", "generic", "m16", "route", "reenc", "batch",
-                                                                 "batch16", "dropin", "ps16", "orbit", "dropin_reg"]
+                                                                 "batch16", "dropin", "ps16", "orbit", "dropin_reg", "symops"]
     i = 0
     while time.time() < t_end:
         fam = families[i % len(families)]

@@ -63,10 +63,13 @@ def per_leg_composite(d, counter, legs):
         if got != want:  # not at a leg boundary (e.g. a dense first launch): skip one dispatch
             i += 1
             continue
-        out[leg].append(sum(v for _, v in seq[i:i + len(want)]))
+        split = {}
+        for part, v in seq[i:i + len(want)]:
+            split[part] = split.get(part, 0.0) + v
+        out[leg].append((sum(v for _, v in seq[i:i + len(want)]), split))
         i += len(want)
         li += 1
-    return {leg: sorted(v) for leg, v in out.items()}
+    return {leg: sorted(v, key=lambda x: x[0]) for leg, v in out.items()}
 
 
 def matcher(bench_kernel):
@@ -100,12 +103,17 @@ def main():
             if not fetch or not write:
                 print(f"no complete {bench_kernel} sequences", file=sys.stderr)
                 continue
-            fetch_b = med(fetch) * 1024 * 2
-            write_b = med(write) * 1024
+            (fv, fsplit), (wv, wsplit) = med(fetch), med(write)
+            fetch_b = fv * 1024 * 2
+            write_b = wv * 1024
+            # per component kernel (of the median launch): corrected fetch + write bytes
+            split = {part: {"fetch_bytes_corrected": fsplit.get(part, 0.0) * 1024 * 2,
+                            "write_bytes": wsplit.get(part, 0.0) * 1024} for part in legs[leg]}
             records.append({"leg": leg, "src_hash": kernel_src_hash(bench_kernel), "bench_kernel": bench_kernel,
                             "config": cfg, "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
                             "traffic_bytes": fetch_b + write_b, "dispatches": [len(fetch), len(write)],
-                            "components": legs[leg], "raw_kib": {"FETCH_SIZE": med(fetch), "WRITE_SIZE": med(write)}})
+                            "components": legs[leg], "component_bytes": split,
+                            "raw_kib": {"FETCH_SIZE": fv, "WRITE_SIZE": wv}})
             continue
         match = matcher(bench_kernel)
         fetch = per_dispatch(fd, "FETCH_SIZE", match)

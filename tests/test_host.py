@@ -500,3 +500,30 @@ def test_symbol_ops_validation_without_gpu():
         assert rs_amd.symbol_ops(ops, S, stream=0, check=False) == rs_amd.RS_ERR_INVALID, ops
     assert rs_amd.symbol_ops([], S, stream=0) == 0
     assert rs_amd.symbol_ops([(rs_amd.OP_ADD, A, B, 0)], 1, stream=0) == 0  # no whole word: nothing to do
+
+
+def test_traffic_composite_legs_and_component_split(tmp_path):
+    """scripts/traffic.py on synthetic rocprofv3 counter CSVs: composite legs (the GF(2^16) route's
+    cs16t + bs16) are cut out of the dispatch order encode / decode alternately, summed per launch, and split
+    per component kernel; a stray dispatch at a leg boundary (a dense first launch) is skipped."""
+    import csv
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(REPO, "scripts"))
+    import traffic
+    d = tmp_path / "f"
+    d.mkdir()
+    rows = [(1, "rsamd::k_bs16(x)", 5.0),  # boundary stray: skipped
+            (2, "rsamd::k_cs16t(x)", 100.0), (3, "rsamd::k_bs16(x)", 10.0),   # encode 1
+            (4, "rsamd::k_cs16t(x)", 300.0), (5, "rsamd::k_bs16(x)", 30.0),   # decode 1
+            (6, "rsamd::k_cs16t(x)", 110.0), (7, "rsamd::k_bs16(x)", 12.0),   # encode 2
+            (8, "rsamd::k_cs16t(x)", 290.0), (9, "rsamd::k_bs16(x)", 31.0)]   # decode 2
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for did, name, v in rows:
+            for half in (0.5, 0.5):  # counters come per XCD / SE: summed per dispatch
+                w.writerow({"Dispatch_Id": did, "Kernel_Name": name, "Counter_Name": "FETCH_SIZE", "Counter_Value": v * half})
+    out = traffic.per_leg_composite(str(d), "FETCH_SIZE", {"encode": ["cs16t", "bs16"], "decode": ["cs16t", "bs16"]})
+    assert [t for t, _ in out["encode"]] == [110.0, 122.0]
+    assert [t for t, _ in out["decode"]] == [321.0, 330.0]
+    assert out["decode"][0][1] == {"cs16t": 290.0, "bs16": 31.0}
