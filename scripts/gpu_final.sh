@@ -24,6 +24,6 @@ TR=${CLOSE:-final}/c2 bash scripts/gpu_traffic.sh --k 10 --r 4 --symbol 4096 --s
 timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 2 --k 4096 --r 1024 --symbol 1024 --stripes 1024 --no-extras > $D/bench_c5.log 2>&1 || { tail -5 $D/bench_c5.log; exit 1; }
 grep '^{' $D/bench_c5.log | cut -c1-300
 if [ "${FUZZ:-0}" = 1 ]; then
-  timeout -k 10 420 python3 -u scripts/fuzz_parity.py 404 300 > $D/fuzz.log 2>&1 || { tail -20 $D/fuzz.log; exit 1; }
+  timeout -k 10 360 python3 -u scripts/fuzz_parity.py 606 240 > $D/fuzz.log 2>&1 || { tail -20 $D/fuzz.log; exit 1; }
   tail -1 $D/fuzz.log
 fi
