@@ -596,9 +596,9 @@ def symbol_ops_leg(dev, stream):
         ops["a"] = tgt.data_ptr() + np.repeat(np.arange(n_t, dtype=np.uint64), per_t) * S
         ops["b"] = src.data_ptr() + np.tile(np.arange(per_t, dtype=np.uint64), n_t) * S
         ops["coef"] = coefs.reshape(-1)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(9)]
         host = []
-        for e0, e1 in ev:
+        for e0, e1 in ev:  # calls 0-3 fill the library's 4 op-list staging slots: not counted
             tgt.zero_()
             torch.cuda.synchronize()
             torch.cuda._sleep(2_000_000)  # the stream waits ~1 ms: the events bracket the op-list copy + kernel only
@@ -608,7 +608,7 @@ def symbol_ops_leg(dev, stream):
             host.append(time.perf_counter() - t0)
             e1.record(stream)
         torch.cuda.synchronize()
-        ms = float(np.median([a.elapsed_time(b) for a, b in ev[1:]]))
+        ms = float(np.median([a.elapsed_time(b) for a, b in ev[4:]]))
         got = tgt.cpu().numpy().view("<u2").astype(np.int64)
         ws = src.cpu().numpy().view("<u2").astype(np.int64)
         want = np.zeros_like(got)
@@ -618,11 +618,12 @@ def symbol_ops_leg(dev, stream):
             want ^= prod
         n_ops = n_t * per_t
         out[f"S{S}"] = {"ops": n_ops, "targets": n_t, "ops_per_target": per_t, "call_ms": round(ms, 4),
-                        "us_per_op": round(ms * 1e3 / n_ops, 4), "host_us_per_call": round(float(np.median(host[1:])) * 1e6, 1),
-                        "host_us_per_op": round(float(np.median(host[1:])) * 1e6 / n_ops, 4),
+                        "us_per_op": round(ms * 1e3 / n_ops, 4), "host_us_per_call": round(float(np.median(host[4:])) * 1e6, 1),
+                        "host_us_per_op": round(float(np.median(host[4:])) * 1e6 / n_ops, 4),
                         "source_GBps": round(n_ops * S / ms / 1e6, 1), "parity": "ok" if np.array_equal(got, want) else "MISMATCH"}
     out["note"] = ("gf_madd chains in one rsg_symbol_ops call (SYMBOL_OP_DTYPE array); call_ms = HIP events around the "
-                   "op-list copy + kernel (stream held by a spin kernel while the call is queued); host_us = the C call's "
+                   "op-list copy + kernel (stream held by a spin kernel while the call is queued), median of 5 calls after 4 "
+                   "warm-up calls; host_us = the C call's "
                    "host time (validation, chains, staging). The per-call gf_madd on host symbols is a synchronous round "
                    "trip of ~16-23 us (DESIGN.md section 9)")
     return out

@@ -1198,19 +1198,20 @@ __device__ __forceinline__ void gf_mul_consts(uint32_t c, uint32_t (&K)[16]) {
     }
 }
 
-constexpr int kSymOpDw = 4;     // dwords per lane (stride 64): 1 KiB of a symbol per wave
 constexpr int kSymOpGroup = 4;  // ops whose sources are loaded together
 
+// DW dwords per lane (stride 64): 256 * DW bytes of a symbol per wave
+template <int DW>
 __global__ void __launch_bounds__(64) k_symbol_chains(const SymChain* __restrict__ chains,
                                                       const SymOpRec* __restrict__ ops, uint64_t nwords) {
     const SymChain ch = chains[blockIdx.y];
     const uint64_t nd = nwords / 2;  // whole dwords; an odd word count leaves one 16-bit word at dword nd
     const bool odd = nwords & 1;
-    const uint64_t d0 = uint64_t(blockIdx.x) * (64 * kSymOpDw) + threadIdx.x;
-    uint32_t acc[kSymOpDw];
-    auto load = [&](const uint8_t* p, uint32_t (&v)[kSymOpDw]) {
+    const uint64_t d0 = uint64_t(blockIdx.x) * (64 * DW) + threadIdx.x;
+    uint32_t acc[DW];
+    auto load = [&](const uint8_t* p, uint32_t (&v)[DW]) {
 #pragma unroll
-        for (int j = 0; j < kSymOpDw; ++j) {
+        for (int j = 0; j < DW; ++j) {
             const uint64_t d = d0 + 64u * j;
             v[j] = d < nd ? reinterpret_cast<const uint32_t*>(p)[d]
                           : (odd && d == nd ? uint32_t(reinterpret_cast<const uint16_t*>(p)[2 * d]) : 0u);
@@ -1224,42 +1225,42 @@ __global__ void __launch_bounds__(64) k_symbol_chains(const SymChain* __restrict
     const uint32_t end = ch.start + ch.count;
     // sources go in by groups of kSymOpGroup ops; group g + 1's loads are issued before group g's work, so
     // up to two groups of loads are in flight against one wait per group
-    auto load_group = [&](uint32_t g0, uint32_t (&x)[kSymOpGroup][kSymOpDw]) {
+    auto load_group = [&](uint32_t g0, uint32_t (&x)[kSymOpGroup][DW]) {
 #pragma unroll
         for (int q = 0; q < kSymOpGroup; ++q)
             if (g0 + q < end && loads_src(g0 + q)) load(ops[g0 + q].b, x[q]);
     };
-    auto apply = [&](uint32_t o, const uint32_t (&xs)[kSymOpDw]) {
+    auto apply = [&](uint32_t o, const uint32_t (&xs)[DW]) {
         const uint32_t f = ops[o].flags, c = ops[o].coef, kind = f & 3u;
-        uint32_t cur[kSymOpDw];
+        uint32_t cur[DW];
 #pragma unroll
-        for (int j = 0; j < kSymOpDw; ++j) cur[j] = (f & kSymOpSelf) ? acc[j] : xs[j];
+        for (int j = 0; j < DW; ++j) cur[j] = (f & kSymOpSelf) ? acc[j] : xs[j];
         if (kind == 1u) {  // a = c a
             if (c == 0u) {
 #pragma unroll
-                for (int j = 0; j < kSymOpDw; ++j) acc[j] = 0u;
+                for (int j = 0; j < DW; ++j) acc[j] = 0u;
             } else if (c != 1u) {
                 uint32_t K[16];
                 gf_mul_consts(c, K);
 #pragma unroll
-                for (int j = 0; j < kSymOpDw; ++j) acc[j] = gf_mul_packed(acc[j], K);
+                for (int j = 0; j < DW; ++j) acc[j] = gf_mul_packed(acc[j], K);
             }
         } else if (kind == 0u || c == 1u) {  // a ^= b
 #pragma unroll
-            for (int j = 0; j < kSymOpDw; ++j) acc[j] ^= cur[j];
+            for (int j = 0; j < DW; ++j) acc[j] ^= cur[j];
         } else if (c != 0u) {  // a ^= c b
             uint32_t K[16];
             gf_mul_consts(c, K);
 #pragma unroll
-            for (int j = 0; j < kSymOpDw; ++j) acc[j] ^= gf_mul_packed(cur[j], K);
+            for (int j = 0; j < DW; ++j) acc[j] ^= gf_mul_packed(cur[j], K);
         }
     };
-    auto run_group = [&](uint32_t g0, const uint32_t (&x)[kSymOpGroup][kSymOpDw]) {
+    auto run_group = [&](uint32_t g0, const uint32_t (&x)[kSymOpGroup][DW]) {
 #pragma unroll
         for (int q = 0; q < kSymOpGroup; ++q)
             if (g0 + q < end) apply(g0 + q, x[q]);
     };
-    uint32_t xa[kSymOpGroup][kSymOpDw], xb[kSymOpGroup][kSymOpDw];
+    uint32_t xa[kSymOpGroup][DW], xb[kSymOpGroup][DW];
     load_group(ch.start, xa);
     for (uint32_t g0 = ch.start; g0 < end; g0 += 2 * kSymOpGroup) {
         load_group(g0 + kSymOpGroup, xb);
@@ -1268,7 +1269,7 @@ __global__ void __launch_bounds__(64) k_symbol_chains(const SymChain* __restrict
         run_group(g0 + kSymOpGroup, xb);
     }
 #pragma unroll
-    for (int j = 0; j < kSymOpDw; ++j) {
+    for (int j = 0; j < DW; ++j) {
         const uint64_t d = d0 + 64u * j;
         if (d < nd)
             reinterpret_cast<uint32_t*>(ch.a)[d] = acc[j];
@@ -1278,11 +1279,20 @@ __global__ void __launch_bounds__(64) k_symbol_chains(const SymChain* __restrict
 }
 
 hipError_t launch_symbol_chains(const SymChain* chains, const SymOpRec* ops, uint32_t n_chains, uint64_t nwords,
-                                hipStream_t st) {
+                                hipStream_t st, int dw) {
     if (!n_chains || !nwords) return hipSuccess;
-    const uint64_t spans = (nwords / 2 + (nwords & 1) + 64 * kSymOpDw - 1) / (64 * kSymOpDw);
+    const uint64_t nd = nwords / 2 + (nwords & 1);
+    const uint64_t spans = (nd + 64 * uint64_t(dw) - 1) / (64 * uint64_t(dw));
     if (spans > 0x7FFFFFFFu || n_chains > 65535u) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_symbol_chains, dim3(unsigned(spans), n_chains), dim3(64), 0, st, chains, ops, nwords);
+    const dim3 grid(unsigned(spans), n_chains);
+    if (dw == 1)
+        hipLaunchKernelGGL(k_symbol_chains<1>, grid, dim3(64), 0, st, chains, ops, nwords);
+    else if (dw == 2)
+        hipLaunchKernelGGL(k_symbol_chains<2>, grid, dim3(64), 0, st, chains, ops, nwords);
+    else if (dw == 4)
+        hipLaunchKernelGGL(k_symbol_chains<4>, grid, dim3(64), 0, st, chains, ops, nwords);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

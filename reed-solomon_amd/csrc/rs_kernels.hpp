@@ -214,8 +214,9 @@ struct SymOpRec {
     uint32_t coef, flags;
 };
 constexpr uint32_t kSymOpSelf = 0x100u;
+// dw: dwords per lane (1, 2 or 4), i.e. 256 * dw bytes of a symbol per wave
 hipError_t launch_symbol_chains(const SymChain* chains, const SymOpRec* ops, uint32_t n_chains, uint64_t nwords,
-                                hipStream_t st);
+                                hipStream_t st, int dw);
 
 int apply_tile_rows(int m, int R);
 // V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)

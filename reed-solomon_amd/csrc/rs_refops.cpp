@@ -384,58 +384,41 @@ struct DeviceScope {  // restores the caller's current device
 extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n_ops, uint64_t symbol_size,
                               void* stream) {
     if (n_ops && !ops) return RS_ERR_INVALID;
+    if (n_ops > 0xFFFFFFFFull) return RS_ERR_INVALID;
     const uint64_t nwords = symbol_size / 2, span = nwords * 2;  // an odd last byte is not touched
-    // chains: the ops of each target in array order; every pointer 4-byte aligned (dword kernel)
-    std::vector<SymChain> chains;
-    std::vector<std::vector<SymOpRec>> per;
-    std::unordered_map<uintptr_t, uint32_t> by_target;
+    // chains: the ops of each target in array order = the (target, index) pairs sorted; every pointer 4-byte
+    // aligned (dword kernel)
+    std::vector<std::pair<uintptr_t, uint32_t>> order(n_ops);
     for (uint64_t i = 0; i < n_ops; ++i) {
         const rsg_symbol_op_t& o = ops[i];
         if (o.op > RSG_OP_MADD || !o.a || (uintptr_t(o.a) & 3)) return RS_ERR_INVALID;
-        const bool src = o.op != RSG_OP_MUL;
-        if (src && (!o.b || (uintptr_t(o.b) & 3))) return RS_ERR_INVALID;
-        auto it = by_target.find(uintptr_t(o.a));
-        if (it == by_target.end()) {
-            if (chains.size() >= 0xFFFFFFFFu) return RS_ERR_INVALID;
-            it = by_target.emplace(uintptr_t(o.a), uint32_t(chains.size())).first;
-            chains.push_back(SymChain{static_cast<uint8_t*>(o.a), 0, 0});
-            per.emplace_back();
-        }
-        const bool self = src && o.b == o.a;
-        per[it->second].push_back(SymOpRec{static_cast<const uint8_t*>(src ? o.b : nullptr), o.coef,
-                                           uint32_t(o.op) | (self ? kSymOpSelf : 0u)});
+        if (o.op != RSG_OP_MUL && (!o.b || (uintptr_t(o.b) & 3))) return RS_ERR_INVALID;
+        order[i] = {uintptr_t(o.a), uint32_t(i)};
     }
-    // targets must not overlap each other, and no op may read another op's target (the chains run side
-    // by side): both rejected, nothing is queued
+    std::sort(order.begin(), order.end());
+    // distinct targets (ascending): they must not overlap each other, and no op may read another op's target
+    // (the chains run side by side): both rejected, nothing is queued
     std::vector<uintptr_t> tg;
-    tg.reserve(chains.size());
-    for (const SymChain& c : chains) tg.push_back(uintptr_t(c.a));
-    std::sort(tg.begin(), tg.end());
+    for (size_t j = 0; j < order.size(); ++j)
+        if (!j || order[j].first != order[j - 1].first) tg.push_back(order[j].first);
     for (size_t i = 1; i < tg.size(); ++i)
         if (tg[i - 1] + span > tg[i]) return RS_ERR_INVALID;
     if (span) {
-        for (size_t ci = 0; ci < chains.size(); ++ci)
-            for (const SymOpRec& r : per[ci]) {
-                if (!r.b || (r.flags & kSymOpSelf)) continue;
-                const uintptr_t b = uintptr_t(r.b);
-                auto hi = std::upper_bound(tg.begin(), tg.end(), b + span - 1);  // first target past the source
-                if (hi != tg.begin() && *(hi - 1) + span > b) return RS_ERR_INVALID;
-            }
+        for (uint64_t i = 0; i < n_ops; ++i) {
+            const rsg_symbol_op_t& o = ops[i];
+            if (o.op == RSG_OP_MUL || o.b == o.a) continue;
+            const uintptr_t b = uintptr_t(o.b);
+            auto hi = std::upper_bound(tg.begin(), tg.end(), b + span - 1);  // first target past the source
+            if (hi != tg.begin() && *(hi - 1) + span > b) return RS_ERR_INVALID;
+        }
     }
-    if (chains.empty() || !nwords) return 0;
+    if (tg.empty() || !nwords) return 0;
     if (device < 0) return RS_ERR_INVALID;
     DeviceScope scope;
     HIP_TRY(hipSetDevice(device));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t nc = chains.size();
-    uint64_t at = 0;
-    for (size_t ci = 0; ci < nc; ++ci) {
-        chains[ci].start = uint32_t(at);
-        chains[ci].count = uint32_t(per[ci].size());
-        at += per[ci].size();
-    }
-    if (at > 0xFFFFFFFFull) return RS_ERR_INVALID;
-    const size_t bytes = nc * sizeof(SymChain) + at * sizeof(SymOpRec);
+    const size_t nc = tg.size();
+    const size_t bytes = nc * sizeof(SymChain) + n_ops * sizeof(SymOpRec);
     OpStage& S = op_stage(device);
     std::lock_guard<std::mutex> lk(S.mu);
     OpSlot& sl = S.slot[S.next];
@@ -448,22 +431,40 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
         if (sl.d) (void)hipFree(sl.d);
         sl.h = sl.d = nullptr;
         sl.cap = 0;
-        const size_t cap = std::max<size_t>(bytes, 64 << 10);
+        const size_t cap = std::max<size_t>(bytes + bytes / 2, 1 << 20);  // grows by half again: few reallocations
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.h), cap, hipHostMallocDefault));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.d), cap));
         sl.cap = cap;
     }
+    // records straight into the page-locked slot: chains, then the ops in chain order
     SymChain* hc = reinterpret_cast<SymChain*>(sl.h);
     SymOpRec* ho = reinterpret_cast<SymOpRec*>(sl.h + nc * sizeof(SymChain));
-    std::memcpy(hc, chains.data(), nc * sizeof(SymChain));
-    for (size_t ci = 0; ci < nc; ++ci)
-        if (!per[ci].empty()) std::memcpy(ho + chains[ci].start, per[ci].data(), per[ci].size() * sizeof(SymOpRec));
+    size_t ci = 0;
+    for (size_t j = 0; j < order.size(); ++j) {
+        const rsg_symbol_op_t& o = ops[order[j].second];
+        if (j && order[j].first != order[j - 1].first) ++ci;
+        if (!j || order[j].first != order[j - 1].first) hc[ci] = SymChain{static_cast<uint8_t*>(o.a), uint32_t(j), 0};
+        ++hc[ci].count;
+        const bool src = o.op != RSG_OP_MUL;
+        ho[j] = SymOpRec{static_cast<const uint8_t*>(src ? o.b : nullptr), o.coef,
+                         uint32_t(o.op) | (src && o.b == o.a ? kSymOpSelf : 0u)};
+    }
     HIP_TRY(hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st));
     const SymChain* dc = reinterpret_cast<const SymChain*>(sl.d);
     const SymOpRec* dops = reinterpret_cast<const SymOpRec*>(sl.d + nc * sizeof(SymChain));
+    // dwords per lane: the largest of 4 / 2 that still gives >= 4096 waves (4 per SIMD), else 1 (more waves
+    // for few or short targets: the chains are bound by load latency); RS_AMD_SYMOP_DW = 1 / 2 / 4 overrides
+    static const int dw_env = [] {
+        const char* e = std::getenv("RS_AMD_SYMOP_DW");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    const uint64_t nd = nwords / 2 + (nwords & 1);
+    auto waves = [&](uint64_t dw) { return uint64_t(nc) * ((nd + 64 * dw - 1) / (64 * dw)); };
+    const int dw = dw_env ? dw_env : waves(4) >= 4096 ? 4 : waves(2) >= 4096 ? 2 : 1;
     hipError_t e = hipSuccess;
     for (size_t c0 = 0; c0 < nc && e == hipSuccess; c0 += 65535)
-        e = launch_symbol_chains(dc + c0, dops, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st);
+        e = launch_symbol_chains(dc + c0, dops, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st, dw);
     // the slot is reused after this event, whatever happened to the launches
     HIP_TRY(hipEventRecord(sl.ev, st));
     sl.pending = true;
