@@ -194,8 +194,8 @@ def _alive(pid):
 
 def test_bench_launcher_eight_ranks_dry_run():
     """The C4 shape (BASELINE.json configs[3]): `bench.py --gpus 8` at the default 8192 stripes per rank
-    reports 65536 stripes, 8 distinct ranks on 8 distinct devices, per-rank times, and -- like every
-    N -- a CPU baseline timed by rank 0 after the timed region while the other ranks wait."""
+    reports 65536 stripes, 8 distinct ranks on 8 distinct devices and per-rank times; the CPU baseline
+    belongs to the N = 1 line only (rank 0 of a single-rank run times it after the timed region)."""
     p = _run_bench("--gpus", "8", "--dry-run", "--steps", "2", "--cpu-stripes", "2", "--cpu-seconds", "0.1")
     assert p.returncode == 0, p.stderr[-2000:]
     line = _bench_line(p.stdout)
@@ -203,10 +203,14 @@ def test_bench_launcher_eight_ranks_dry_run():
     assert line["config"]["stripes_total"] == 65536
     assert [e["rank"] for e in line["per_rank"]] == list(range(8))
     assert len({e["pci_bus_id"] for e in line["per_rank"]}) == 8
-    cpu = line["cpu_baseline"]
-    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert line["cpu_baseline"] is None
     pids = _rank_pids(p.stderr)
     assert sorted(pids) == list(range(8)) and not any(_alive(q) for q in pids.values())
+    # N = 1 through the same launcher: the line carries the baseline
+    p1 = _run_bench("--gpus", "1", "--dry-run", "--steps", "2", "--cpu-stripes", "2", "--cpu-seconds", "0.1")
+    assert p1.returncode == 0, p1.stderr[-2000:]
+    cpu = _bench_line(p1.stdout)["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1
 
 
 def test_bench_launcher_rank_failure_stops_everyone():
