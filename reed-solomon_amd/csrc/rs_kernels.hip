@@ -1176,126 +1176,6 @@ hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc,
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------ batched symbol ops
-// rsg_symbol_ops: chains of gf_add / gf_mul / gf_madd (reference gf65536.c:155-219) on one target symbol
-// each, applied in order. One wave per (1 KiB column span, chain): the target's four dwords per lane stay in
-// registers across the chain, every op reads its source once (sources are loaded a group of ops ahead of
-// their use), the target is written once. c * x on two packed words is bit-sliced with the
-// op's 16 constants c * alpha^i (uniform, built on the scalar unit):  c x = XOR_i [x_i] c alpha^i, the lane
-// masks of bit i of both halves formed by one 24-bit multiply (((x >> i) & 0x10001) * 0xFFFF).
-__device__ __forceinline__ uint32_t gf_mul_packed(uint32_t x, const uint32_t (&K)[16]) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) r ^= __umul24((x >> i) & 0x10001u, 0xFFFFu) & K[i];
-    return r;
-}
-
-__device__ __forceinline__ void gf_mul_consts(uint32_t c, uint32_t (&K)[16]) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        K[i] = c | (c << 16);
-        c = (c << 1) ^ ((c >> 15) ? 0x1002Du : 0u);  // c * alpha mod x^16 + x^5 + x^3 + x^2 + 1
-    }
-}
-
-constexpr int kSymOpGroup = 4;  // ops whose sources are loaded together
-
-// DW dwords per lane (stride 64): 256 * DW bytes of a symbol per wave
-template <int DW>
-__global__ void __launch_bounds__(64) k_symbol_chains(const SymChain* __restrict__ chains,
-                                                      const SymOpRec* __restrict__ ops, uint64_t nwords) {
-    const SymChain ch = chains[blockIdx.y];
-    const uint64_t nd = nwords / 2;  // whole dwords; an odd word count leaves one 16-bit word at dword nd
-    const bool odd = nwords & 1;
-    const uint64_t d0 = uint64_t(blockIdx.x) * (64 * DW) + threadIdx.x;
-    uint32_t acc[DW];
-    auto load = [&](const uint8_t* p, uint32_t (&v)[DW]) {
-#pragma unroll
-        for (int j = 0; j < DW; ++j) {
-            const uint64_t d = d0 + 64u * j;
-            v[j] = d < nd ? reinterpret_cast<const uint32_t*>(p)[d]
-                          : (odd && d == nd ? uint32_t(reinterpret_cast<const uint16_t*>(p)[2 * d]) : 0u);
-        }
-    };
-    load(ch.a, acc);
-    auto loads_src = [&](uint32_t o) {  // op o reads a source other than the target
-        const uint32_t f = ops[o].flags;
-        return (f & 3u) != 1u && !(f & kSymOpSelf) && !((f & 3u) == 2u && ops[o].coef == 0u);
-    };
-    const uint32_t end = ch.start + ch.count;
-    // sources go in by groups of kSymOpGroup ops; group g + 1's loads are issued before group g's work, so
-    // up to two groups of loads are in flight against one wait per group
-    auto load_group = [&](uint32_t g0, uint32_t (&x)[kSymOpGroup][DW]) {
-#pragma unroll
-        for (int q = 0; q < kSymOpGroup; ++q)
-            if (g0 + q < end && loads_src(g0 + q)) load(ops[g0 + q].b, x[q]);
-    };
-    auto apply = [&](uint32_t o, const uint32_t (&xs)[DW]) {
-        const uint32_t f = ops[o].flags, c = ops[o].coef, kind = f & 3u;
-        uint32_t cur[DW];
-#pragma unroll
-        for (int j = 0; j < DW; ++j) cur[j] = (f & kSymOpSelf) ? acc[j] : xs[j];
-        if (kind == 1u) {  // a = c a
-            if (c == 0u) {
-#pragma unroll
-                for (int j = 0; j < DW; ++j) acc[j] = 0u;
-            } else if (c != 1u) {
-                uint32_t K[16];
-                gf_mul_consts(c, K);
-#pragma unroll
-                for (int j = 0; j < DW; ++j) acc[j] = gf_mul_packed(acc[j], K);
-            }
-        } else if (kind == 0u || c == 1u) {  // a ^= b
-#pragma unroll
-            for (int j = 0; j < DW; ++j) acc[j] ^= cur[j];
-        } else if (c != 0u) {  // a ^= c b
-            uint32_t K[16];
-            gf_mul_consts(c, K);
-#pragma unroll
-            for (int j = 0; j < DW; ++j) acc[j] ^= gf_mul_packed(cur[j], K);
-        }
-    };
-    auto run_group = [&](uint32_t g0, const uint32_t (&x)[kSymOpGroup][DW]) {
-#pragma unroll
-        for (int q = 0; q < kSymOpGroup; ++q)
-            if (g0 + q < end) apply(g0 + q, x[q]);
-    };
-    uint32_t xa[kSymOpGroup][DW], xb[kSymOpGroup][DW];
-    load_group(ch.start, xa);
-    for (uint32_t g0 = ch.start; g0 < end; g0 += 2 * kSymOpGroup) {
-        load_group(g0 + kSymOpGroup, xb);
-        run_group(g0, xa);
-        load_group(g0 + 2 * kSymOpGroup, xa);
-        run_group(g0 + kSymOpGroup, xb);
-    }
-#pragma unroll
-    for (int j = 0; j < DW; ++j) {
-        const uint64_t d = d0 + 64u * j;
-        if (d < nd)
-            reinterpret_cast<uint32_t*>(ch.a)[d] = acc[j];
-        else if (odd && d == nd)
-            reinterpret_cast<uint16_t*>(ch.a)[2 * d] = uint16_t(acc[j]);
-    }
-}
-
-hipError_t launch_symbol_chains(const SymChain* chains, const SymOpRec* ops, uint32_t n_chains, uint64_t nwords,
-                                hipStream_t st, int dw) {
-    if (!n_chains || !nwords) return hipSuccess;
-    const uint64_t nd = nwords / 2 + (nwords & 1);
-    const uint64_t spans = (nd + 64 * uint64_t(dw) - 1) / (64 * uint64_t(dw));
-    if (spans > 0x7FFFFFFFu || n_chains > 65535u) return hipErrorInvalidValue;
-    const dim3 grid(unsigned(spans), n_chains);
-    if (dw == 1)
-        hipLaunchKernelGGL(k_symbol_chains<1>, grid, dim3(64), 0, st, chains, ops, nwords);
-    else if (dw == 2)
-        hipLaunchKernelGGL(k_symbol_chains<2>, grid, dim3(64), 0, st, chains, ops, nwords);
-    else if (dw == 4)
-        hipLaunchKernelGGL(k_symbol_chains<4>, grid, dim3(64), 0, st, chains, ops, nwords);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------ launchers
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff) {
     V1Args v{};

@@ -203,21 +203,6 @@ hipError_t launch_cs16_goff(const int32_t* slots, uint32_t* goff, int n, int64_t
 // 2 a ^= c * b (lc = log c; logt / expt: discrete log and alpha^i tables, i < 65535)
 hipError_t launch_symbol_op(uint16_t* a, const uint16_t* b, int op, uint32_t lc, int64_t nw, const uint16_t* logt,
                             const uint16_t* expt, hipStream_t st);
-// rsg_symbol_ops records: a chain of ops on one target (ops[start, start + count), in order); an op's flags
-// are its kind (0 a ^= b, 1 a = coef a, 2 a ^= coef b) | kSymOpSelf when its source is the chain's target
-struct SymChain {
-    uint8_t* a;
-    uint32_t start, count;
-};
-struct SymOpRec {
-    const uint8_t* b;
-    uint32_t coef, flags;
-};
-constexpr uint32_t kSymOpSelf = 0x100u;
-// dw: dwords per lane (1, 2 or 4), i.e. 256 * dw bytes of a symbol per wave
-hipError_t launch_symbol_chains(const SymChain* chains, const SymOpRec* ops, uint32_t n_chains, uint64_t nwords,
-                                hipStream_t st, int dw);
-
 int apply_tile_rows(int m, int R);
 // V = 1 kernel arguments from an ApplyArgs (nchunks_1k full 1 KiB chunks; boff for the JIT kernel)
 V1Args v1_args(const ApplyArgs& a, int64_t nchunks_1k, const int32_t* boff);

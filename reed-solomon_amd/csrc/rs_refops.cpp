@@ -2,6 +2,7 @@
 // the context-free symbol operations gf_add / gf_mul / gf_madd and the four fft_* transforms, run on
 // the GPU through a pool of engines.
 #include "rs_core.hpp"
+#include "rs_symops.hpp"
 
 using namespace rsamd;
 
@@ -370,6 +371,29 @@ OpStage& op_stage(int device) {
     return *p;
 }
 
+// An rsg_symbol_op_t in the kernel's canonical form (rs_symops.hpp): the reference's special cases folded on
+// the host (gf65536.c:175-181 mul by 0 / 1, :199-205 madd by 0 / 1), a source equal to the target read as a
+// scale (a ^= a is 0, a ^= c a is (1 + c) a), so the device never branches on them per word.
+SymOpRec canonical_op(const rsg_symbol_op_t& o) {
+    const uint32_t c = o.coef;
+    const bool self = o.b == o.a;
+    auto scale = [](uint32_t m) {
+        if (m == 0u) return SymOpRec{nullptr, 0u, kSymZero};
+        return m == 1u ? SymOpRec{nullptr, 1u, kSymNop} : SymOpRec{nullptr, m, kSymScale};
+    };
+    switch (o.op) {
+        case RSG_OP_ADD:
+            return self ? scale(0u) : SymOpRec{static_cast<const uint8_t*>(o.b), 1u, kSymXor};
+        case RSG_OP_MUL:
+            return scale(c);
+        default:  // RSG_OP_MADD
+            if (c == 0u) return SymOpRec{nullptr, 0u, kSymNop};
+            if (self) return scale(c ^ 1u);
+            return c == 1u ? SymOpRec{static_cast<const uint8_t*>(o.b), 1u, kSymXor}
+                           : SymOpRec{static_cast<const uint8_t*>(o.b), c, kSymMadd};
+    }
+}
+
 struct DeviceScope {  // restores the caller's current device
     int prev = -1;
     DeviceScope() { (void)hipGetDevice(&prev); }
@@ -418,7 +442,9 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     HIP_TRY(hipSetDevice(device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t nc = tg.size();
-    const size_t bytes = nc * sizeof(SymChain) + n_ops * sizeof(SymOpRec);
+    const size_t bytes = nc * sizeof(SymChain) + n_ops * sizeof(SymOpRec);  // copied to the device
+    const size_t cbase = (bytes + 63) / 64 * 64;                           // multiply constants after them
+    const size_t dbytes = cbase + symbol_chains_scratch(n_ops);
     OpStage& S = op_stage(device);
     std::lock_guard<std::mutex> lk(S.mu);
     OpSlot& sl = S.slot[S.next];
@@ -426,12 +452,12 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     if (sl.pending) HIP_TRY(hipEventSynchronize(sl.ev));  // the launch that read this slot is done
     sl.pending = false;
     if (!sl.ev) HIP_TRY(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    if (bytes > sl.cap) {
+    if (dbytes > sl.cap) {  // host staging and device copy of one size (the host side never holds constants)
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.d) (void)hipFree(sl.d);
         sl.h = sl.d = nullptr;
         sl.cap = 0;
-        const size_t cap = std::max<size_t>(bytes + bytes / 2, 1 << 20);  // grows by half again: few reallocations
+        const size_t cap = std::max<size_t>(dbytes + dbytes / 2, 1 << 20);  // grows by half again: few reallocations
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sl.h), cap, hipHostMallocDefault));
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.d), cap));
         sl.cap = cap;
@@ -443,15 +469,23 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     for (size_t j = 0; j < order.size(); ++j) {
         const rsg_symbol_op_t& o = ops[order[j].second];
         if (j && order[j].first != order[j - 1].first) ++ci;
-        if (!j || order[j].first != order[j - 1].first) hc[ci] = SymChain{static_cast<uint8_t*>(o.a), uint32_t(j), 0};
+        if (!j || order[j].first != order[j - 1].first)
+            hc[ci] = SymChain{static_cast<uint8_t*>(o.a), uint32_t(j), 0, kChainSplit, 0};
         ++hc[ci].count;
-        const bool src = o.op != RSG_OP_MUL;
-        ho[j] = SymOpRec{static_cast<const uint8_t*>(src ? o.b : nullptr), o.coef,
-                         uint32_t(o.op) | (src && o.b == o.a ? kSymOpSelf : 0u)};
+        ho[j] = canonical_op(o);
+        if (ho[j].kind == kSymScale || ho[j].kind == kSymZero) hc[ci].flags &= ~kChainSplit;  // not a pure sum
     }
+    uint64_t split_ops = 0;
+    uint32_t split_max = 0;
+    for (size_t c = 0; c < nc; ++c)
+        if (hc[c].flags & kChainSplit) {
+            split_ops += hc[c].count;
+            split_max = std::max(split_max, hc[c].count);
+        }
     HIP_TRY(hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st));
     const SymChain* dc = reinterpret_cast<const SymChain*>(sl.d);
     const SymOpRec* dops = reinterpret_cast<const SymOpRec*>(sl.d + nc * sizeof(SymChain));
+    uint32_t* dconsts = reinterpret_cast<uint32_t*>(sl.d + cbase);
     // dwords per lane: the largest of 4 / 2 that still gives >= 4096 waves (4 per SIMD), else 1 (more waves
     // for few or short targets: the chains are bound by load latency); RS_AMD_SYMOP_DW = 1 / 2 / 4 overrides
     static const int dw_env = [] {
@@ -462,9 +496,24 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     const uint64_t nd = nwords / 2 + (nwords & 1);
     auto waves = [&](uint64_t dw) { return uint64_t(nc) * ((nd + 64 * dw - 1) / (64 * dw)); };
     const int dw = dw_env ? dw_env : waves(4) >= 4096 ? 4 : waves(2) >= 4096 ? 2 : 1;
-    hipError_t e = hipSuccess;
+    // waves per chain: while the launch has fewer than 8192 waves and at least half the ops sit in pure-sum
+    // chains, cut those chains into 2, 4, 8 slices (each slice of the longest chain keeping >= 4 ops);
+    // RS_AMD_SYMOP_WAVES = 1..8 (a power of 2) overrides
+    static const int wv_env = [] {
+        const char* e = std::getenv("RS_AMD_SYMOP_WAVES");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
+    }();
+    int wv = 1;
+    if (wv_env) {
+        wv = wv_env;
+    } else if (2 * split_ops >= n_ops) {
+        while (2 * wv <= kSymMaxWaves && waves(uint64_t(dw)) * wv < 8192 && split_max / (2 * wv) >= 4) wv *= 2;
+    }
+    hipError_t e = launch_symop_consts(dops, n_ops, dconsts, st);
     for (size_t c0 = 0; c0 < nc && e == hipSuccess; c0 += 65535)
-        e = launch_symbol_chains(dc + c0, dops, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st, dw);
+        e = launch_symbol_chains(dc + c0, dops, dconsts, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st, dw,
+                                 wv);
     // the slot is reused after this event, whatever happened to the launches
     HIP_TRY(hipEventRecord(sl.ev, st));
     sl.pending = true;

@@ -78,16 +78,29 @@ def disassemble(path):
             return f.read()
     with open(path, "rb") as f:
         elf = f.read(20)
-    obj = path
+    if elf[18:20] == b"\xe0\x00":  # an AMDGPU ELF
+        return subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", path], text=True)
+    # a host library carrying a fat binary: one offload bundle per translation unit with device code
     with tempfile.TemporaryDirectory() as d:
-        if elf[18:20] != b"\xe0\x00":  # not an AMDGPU ELF: a host library carrying a fat binary
-            fb = os.path.join(d, "fatbin.bin")
-            subprocess.check_call(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, fb])
-            obj = os.path.join(d, "dev.co")
+        fb = os.path.join(d, "fatbin.bin")
+        subprocess.check_call(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, fb])
+        with open(fb, "rb") as f:
+            blob = f.read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts, i = [], blob.find(magic)
+        while i >= 0:
+            starts.append(i)
+            i = blob.find(magic, i + 1)
+        texts = []
+        for n, (a, b) in enumerate(zip(starts, starts[1:] + [len(blob)])):
+            part, obj = os.path.join(d, f"b{n}.bin"), os.path.join(d, f"dev{n}.co")
+            with open(part, "wb") as f:
+                f.write(blob[a:b])
             subprocess.check_call([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                                   "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}",
+                                   "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}",
                                    f"--output={obj}"])
-        return subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", obj], text=True)
+            texts.append(subprocess.check_output([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", obj], text=True))
+        return "\n".join(texts)
 
 
 _BRANCH = re.compile(r"^s_(c?branch)")

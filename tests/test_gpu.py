@@ -1697,6 +1697,42 @@ def test_symbol_ops_chains_vs_numpy(S):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("S,lens", [(1024 + 6, [1, 3, 7, 64, 100, 203]), (65536, [150, 149, 37, 5]),
+                                    (9, [40, 2, 77]), (4096, [8, 9, 31, 33, 64, 65])])
+def test_symbol_ops_split_chains_vs_numpy(S, lens):
+    """Few long pure-sum chains (gf_madd / gf_add only, coefficients 0 / 1 / general) make the library cut each
+    chain into slices on several waves of one workgroup (rs_symops.hip, kChainSplit) and XOR the slice sums; two
+    chains with a gf_mul or a self-source op in the middle stay whole on wave 0 of the same launch. Bit-exact
+    against the ops applied one after another."""
+    rng = np.random.default_rng(len(lens) * 1000 + S)
+    n_s = 48
+    n_t = len(lens) + 2
+    P = (S + 15) // 16 * 16
+    host = rng.integers(0, 256, (n_t + n_s, P), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    addr = [dev[i].data_ptr() for i in range(n_t + n_s)]
+    per_target = []
+    for t, n in enumerate(lens + [30, 30]):
+        ops = []
+        for i in range(n):
+            kind = int(rng.choice([rs_amd.OP_ADD, rs_amd.OP_MADD], p=[0.2, 0.8]))
+            coef = int(rng.choice([0, 1, int(rng.integers(2, 65536))], p=[0.05, 0.05, 0.9]))
+            ops.append((kind, addr[t], addr[n_t + int(rng.integers(n_s))], coef))
+        if t == len(lens):  # not a pure sum: a scale in the middle
+            ops[15] = (rs_amd.OP_MUL, addr[t], 0, int(rng.integers(2, 65536)))
+        if t == len(lens) + 1:  # a self-source madd: (1 + c) a
+            ops[10] = (rs_amd.OP_MADD, addr[t], addr[t], int(rng.integers(2, 65536)))
+        per_target.append(ops)
+    ops = [o for i in range(max(map(len, per_target))) for tl in per_target if i < len(tl) for o in [tl[i]]]
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    mem = {addr[i]: host[i].copy() for i in range(n_t + n_s)}
+    _ops_numpy(mem, ops, S)
+    want = np.stack([mem[addr[i]] for i in range(n_t + n_s)])
+    assert np.array_equal(got, want)
+
+
 def test_symbol_ops_back_to_back_calls_and_streams():
     """More calls than staging slots, on two streams, before any synchronisation (each call's op list must
     survive until its kernel read it), then a reference-style evaluator loop Omega = S * Lambda mod x^r as one

@@ -127,7 +127,7 @@ PRODUCTION = ("k_apply_m8_v1ILi0E", "k_apply_m8_v1ILi2E", "k_apply_m8_idxILi0ELi
               "k_bs16E", "k_cs16_goff", "k_plan_m8", "k_plan_syn_m8", "k_plan_reenc_m8", "k_plan16_sums", "k_plan16_fill",
               "k_plan16_ps", "k_plan16_ps_rec", "k_plan16_reenc", "k_plan16_reenc_logs", "k_plan16_reenc_rec",
               "k_symbol_op", "k_gen_info", "k_fingerprint", "k_gather_rows", "k_put_rows", "k_xor_rows",
-              "k_gather_ptrs", "k_scatter_ptrs", "k_symbol_chains")
+              "k_gather_ptrs", "k_scatter_ptrs", "k_symbol_chains", "k_symop_consts")
 
 
 def test_release_build_has_no_ablation_kernels():
