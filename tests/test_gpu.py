@@ -1733,6 +1733,37 @@ def test_symbol_ops_split_chains_vs_numpy(S, lens):
     assert np.array_equal(got, want)
 
 
+def test_symbol_ops_more_chains_than_one_launch():
+    """More targets than one launch's grid takes (65535 chains per launch): the chain launches share one
+    op array and one constants array (k_symop_consts runs once per call over every op), so the later
+    launches' chains index ops and constants past the first launch's. Bit-exact against numpy."""
+    from _util import gf_tables
+    exp, log = gf_tables()
+    S, n_t, n_s = 16, 70001, 8
+    rng = np.random.default_rng(70001)
+    tgt = torch.from_numpy(rng.integers(0, 256, (n_t, S), dtype=np.uint8)).cuda()
+    src = torch.from_numpy(rng.integers(0, 256, (n_s, S), dtype=np.uint8)).cuda()
+    t0 = tgt.cpu().numpy().view("<u2").astype(np.int64)
+    ws = src.cpu().numpy().view("<u2").astype(np.int64)
+    j1, j2 = rng.integers(0, n_s, n_t), rng.integers(0, n_s, n_t)
+    c1, c2 = rng.integers(2, 65536, n_t), rng.integers(0, 65536, n_t)
+    ops = np.zeros(2 * n_t, rs_amd.SYMBOL_OP_DTYPE)
+    ops["a"] = tgt.data_ptr() + np.repeat(np.arange(n_t, dtype=np.uint64), 2) * S
+    ops["op"] = np.tile([rs_amd.OP_MADD, rs_amd.OP_MUL], n_t)
+    ops["b"][0::2] = src.data_ptr() + j1.astype(np.uint64) * S
+    ops["b"][1::2] = src.data_ptr() + j2.astype(np.uint64) * S  # ignored by gf_mul
+    ops["coef"][0::2], ops["coef"][1::2] = c1, c2
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+
+    def mul(c, w):  # c per row, w [n, words]
+        lw = np.where(w != 0, log[w], -1)
+        out = np.where((lw >= 0) & (c[:, None] != 0), exp[(lw + log[c][:, None]) % 65535], 0)
+        return out
+    want = mul(c2, t0 ^ mul(c1, ws[j1]))
+    assert np.array_equal(tgt.cpu().numpy().view("<u2").astype(np.int64), want)
+
+
 def test_symbol_ops_back_to_back_calls_and_streams():
     """More calls than staging slots, on two streams, before any synchronisation (each call's op list must
     survive until its kernel read it), then a reference-style evaluator loop Omega = S * Lambda mod x^r as one
