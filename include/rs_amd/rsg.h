@@ -236,7 +236,7 @@ int rsg_xj_fixed_source(uint16_t k, uint16_t r, int route, int masked, char* buf
  * route does not apply). Host only. */
 int rsg_xj_fixed_precompile(uint16_t k, uint16_t r, int route);
 /* Batched symbol operations: the reference's gf_add / gf_mul / gf_madd (rs/gf65536.h:146-167,
- * src/rs/gf65536.c:155-219) over many symbols in ONE launch, asynchronous on `stream` -- the form a loop of
+ * src/rs/gf65536.c:155-219) over many symbols in ONE call, asynchronous on `stream` -- the form a loop of
  * gf_* calls takes on the GPU (each gf_* call of rs/gf65536.h is one synchronous round trip, ~15 us).
  *   RSG_OP_ADD   a ^= b            RSG_OP_MUL   a = coef * a            RSG_OP_MADD  a ^= coef * b
  * All symbols are `symbol_size` bytes (little-endian GF(2^16) words; an odd last byte is not touched, as

@@ -344,9 +344,11 @@ extern "C" void gf_madd(GF_t* gf, void* a, element_t coef, const void* b, size_t
 
 // ============================================================================ batched symbol ops
 // rsg_symbol_ops (include/rs_amd/rsg.h): many gf_add / gf_mul / gf_madd triples on device-accessible
-// symbols in one launch, asynchronous on the caller's stream. The op list goes to the device through one
-// of kOpSlots page-locked staging slots per device (each reused only after the launch that read it is
-// done: its event), so a call returns as soon as the copy and the kernel are queued.
+// symbols in one call, asynchronous on the caller's stream: the ops sorted into per-target chains and folded
+// into canonical kinds here, then one op-list copy and two kernels (rs_symops.hip: the multiply constants,
+// then the chains). The op list goes to the device through one of kOpSlots page-locked staging slots per
+// device (each reused only after the launches that read it are done: its event), so a call returns as soon as
+// the copy and the kernels are queued.
 namespace rsamd {
 namespace {
 constexpr int kOpSlots = 4;
