@@ -16,6 +16,7 @@ using namespace rsamd;
 #endif
 
 extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t** out) {
+    rsamd::CallerDevice caller_device;
     if (!out) return RS_ERR_INVALID;
     *out = nullptr;
     if (uint32_t(k) + r > kN) return RS_ERR_INVALID;
@@ -43,11 +44,15 @@ extern "C" int rsg_codec_create(int device, uint16_t k, uint16_t r, rsg_codec_t*
     return 0;
 }
 
-extern "C" void rsg_codec_destroy(rsg_codec_t* c) { delete c; }
+extern "C" void rsg_codec_destroy(rsg_codec_t* c) {
+    rsamd::CallerDevice caller_device;
+    delete c;
+}
 
 extern "C" int rsg_codec_subfield(const rsg_codec_t* c) { return c ? (c->m <= 8 ? 8 : 16) : 0; }
 
 extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
+    rsamd::CallerDevice caller_device;
     if (!c || !name) return RS_ERR_INVALID;
     // The release build accepts only knobs that select a parity-tested production path:
     // option-only A/B families, overlap variants and block layouts are diagnostic-build knobs (make diag).
@@ -261,6 +266,7 @@ extern "C" int rsg_set_option(rsg_codec_t* c, const char* name, int64_t value) {
 }
 
 extern "C" int rsg_codec_trim(rsg_codec_t* c) {
+    rsamd::CallerDevice caller_device;
     if (!c) return RS_ERR_INVALID;
     HIP_TRY(hipSetDevice(c->device));
     // the launches that may still read the scratch: the last batch / route call's (scratch_ev), the side
@@ -593,6 +599,7 @@ extern "C" int rsg_last_work(const rsg_codec_t* c, uint64_t* valu, uint64_t* sal
 extern "C" int rsg_encode(rsg_codec_t* c, const void* d_info, uint64_t info_stripe_stride, uint64_t info_symbol_stride,
                           void* d_rep, uint64_t rep_stripe_stride, uint64_t rep_symbol_stride, uint64_t n_stripes,
                           uint64_t symbol_size, void* stream) {
+    rsamd::CallerDevice caller_device;
     if (!c) return RS_ERR_INVALID;
     c->work_valu = c->work_salu = 0;
     return run_plan(c, *c->enc, static_cast<const uint8_t*>(d_info), int64_t(info_stripe_stride),
@@ -632,6 +639,7 @@ int decode_plan(rsg_codec_t* c, const bool* is_erased, uint16_t t, DevPlan** out
 
 extern "C" int rsg_decode(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                           uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, uint16_t t, void* stream) {
+    rsamd::CallerDevice caller_device;
     if (!c || !is_erased) return RS_ERR_INVALID;
     c->work_valu = c->work_salu = 0;
     if (t > c->r) return RS_ERR_CANNOT_RESTORE;
@@ -707,6 +715,7 @@ int host_pipe_reserve(rsg_codec_t* c, size_t bytes) {
 extern "C" int rsg_encode_host(rsg_codec_t* c, const void* h_info, uint64_t info_stripe_stride,
                                uint64_t info_symbol_stride, void* h_rep, uint64_t rep_stripe_stride,
                                uint64_t rep_symbol_stride, uint64_t n_stripes, uint64_t symbol_size) {
+    rsamd::CallerDevice caller_device;
     if (!c || (n_stripes && (!h_info || !h_rep))) return RS_ERR_INVALID;
     const uint64_t S = symbol_size, k = c->k, r = c->r;
     if (S & 1) return RS_ERR_INVALID;
@@ -745,6 +754,7 @@ extern "C" int rsg_encode_host(rsg_codec_t* c, const void* h_info, uint64_t info
 
 extern "C" int rsg_decode_host(rsg_codec_t* c, void* h_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, uint16_t t) {
+    rsamd::CallerDevice caller_device;
     if (!c || !is_erased || (n_stripes && !h_rcv)) return RS_ERR_INVALID;
     if (t > c->r) return RS_ERR_CANNOT_RESTORE;
     const uint64_t S = symbol_size, n = uint64_t(c->k) + c->r;
@@ -802,6 +812,7 @@ extern "C" int rsg_decode_host(rsg_codec_t* c, void* h_rcv, uint64_t stripe_stri
 
 extern "C" int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symbol_stride, uint64_t symbol_size,
                              uint16_t k, uint64_t stripe0, uint64_t n_stripes, uint64_t seed, void* stream) {
+    rsamd::CallerDevice caller_device;
     if (symbol_size % 8 || symbol_stride % 8 || stripe_stride % 8 || uintptr_t(d_base) % 8) return RS_ERR_INVALID;
     if (!n_stripes || !k) return 0;
     HIP_TRY(launch_gen_info(static_cast<uint8_t*>(d_base), int64_t(stripe_stride), int64_t(symbol_stride),
@@ -813,6 +824,7 @@ extern "C" int rsg_fill_info(void* d_base, uint64_t stripe_stride, uint64_t symb
 extern "C" int rsg_fingerprint(const void* d_base, uint64_t stripe_stride, uint64_t symbol_stride,
                                uint64_t symbol_size, uint32_t sym0, uint32_t nsym, uint64_t n_stripes, uint64_t* d_out,
                                void* stream) {
+    rsamd::CallerDevice caller_device;
     if (symbol_size % 8 || symbol_stride % 8 || stripe_stride % 8 || uintptr_t(d_base) % 8) return RS_ERR_INVALID;
     if (!n_stripes) return 0;
     HIP_TRY(launch_fingerprint(static_cast<const uint8_t*>(d_base), int64_t(stripe_stride), int64_t(symbol_stride),

@@ -866,6 +866,7 @@ int decode_batch_m16_ps(rsg_codec_t* c, uint8_t* base, int64_t stripe_stride, in
 
 extern "C" int rsg_decode_batch(rsg_codec_t* c, void* d_rcv, uint64_t stripe_stride, uint64_t symbol_stride,
                                 uint64_t n_stripes, uint64_t symbol_size, const bool* is_erased, void* stream) {
+    rsamd::CallerDevice caller_device;
     if (!c || (!is_erased && n_stripes)) return RS_ERR_INVALID;
     const size_t n = size_t(c->k) + c->r;
     // validate every stripe first (nothing is written when one pattern cannot be restored), then group

@@ -37,6 +37,22 @@ extern "C" {
 
 namespace rsamd {
 
+// Every public entry that selects the codec's device (hipSetDevice) holds one of these: the calling thread's
+// current HIP device is the same after the call as before it, as with the reference's CPU library, so a
+// caller that drives several GPUs (or torch code relying on its current device) is not moved to the codec's.
+struct CallerDevice {
+    int prev = -1;
+    CallerDevice() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~CallerDevice() {
+        int now = -1;
+        if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+    }
+    CallerDevice(const CallerDevice&) = delete;
+    CallerDevice& operator=(const CallerDevice&) = delete;
+};
+
 inline int hip_fail(hipError_t e, const char* what) {
     std::fprintf(stderr, "librs_amd: %s failed: %s\n", what, hipGetErrorString(e));
     return RS_ERR_DEVICE;

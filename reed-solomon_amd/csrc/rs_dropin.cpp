@@ -119,6 +119,7 @@ size_t chunk_width(size_t S, int maxc = kMaxChunks) {
 }  // namespace rsamd
 
 extern "C" RS_t* rs_create(void) {
+    rsamd::CallerDevice caller_device;
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) {
@@ -162,6 +163,7 @@ extern "C" RS_t* rs_create(void) {
 }
 
 extern "C" void rs_destroy(RS_t* rs) {
+    rsamd::CallerDevice caller_device;
     if (!rs) return;
     delete static_cast<Impl*>(rs->impl);
     gf_destroy(rs->gf);
@@ -447,6 +449,7 @@ int restore_even(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool
 // repair symbol first (fft.c:163), _rs_restore_erased each restored one (reed_solomon.c:326). Golden cases
 // odd_* pin both (tests/golden/make_golden.py).
 extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, symbol_seq_t* rep) {
+    rsamd::CallerDevice caller_device;
     if (!rs || !rs->impl || !inf || !rep) return RS_ERR_INVALID;
     const size_t S = inf->symbol_size;
     if (S != rep->symbol_size || inf->length + rep->length > kN) return RS_ERR_INVALID;
@@ -461,6 +464,7 @@ extern "C" int rs_generate_repair_symbols(RS_t* rs, const symbol_seq_t* inf, sym
 
 extern "C" int rs_restore_symbols(RS_t* rs, uint16_t k, uint16_t r, symbol_seq_t* rcv, const bool* is_erased,
                                   uint16_t t) {
+    rsamd::CallerDevice caller_device;
     if (r < t) return RS_ERR_CANNOT_RESTORE;  // checked first, as reference reed_solomon.c:467-470
     if (!rs || !rs->impl || !rcv || !is_erased) return RS_ERR_INVALID;
     const size_t S = rcv->symbol_size, n = size_t(k) + r;

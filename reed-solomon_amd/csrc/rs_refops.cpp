@@ -323,10 +323,12 @@ inline element_t pow_mod(uint64_t a, uint64_t b) { return field().exp[(a * b) % 
 }  // namespace rsamd
 
 extern "C" void gf_add(void* a, const void* b, size_t symbol_size) {
+    rsamd::CallerDevice caller_device;
     if (int rc = symbol_op(0, a, 0, b, symbol_size)) symbol_op_failed("gf_add", rc);
 }
 
 extern "C" void gf_mul(GF_t* gf, void* a, element_t coef, size_t symbol_size) {
+    rsamd::CallerDevice caller_device;
     (void)gf;
     if (coef == 0) {  // reference gf65536.c:175-181
         std::memset(a, 0, symbol_size);
@@ -337,6 +339,7 @@ extern "C" void gf_mul(GF_t* gf, void* a, element_t coef, size_t symbol_size) {
 }
 
 extern "C" void gf_madd(GF_t* gf, void* a, element_t coef, const void* b, size_t symbol_size) {
+    rsamd::CallerDevice caller_device;
     (void)gf;
     if (coef == 0) return;  // reference gf65536.c:199-205
     if (int rc = symbol_op(coef == 1 ? 0 : 2, a, coef, b, symbol_size)) symbol_op_failed("gf_madd", rc);
@@ -396,13 +399,6 @@ SymOpRec canonical_op(const rsg_symbol_op_t& o) {
     }
 }
 
-struct DeviceScope {  // restores the caller's current device
-    int prev = -1;
-    DeviceScope() { (void)hipGetDevice(&prev); }
-    ~DeviceScope() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
 }  // namespace
 
 }  // namespace rsamd
@@ -440,7 +436,7 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     }
     if (tg.empty() || !nwords) return 0;
     if (device < 0) return RS_ERR_INVALID;
-    DeviceScope scope;
+    CallerDevice scope;
     HIP_TRY(hipSetDevice(device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t nc = tg.size();
@@ -533,12 +529,14 @@ static std::vector<uint16_t> dft_matrix(const symbol_seq_t* f, const uint16_t* p
 }
 
 extern "C" void fft_transform(GF_t* gf, const symbol_seq_t* f, const uint16_t* positions, symbol_seq_t* res) {
+    rsamd::CallerDevice caller_device;
     (void)gf;
     if (!f || !res || (!positions && f->length)) symbol_op_failed("fft_transform (bad arguments)", RS_ERR_INVALID);
     if (int rc = transform_apply(dft_matrix(f, positions, res), f, res)) symbol_op_failed("fft_transform", rc);
 }
 
 extern "C" int fft_transform_cycl(GF_t* gf, const symbol_seq_t* f, const uint16_t* positions, symbol_seq_t* res) {
+    rsamd::CallerDevice caller_device;
     (void)gf;
     if (!f || !res || (!positions && f->length)) return RS_ERR_INVALID;
     return transform_apply(dft_matrix(f, positions, res), f, res);
@@ -546,6 +544,7 @@ extern "C" int fft_transform_cycl(GF_t* gf, const symbol_seq_t* f, const uint16_
 
 extern "C" void fft_partial_transform(GF_t* gf, const symbol_seq_t* f, const uint16_t* components,
                                       symbol_seq_t* res) {
+    rsamd::CallerDevice caller_device;
     (void)gf;
     if (!f || !res || (!components && res->length))
         symbol_op_failed("fft_partial_transform (bad arguments)", RS_ERR_INVALID);
@@ -560,6 +559,7 @@ extern "C" void fft_partial_transform(GF_t* gf, const symbol_seq_t* f, const uin
 
 extern "C" int fft_partial_transform_cycl(GF_t* gf, const symbol_seq_t* f, const coset_t* cosets, uint16_t cosets_cnt,
                                           symbol_seq_t* res) {
+    rsamd::CallerDevice caller_device;
     if (!f || !res || (!cosets && cosets_cnt)) return RS_ERR_INVALID;
     const size_t K = f->length, R = res->length;
     size_t total = 0;

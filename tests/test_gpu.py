@@ -335,6 +335,33 @@ def test_errors():
     assert rs.restore_symbols(4, 2, syms[:5], np.zeros(6, bool), 0) == rs_amd.RS_ERR_INVALID  # length != k + r
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (the box has one)")
+def test_calls_keep_the_callers_current_device():
+    """A codec on device 0 called from a thread whose current device is 1 (a host driving several GPUs, or
+    torch code relying on its current device) leaves the thread on device 1: every public entry that selects
+    the codec's device restores the caller's (rs_core.hpp CallerDevice)."""
+    k, r, S, n = 10, 4, 4096, 4
+    torch.cuda.set_device(1)
+    try:
+        dev = torch.zeros((n, k + r, S), dtype=torch.uint8, device="cuda:0")
+        rs_amd.fill_info(dev, k, seed=3)
+        codec = rs_amd.Codec(k, r, device=0)
+        assert torch.cuda.current_device() == 1
+        codec.encode(dev)
+        er = rs_amd.bench_pattern(k, r)
+        codec.decode(dev, er)
+        codec.decode_batch(dev, np.tile(er, (n, 1)))
+        assert torch.cuda.current_device() == 1
+        rs = rs_amd.RS()
+        syms = [np.zeros(64, np.uint8) for _ in range(k + r)]
+        assert rs.generate_repair_symbols(syms[:k], syms[k:]) == 0
+        rs.close()
+        assert torch.cuda.current_device() == 1
+        codec.close()
+    finally:
+        torch.cuda.set_device(0)
+
+
 def test_fingerprint_matches_cpu_port():
     """The device fingerprint used by bench.py's verification == tests/_util.py:fingerprint_np."""
     from _util import fingerprint_np
