@@ -15,10 +15,10 @@ def key(rec):
     return (rec.get("leg"), rec.get("bench_kernel"), rec.get("config"), rec.get("src_hash"))
 
 
-def main(paths):
-    with open(TABLE) as f:
-        table = json.load(f)
-    recs = table["records"]
+def main(paths, table=TABLE):
+    with open(table) as f:
+        doc = json.load(f)
+    recs = doc["records"]
     added = replaced = 0
     for p in paths:
         with open(p) as f:
@@ -30,10 +30,10 @@ def main(paths):
             replaced += bool(old)
             added += not old
             recs.append(rec)
-    with open(TABLE, "w") as f:
-        json.dump(table, f, indent=1)
+    with open(table, "w") as f:
+        json.dump(doc, f, indent=1)
         f.write("\n")
-    print(f"{TABLE}: {added} added, {replaced} replaced, {len(recs)} records")
+    print(f"{table}: {added} added, {replaced} replaced, {len(recs)} records")
 
 
 if __name__ == "__main__":

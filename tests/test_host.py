@@ -527,3 +527,33 @@ def test_traffic_composite_legs_and_component_split(tmp_path):
     assert [t for t, _ in out["encode"]] == [110.0, 122.0]
     assert [t for t, _ in out["decode"]] == [321.0, 330.0]
     assert out["decode"][0][1] == {"cs16t": 290.0, "bs16": 31.0}
+
+
+def test_traffic_merge_replaces_by_key_and_bench_finds_the_record(tmp_path):
+    """scripts/traffic_merge.py folds a traffic.py run into the PMC table: a record with the same (leg, kernel,
+    config, source hash) replaces the old one, others are kept; bench.measured_traffic then reads it for a
+    JIT kernel name (content-addressed, no source-hash check)."""
+    import importlib.util
+    import json
+
+    def load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    tm = load("traffic_merge", os.path.join(REPO, "scripts", "traffic_merge.py"))
+    rec = lambda leg, b, h="h0": {"leg": leg, "bench_kernel": "rs_xj[4x10:abc]", "config": "k10_r4_S4096_n1024_t4",
+                                   "src_hash": h, "traffic_bytes": b}
+    table = tmp_path / "traffic.json"
+    table.write_text(json.dumps({"records": [rec("encode", 1), rec("decode", 2)]}))
+    run = tmp_path / "run.json"
+    run.write_text(json.dumps({"records": [rec("encode", 10), rec("encode", 30, "h1")]}))
+    tm.main([str(run)], table=str(table))
+    recs = json.loads(table.read_text())["records"]
+    assert sorted((r["leg"], r["src_hash"], r["traffic_bytes"]) for r in recs) == \
+        [("decode", "h0", 2), ("encode", "h0", 10), ("encode", "h1", 30)]
+    bench = load("bench_for_traffic", os.path.join(REPO, "bench.py"))
+    bench.TRAFFIC_JSON = str(table)
+    assert bench.measured_traffic("rs_xj[4x10:abc]", "k10_r4_S4096_n1024_t4", leg="encode") == 30  # newest wins
+    assert bench.measured_traffic("rs_xj[4x10:abc]", "k10_r4_S4096_n1024_t4", leg="decode") == 2
+    assert bench.measured_traffic("rs_xj[4x10:abc]", "k10_r4_S4096_n1024_t1", leg="decode") is None
