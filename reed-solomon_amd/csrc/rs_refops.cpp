@@ -411,18 +411,32 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     // chains: the ops of each target in array order = the (target, index) pairs sorted; every pointer 4-byte
     // aligned (dword kernel)
     std::vector<std::pair<uintptr_t, uint32_t>> order(n_ops);
+    std::vector<uint8_t> scaling(n_ops);  // the op scales its target (canonical kSymScale / kSymZero)
     for (uint64_t i = 0; i < n_ops; ++i) {
         const rsg_symbol_op_t& o = ops[i];
         if (o.op > RSG_OP_MADD || !o.a || (uintptr_t(o.a) & 3)) return RS_ERR_INVALID;
         if (o.op != RSG_OP_MUL && (!o.b || (uintptr_t(o.b) & 3))) return RS_ERR_INVALID;
         order[i] = {uintptr_t(o.a), uint32_t(i)};
+        const bool self = o.op != RSG_OP_MUL && o.b == o.a && !(o.op == RSG_OP_MADD && o.coef == 0);  // (1 + c) a
+        scaling[i] = (o.op == RSG_OP_MUL && o.coef != 1) || self;
     }
     std::sort(order.begin(), order.end());
-    // distinct targets (ascending): they must not overlap each other, and no op may read another op's target
-    // (the chains run side by side): both rejected, nothing is queued
+    // distinct targets (ascending), each chain's length and whether it scales its target (known before any
+    // record is written: the slice count decides how many combine records those chains need). Targets must not
+    // overlap each other, and no op may read another op's target (the chains run side by side): both rejected,
+    // nothing is queued
     std::vector<uintptr_t> tg;
-    for (size_t j = 0; j < order.size(); ++j)
-        if (!j || order[j].first != order[j - 1].first) tg.push_back(order[j].first);
+    std::vector<uint32_t> cnt;
+    std::vector<uint8_t> scales;
+    for (size_t j = 0; j < order.size(); ++j) {
+        if (!j || order[j].first != order[j - 1].first) {
+            tg.push_back(order[j].first);
+            cnt.push_back(0);
+            scales.push_back(0);
+        }
+        ++cnt.back();
+        scales.back() |= scaling[order[j].second];
+    }
     for (size_t i = 1; i < tg.size(); ++i)
         if (tg[i - 1] + span > tg[i]) return RS_ERR_INVALID;
     if (span) {
@@ -440,9 +454,35 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
     HIP_TRY(hipSetDevice(device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t nc = tg.size();
-    const size_t bytes = nc * sizeof(SymChain) + n_ops * sizeof(SymOpRec);  // copied to the device
+    const uint32_t cnt_max = *std::max_element(cnt.begin(), cnt.end());
+    const size_t n_scaling = size_t(std::count(scales.begin(), scales.end(), uint8_t(1)));
+    // dwords per lane: the largest of 4 / 2 that still gives >= 4096 waves (4 per SIMD), else 1 (more waves
+    // for few or short targets: the chains are bound by load latency); RS_AMD_SYMOP_DW = 1 / 2 / 4 overrides
+    static const int dw_env = [] {
+        const char* e = std::getenv("RS_AMD_SYMOP_DW");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    const uint64_t nd = nwords / 2 + (nwords & 1);
+    auto waves = [&](uint64_t dw) { return uint64_t(nc) * ((nd + 64 * dw - 1) / (64 * dw)); };
+    const int dw = dw_env ? dw_env : waves(4) >= 4096 ? 4 : waves(2) >= 4096 ? 2 : 1;
+    // waves per chain: while the launch has fewer than 8192 waves, cut the chains into 2, 4, 8 slices (each
+    // slice of the longest chain keeping >= 4 ops); RS_AMD_SYMOP_WAVES = 1..8 (a power of 2) overrides
+    static const int wv_env = [] {
+        const char* e = std::getenv("RS_AMD_SYMOP_WAVES");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
+    }();
+    int wv = 1;
+    if (wv_env)
+        wv = wv_env;
+    else
+        while (2 * wv <= kSymMaxWaves && waves(uint64_t(dw)) * wv < 8192 && cnt_max / (2 * wv) >= 4) wv *= 2;
+    if (wv > 1 && n_ops + uint64_t(wv) * n_scaling > 0xFFFFFFFFull) wv = 1;  // combine records past 32-bit ids
+    const uint64_t n_rec = n_ops + (wv > 1 ? uint64_t(wv) * n_scaling : 0);  // ops + combine records
+    const size_t bytes = nc * sizeof(SymChain) + n_rec * sizeof(SymOpRec);  // copied to the device
     const size_t cbase = (bytes + 63) / 64 * 64;                           // multiply constants after them
-    const size_t dbytes = cbase + symbol_chains_scratch(n_ops);
+    const size_t dbytes = cbase + symbol_chains_scratch(n_rec);
     OpStage& S = op_stage(device);
     std::lock_guard<std::mutex> lk(S.mu);
     OpSlot& sl = S.slot[S.next];
@@ -460,55 +500,54 @@ extern "C" int rsg_symbol_ops(int device, const rsg_symbol_op_t* ops, uint64_t n
         HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sl.d), cap));
         sl.cap = cap;
     }
-    // records straight into the page-locked slot: chains, then the ops in chain order
+    // records straight into the page-locked slot: chains, the ops in chain order, the combine records
     SymChain* hc = reinterpret_cast<SymChain*>(sl.h);
     SymOpRec* ho = reinterpret_cast<SymOpRec*>(sl.h + nc * sizeof(SymChain));
-    size_t ci = 0;
-    for (size_t j = 0; j < order.size(); ++j) {
+    for (size_t j = 0, ci = 0; j < order.size(); ++j) {
         const rsg_symbol_op_t& o = ops[order[j].second];
         if (j && order[j].first != order[j - 1].first) ++ci;
         if (!j || order[j].first != order[j - 1].first)
-            hc[ci] = SymChain{static_cast<uint8_t*>(o.a), uint32_t(j), 0, kChainSplit, 0};
-        ++hc[ci].count;
+            hc[ci] = SymChain{static_cast<uint8_t*>(o.a), uint32_t(j), cnt[ci],
+                              kChainSplit | (scales[ci] && wv > 1 ? kChainAffine : 0u), 0};
         ho[j] = canonical_op(o);
-        if (ho[j].kind == kSymScale || ho[j].kind == kSymZero) hc[ci].flags &= ~kChainSplit;  // not a pure sum
     }
-    uint64_t split_ops = 0;
-    uint32_t split_max = 0;
-    for (size_t c = 0; c < nc; ++c)
-        if (hc[c].flags & kChainSplit) {
-            split_ops += hc[c].count;
-            split_max = std::max(split_max, hc[c].count);
+    if (wv > 1 && n_scaling) {
+        // slice w of a chain = ops [w len, (w + 1) len) as the kernel cuts it; its result is multiplied by
+        // S_w = M_(w+1) ... M_(W-1), M_l = the product of slice l's scale factors (0 if it zeroes the target)
+        const Field& F = field();
+        uint64_t comb = n_ops;
+        for (size_t c = 0; c < nc; ++c) {
+            if (!scales[c]) continue;
+            hc[c].comb = uint32_t(comb);
+            const uint32_t len = (hc[c].count + uint32_t(wv) - 1) / uint32_t(wv);
+            uint16_t M[kSymMaxWaves];
+            for (int w = 0; w < wv; ++w) {
+                M[w] = 1;
+                const uint32_t e0 = std::min(uint32_t(w) * len, hc[c].count);
+                const uint32_t e1 = std::min((uint32_t(w) + 1) * len, hc[c].count);
+                for (uint32_t i = e0; i < e1; ++i) {
+                    const SymOpRec& r = ho[hc[c].start + i];
+                    if (r.kind == kSymZero)
+                        M[w] = 0;
+                    else if (r.kind == kSymScale)
+                        M[w] = F.mul(M[w], uint16_t(r.coef));
+                }
+            }
+            uint16_t after = 1;
+            for (int w = wv - 1; w >= 0; --w) {
+                ho[comb + uint64_t(w)] = after == 0   ? SymOpRec{nullptr, 0u, kSymZero}
+                                         : after == 1 ? SymOpRec{nullptr, 1u, kSymNop}
+                                                      : SymOpRec{nullptr, after, kSymScale};
+                after = F.mul(after, M[w]);
+            }
+            comb += uint64_t(wv);
         }
+    }
     HIP_TRY(hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st));
     const SymChain* dc = reinterpret_cast<const SymChain*>(sl.d);
     const SymOpRec* dops = reinterpret_cast<const SymOpRec*>(sl.d + nc * sizeof(SymChain));
     uint32_t* dconsts = reinterpret_cast<uint32_t*>(sl.d + cbase);
-    // dwords per lane: the largest of 4 / 2 that still gives >= 4096 waves (4 per SIMD), else 1 (more waves
-    // for few or short targets: the chains are bound by load latency); RS_AMD_SYMOP_DW = 1 / 2 / 4 overrides
-    static const int dw_env = [] {
-        const char* e = std::getenv("RS_AMD_SYMOP_DW");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 1 || v == 2 || v == 4 ? v : 0;
-    }();
-    const uint64_t nd = nwords / 2 + (nwords & 1);
-    auto waves = [&](uint64_t dw) { return uint64_t(nc) * ((nd + 64 * dw - 1) / (64 * dw)); };
-    const int dw = dw_env ? dw_env : waves(4) >= 4096 ? 4 : waves(2) >= 4096 ? 2 : 1;
-    // waves per chain: while the launch has fewer than 8192 waves and at least half the ops sit in pure-sum
-    // chains, cut those chains into 2, 4, 8 slices (each slice of the longest chain keeping >= 4 ops);
-    // RS_AMD_SYMOP_WAVES = 1..8 (a power of 2) overrides
-    static const int wv_env = [] {
-        const char* e = std::getenv("RS_AMD_SYMOP_WAVES");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
-    }();
-    int wv = 1;
-    if (wv_env) {
-        wv = wv_env;
-    } else if (2 * split_ops >= n_ops) {
-        while (2 * wv <= kSymMaxWaves && waves(uint64_t(dw)) * wv < 8192 && split_max / (2 * wv) >= 4) wv *= 2;
-    }
-    hipError_t e = launch_symop_consts(dops, n_ops, dconsts, st);
+    hipError_t e = launch_symop_consts(dops, n_rec, dconsts, st);
     for (size_t c0 = 0; c0 < nc && e == hipSuccess; c0 += 65535)
         e = launch_symbol_chains(dc + c0, dops, dconsts, uint32_t(std::min<size_t>(65535, nc - c0)), nwords, st, dw,
                                  wv);

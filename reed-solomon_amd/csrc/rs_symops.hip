@@ -6,9 +6,10 @@
 // k_symbol_chains then takes one workgroup of W waves per (256 * DW byte column span, chain): the target's DW
 // dwords per lane stay in registers across the chain, every op reads its source once (sources are loaded a
 // group of ops ahead of their use), the constants arrive by one scalar load per op, and the target is written
-// once. A chain that only accumulates (kChainSplit) is cut into W slices of consecutive ops, one per wave, each
-// summed from zero (wave 0 from the target), and the W sums are XORed through LDS: the latency of a long chain
-// is paid W times in parallel instead of once in series. Other chains run on wave 0 alone.
+// once. With W waves per workgroup a chain is cut into W slices of consecutive ops, one per wave, each applied
+// from zero (wave 0 from the target); a chain that scales its target multiplies each slice's result by the
+// product of the later slices' scale factors (records the host appends, rs_symops.hpp); the W results are XORed
+// through LDS: the latency of a long chain is paid W times in parallel instead of once in series.
 // c * x on two packed words is bit-sliced: XOR over the bits i of x of c alpha^i, the lane mask of bit i in
 // each 16-bit half being the half's sign after a packed shift left by 15 - i -- three VALU per bit and dword
 // (packed shift, packed arithmetic shift, one v_bitop3 for the masked XOR).
@@ -133,6 +134,19 @@ __global__ void __launch_bounds__(64 * kSymMaxWaves) k_symbol_chains(const SymCh
         run_group(g0, xa);
         load_group(g0 + 2 * kSymOpGroup, xa);
         run_group(g0 + kSymOpGroup, xb);
+    }
+    if (split && (ch.flags & kChainAffine)) {  // times the scale factors of the slices after this one
+        const uint32_t o = ch.comb + w, kind = ops[o].kind;
+        if (kind == kSymScale) {
+            uint32_t K[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) K[i] = consts[16u * o + i];
+#pragma unroll
+            for (int j = 0; j < DW; ++j) acc[j] = madd_packed(0u, acc[j], K);
+        } else if (kind == kSymZero) {
+#pragma unroll
+            for (int j = 0; j < DW; ++j) acc[j] = 0u;
+        }
     }
     if (nw > 1) {  // every wave reaches the barrier (uniform per workgroup: nw, split)
         if (split && w) {

@@ -13,14 +13,17 @@ namespace rsamd {
 //   kSymZero  a = 0                (gf_mul by 0, a ^= a)       kSymNop   nothing (gf_mul by 1, madd by 0)
 enum : uint32_t { kSymNop = 0, kSymXor = 1, kSymMadd = 2, kSymScale = 3, kSymZero = 4 };
 
-// a chain: the ops of one target, ops[start, start + count) in order; kChainSplit: the chain only accumulates
-// (no kSymScale / kSymZero), so its ops may run as W slices on W waves whose results are XORed
+// a chain: the ops of one target, ops[start, start + count) in order. kChainSplit: its ops may run as W slices of
+// consecutive ops on W waves (wave 0 from the target, the others from zero) whose results are XORed. Every op is
+// affine in the target (a = m a + b), so that is exact once each slice's result is multiplied by the product of
+// the scale factors of the slices after it; kChainAffine: the chain scales (kSymScale / kSymZero ops) and those
+// W products are the records ops[comb + w] (kinds kSymScale / kSymZero / kSymNop), else they are all 1.
 struct SymChain {
     uint8_t* a;
     uint32_t start, count;
-    uint32_t flags, pad;
+    uint32_t flags, comb;
 };
-constexpr uint32_t kChainSplit = 1u;
+constexpr uint32_t kChainSplit = 1u, kChainAffine = 2u;
 constexpr int kSymMaxWaves = 8;  // waves per chain (workgroup size / 64)
 struct SymOpRec {
     const uint8_t* b;  // source (kSymXor / kSymMadd), else null

@@ -1727,10 +1727,10 @@ def test_symbol_ops_chains_vs_numpy(S):
 @pytest.mark.parametrize("S,lens", [(1024 + 6, [1, 3, 7, 64, 100, 203]), (65536, [150, 149, 37, 5]),
                                     (9, [40, 2, 77]), (4096, [8, 9, 31, 33, 64, 65])])
 def test_symbol_ops_split_chains_vs_numpy(S, lens):
-    """Few long pure-sum chains (gf_madd / gf_add only, coefficients 0 / 1 / general) make the library cut each
-    chain into slices on several waves of one workgroup (rs_symops.hip, kChainSplit) and XOR the slice sums; two
-    chains with a gf_mul or a self-source op in the middle stay whole on wave 0 of the same launch. Bit-exact
-    against the ops applied one after another."""
+    """Few long chains (gf_madd / gf_add, coefficients 0 / 1 / general) make the library cut each chain into
+    slices on several waves of one workgroup (rs_symops.hip) and XOR the slice results; the two chains with a
+    gf_mul or a self-source op in the middle (the target scaled) multiply each slice's result by the later
+    slices' scale factors first (kChainAffine). Bit-exact against the ops applied one after another."""
     rng = np.random.default_rng(len(lens) * 1000 + S)
     n_s = 48
     n_t = len(lens) + 2
@@ -1751,6 +1751,43 @@ def test_symbol_ops_split_chains_vs_numpy(S, lens):
             ops[10] = (rs_amd.OP_MADD, addr[t], addr[t], int(rng.integers(2, 65536)))
         per_target.append(ops)
     ops = [o for i in range(max(map(len, per_target))) for tl in per_target if i < len(tl) for o in [tl[i]]]
+    rs_amd.symbol_ops(ops, S)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy()
+    mem = {addr[i]: host[i].copy() for i in range(n_t + n_s)}
+    _ops_numpy(mem, ops, S)
+    want = np.stack([mem[addr[i]] for i in range(n_t + n_s)])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("S", [1024 + 6, 4096, 9])
+def test_symbol_ops_split_scaling_chains(S):
+    """Split chains that scale their target at chosen places: a gf_mul first and last, gf_mul by 0 and by 1,
+    a self gf_add (zeroes the target) and self gf_madds ((1 + c) a, incl. c = 1) at slice starts, ends and
+    middles, chains of every length 1 .. 64 so every slice count and ragged last slice occurs. Each slice's result
+    times the later slices' scale factors, XORed: bit-exact against the ops applied one after another."""
+    rng = np.random.default_rng(S + 5)
+    n_s = 16
+    lens = list(range(1, 65, 3))
+    n_t = len(lens)
+    P = (S + 15) // 16 * 16
+    host = rng.integers(0, 256, (n_t + n_s, P), dtype=np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    addr = [dev[i].data_ptr() for i in range(n_t + n_s)]
+    special = [lambda t: (rs_amd.OP_MUL, addr[t], 0, int(rng.integers(2, 65536))),
+               lambda t: (rs_amd.OP_MUL, addr[t], 0, 0), lambda t: (rs_amd.OP_MUL, addr[t], 0, 1),
+               lambda t: (rs_amd.OP_ADD, addr[t], addr[t], 0),
+               lambda t: (rs_amd.OP_MADD, addr[t], addr[t], int(rng.integers(2, 65536))),
+               lambda t: (rs_amd.OP_MADD, addr[t], addr[t], 1)]
+    per_target = []
+    for t, n in enumerate(lens):
+        ops = [(rs_amd.OP_MADD, addr[t], addr[n_t + int(rng.integers(n_s))], int(rng.integers(1, 65536)))
+               for _ in range(n)]
+        for pos in {0, n - 1, n // 2, n // 3, (2 * n) // 3}:
+            if rng.random() < 0.8:
+                ops[pos] = special[int(rng.integers(len(special)))](t)
+        per_target.append(ops)
+    ops = [o for i in range(max(lens)) for tl in per_target if i < len(tl) for o in [tl[i]]]
     rs_amd.symbol_ops(ops, S)
     torch.cuda.synchronize()
     got = dev.cpu().numpy()
